@@ -1,0 +1,148 @@
+"""numpy restatement of the three hot-path kernels the reference specifies only
+in prose — TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).
+
+Semantic sources (no reference code exists for these):
+  VQ argmin        pseudocode.txt:11-18 (quantize / straight-through / commit
+                   + codebook MSE); hard-regime argmax backtesting.py:154-155.
+  forward-backward math.md:23-67 (pi, row-stochastic A_t conditioned on u_t);
+                   tables from Prior.forward VQ_VAE_HMM_fixed.py:59-71 with
+                   log_A[:, t] = transition t-1 -> t (:125-127; t=0 unused).
+  Viterbi          same tables, max-plus instead of log-sum-exp.
+
+Exact contracts (the HIP kernels follow them operation for operation):
+  vq_argmin  dist[n,k] = fmaf chain over d = 0..Dv-1 of (z[n,d]-c[k,d])^2
+             starting from +0.0f; idx = first k with the smallest dist.
+             (fmaf is emulated exactly here via the C oracle; the pure-numpy
+             `vq_argmin_np` uses float64 and is only used for KATs.)
+  viterbi    d0[j] = log_pi[j] + e[0,j];
+             d_t[j] = (max_i (d_{t-1}[i] + log_A[t,i,j])) + e[t,j]   (fp32,
+             i ascending, strict '>' so ties keep the lowest i);
+             last = first argmax_j d_{L-1}[j]; path[t >= L] = -1;
+             score = d_{L-1}[last]; L = 0 -> path all -1, score = -inf.
+  fwd-bwd    log-space alpha/beta; gamma_t = softmax(alpha_t + beta_t) for
+             t < L, 0 beyond; logZ = LSE_j alpha_{L-1}[j]  (fp64 reference).
+"""
+import itertools
+
+import numpy as np
+
+
+# ----------------------------------------------------------------- VQ argmin
+def vq_argmin_np(z, codebook):
+    """z (B,Dv,T), codebook (K,Dv) -> idx (B,T) int32 (float64 distances; KAT use)."""
+    z = np.asarray(z, np.float64)
+    c = np.asarray(codebook, np.float64)
+    d = ((z[:, None, :, :] - c[None, :, :, None]) ** 2).sum(axis=2)  # (B,K,T)
+    return d.argmin(axis=1).astype(np.int32), d.min(axis=1)
+
+
+# ------------------------------------------------------------------- Viterbi
+def viterbi_f32(log_pi, log_A, em, lengths):
+    """fp32 max-plus Viterbi with the exact op order of the contract above.
+
+    log_pi (K,), log_A (B,T,K,K), em (B,T,K), lengths (B,) -> path (B,T) int32, score (B,) f32
+    """
+    log_pi = np.asarray(log_pi, np.float32)
+    log_A = np.asarray(log_A, np.float32)
+    em = np.asarray(em, np.float32)
+    B, T, K = em.shape
+    L = np.minimum(np.asarray(lengths, np.int64), T)
+    path = np.full((B, T), -1, np.int32)
+    score = np.full(B, -np.inf, np.float32)
+    if T == 0:
+        return path, score
+    bp = np.zeros((B, T, K), np.int8)
+    delta = (log_pi[None, :] + em[:, 0, :]).astype(np.float32)
+    hist = [delta.copy()]
+    for t in range(1, T):
+        best = delta[:, 0, None] + log_A[:, t, 0, :]         # (B,K) fp32
+        arg = np.zeros((B, K), np.int8)
+        for i in range(1, K):
+            v = delta[:, i, None] + log_A[:, t, i, :]
+            gt = v > best
+            best = np.where(gt, v, best)
+            arg = np.where(gt, np.int8(i), arg)
+        nd = (best + em[:, t, :]).astype(np.float32)
+        live = (t < L)[:, None]
+        delta = np.where(live, nd, delta)
+        bp[:, t] = arg
+        hist.append(delta.copy())
+    for b in range(B):
+        n = int(L[b])
+        if n <= 0:
+            continue
+        dl = hist[n - 1][b]
+        s = int(np.argmax(dl))  # first maximum
+        score[b] = dl[s]
+        path[b, n - 1] = s
+        for t in range(n - 1, 0, -1):
+            s = int(bp[b, t, s])
+            path[b, t - 1] = s
+    return path, score
+
+
+# ---------------------------------------------------------- forward-backward
+def _lse(a, axis):
+    m = np.max(a, axis=axis, keepdims=True)
+    m = np.where(np.isfinite(m), m, 0.0)
+    return (m + np.log(np.sum(np.exp(a - m), axis=axis, keepdims=True))).squeeze(axis)
+
+
+def forward_backward_f64(log_pi, log_A, em, lengths):
+    """fp64 log-space alpha/beta.  Returns gamma (B,T,K) f64, logZ (B,) f64."""
+    log_pi = np.asarray(log_pi, np.float64)
+    log_A = np.asarray(log_A, np.float64)
+    em = np.asarray(em, np.float64)
+    B, T, K = em.shape
+    L = np.minimum(np.asarray(lengths, np.int64), T)
+    alpha = np.zeros((B, T, K))
+    beta = np.zeros((B, T, K))
+    alpha[:, 0] = log_pi[None] + em[:, 0]
+    for t in range(1, T):
+        alpha[:, t] = _lse(alpha[:, t - 1, :, None] + log_A[:, t], axis=1) + em[:, t]
+    for t in range(T - 2, -1, -1):
+        nxt = beta[:, t + 1] + em[:, t + 1]                       # (B,K) over j
+        cand = _lse(log_A[:, t + 1] + nxt[:, None, :], axis=2)     # (B,K) over i
+        live = (t + 1 < L)[:, None]
+        beta[:, t] = np.where(live, cand, 0.0)
+    logZ = np.full(B, np.nan)
+    gamma = np.zeros((B, T, K))
+    for b in range(B):
+        n = int(L[b])
+        if n <= 0:
+            continue
+        logZ[b] = _lse(alpha[b, n - 1], axis=0)
+        g = alpha[b, :n] + beta[b, :n] - logZ[b]
+        gamma[b, :n] = np.exp(g)
+    return gamma, logZ
+
+
+# ------------------------------------------------------ brute-force pinning
+def brute_force(log_pi, log_A, em, length):
+    """Enumerate all K^L paths of ONE sequence (small K, L only).
+
+    Returns (logZ, gamma (L,K), best_path tuple, best_score) in float64.
+    The MAP path is the lexicographically-first among exact-score ties.
+    """
+    log_pi = np.asarray(log_pi, np.float64)
+    log_A = np.asarray(log_A, np.float64)
+    em = np.asarray(em, np.float64)
+    K = em.shape[-1]
+    L = int(length)
+    scores, paths = [], []
+    for z in itertools.product(range(K), repeat=L):
+        s = log_pi[z[0]] + em[0, z[0]]
+        for t in range(1, L):
+            s += log_A[t, z[t - 1], z[t]] + em[t, z[t]]
+        scores.append(s)
+        paths.append(z)
+    scores = np.array(scores)
+    m = scores.max()
+    logZ = m + np.log(np.exp(scores - m).sum())
+    w = np.exp(scores - logZ)
+    gamma = np.zeros((L, K))
+    for wi, z in zip(w, paths):
+        for t in range(L):
+            gamma[t, z[t]] += wi
+    bi = int(np.argmax(scores))
+    return logZ, gamma, paths[bi], scores[bi]
