@@ -1,0 +1,75 @@
+/* vqhmm — C-ABI of the MI355X-native VAE_HMM hot path (libvqhmm.so, gfx950).
+ *
+ * The reference (yashnaray/VQ-VAE-HMM-model) is pure Python/PyTorch and exposes
+ * no FFI: its boundary is the nn.Module surface of VQ_VAE_HMM_fixed.py.  Each
+ * entry point below replaces the ATen work behind one piece of that surface
+ * (citations per function).  The Python package `vqhmm` binds these with
+ * ctypes (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *  - Every pointer is a DEVICE pointer (allocated by the caller, e.g. the
+ *    PyTorch caching allocator) unless documented otherwise; the library never
+ *    allocates, frees or synchronises.  Scratch memory is a caller-provided
+ *    workspace whose size comes from the matching *_workspace_size query.
+ *  - Work is enqueued on `stream` (a hipStream_t; NULL = default stream) and
+ *    is asynchronous; kernel faults surface at the caller's next sync.
+ *  - Return value: 0 on success, negative VQHMM_E* code on bad arguments or a
+ *    failed launch.  No global mutable state: calls are reentrant from any
+ *    host thread with its own stream, and graph-capturable.
+ *  - Tensors are dense row-major in the reference's layouts: "CF" = (B, C, T)
+ *    channels-first as nn.Conv1d uses; log_A is (B, T, K, K) with index t the
+ *    transition t-1 -> t (VQ_VAE_HMM_fixed.py:69,125-127).
+ *  - fp32 throughout (the reference computes in fp32).
+ */
+#ifndef VQHMM_H
+#define VQHMM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VQHMM_OK 0
+#define VQHMM_EINVAL -1
+#define VQHMM_ELAUNCH -2
+#define VQHMM_EWORKSPACE -3
+#define VQHMM_EUNSUPPORTED -4
+
+/* Number of parameter tensors of a VAE_HMM, in nn.Module.parameters() order
+ * (VQ_VAE_HMM_fixed.py:92-98 -> encoder :32-36, prior :44-57, decoder :74-79). */
+#define VQHMM_NPARAMS 18
+
+/* Constructor arguments of VAE_HMM(input_dim, hidden_dim, K, hidden_dim2,
+ * u_dim, trans_hidden)  (VQ_VAE_HMM_fixed.py:93). */
+typedef struct vqhmm_dims {
+  int32_t input_dim;    /* D  */
+  int32_t hidden_dim;   /* H  (encoder conv1, decoder embedding + convs) */
+  int32_t K;            /* number of regimes */
+  int32_t hidden_dim2;  /* H2 (encoder conv2) */
+  int32_t u_dim;        /* U  */
+  int32_t trans_hidden; /* TH */
+} vqhmm_dims_t;
+
+/* Library ABI version (bumped on any signature change). */
+int32_t vqhmm_abi_version(void);
+
+/* Element offsets of the 18 parameters inside one flat fp32 buffer laid out
+ * in parameters() order; offsets[18] = total element count.  Host-only. */
+int vqhmm_param_layout(const vqhmm_dims_t* dims, int64_t offsets[VQHMM_NPARAMS + 1]);
+
+/* ---------------------------------------------------------------- VQ ----
+ * Nearest-codeword quantization (semantics pseudocode.txt:11
+ * `quantize`, hard regimes backtesting.py:154-155 — no reference code).
+ * z (B, Dv, T) CF, codebook (K, Dv) -> idx (B, T) int32, dmin (B, T) fp32
+ * (nullable).  dist_k = fmaf chain over d ascending of (z_d - c_kd)^2 from
+ * +0.0f; ties -> lowest k.  Bit-exact vs oracle/c/hmm_oracle.c. */
+int vqhmm_vq_argmin_f32(const float* z, int64_t B, int64_t Dv, int64_t T,
+                        const float* codebook, int64_t K,
+                        int32_t* idx, float* dmin, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VQHMM_H */

@@ -1,0 +1,60 @@
+"""CPU checks of the C-ABI boundary: libvqhmm.so loads without a GPU and
+exports every function include/vqhmm.h declares (no compute calls here)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "vqhmm.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(vqhmm_\w+)\s*\(", src)))
+
+
+def test_header_declares_functions():
+    names = declared_functions()
+    assert "vqhmm_vq_argmin_f32" in names and len(names) >= 3
+
+
+def test_library_exports_every_declared_symbol():
+    from vqhmm import _ext
+    lib = _ext.load()
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+    # and the ctypes signature table covers the header exactly
+    assert sorted(_ext.exported_symbols()) == declared_functions()
+
+
+def test_param_layout_matches_reference_shapes():
+    from oracle import ref_model as RM
+    from vqhmm import _ext
+    lib = _ext.load()
+    d = _ext.Dims(5, 64, 3, 32, 4, 128)
+    off = (ctypes.c_int64 * 19)()
+    assert lib.vqhmm_param_layout(ctypes.byref(d), off) == 0
+    shapes = RM.param_shapes(5, 64, 3, 32, 4, 128)
+    import math
+    sizes = [math.prod(shapes[n]) for n in RM.PARAM_ORDER]
+    assert [off[i + 1] - off[i] for i in range(18)] == sizes
+    assert off[18] == 34649  # 34,649 params at cfg2
+
+
+def test_invalid_args_rejected_without_gpu():
+    from vqhmm import _ext
+    lib = _ext.load()
+    # null pointers with a non-empty problem are rejected before any launch
+    rc = lib.vqhmm_vq_argmin_f32(None, 2, 4, 8, None, 3, None, None, None)
+    assert rc == -1
+
+
+def test_cpu_tensors_fail_loudly():
+    import torch
+    import vqhmm
+    with pytest.raises(RuntimeError, match="HIP"):
+        vqhmm.vq_argmin(torch.zeros(1, 2, 3), torch.zeros(4, 2))

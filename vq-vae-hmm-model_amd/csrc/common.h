@@ -1,0 +1,55 @@
+// Shared device/host helpers for the vqhmm HIP kernels (gfx950 / CDNA4 only).
+//
+// Activation layout used by every training-path kernel ("PCL", padded
+// channels-last): rows r in [0, R), R = B * (T + 2).  Row b*(T+2) + 1 + t
+// holds time step t of sequence b; rows b*(T+2) and b*(T+2) + T + 1 are kept
+// all-zero, so a k=3 convolution never needs a boundary test: the zero rows
+// ARE the Conv1d zero padding of the reference (padding=1,
+// VQ_VAE_HMM_fixed.py:34-35,77-78).  Row stride = channel count (dense).
+//
+// "CF" = the reference's channels-first (B, C, T) layout, used at the
+// module boundary (x, u, logits, mu, logvar).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define VQHMM_OK 0
+#define VQHMM_EINVAL -1
+#define VQHMM_ELAUNCH -2
+#define VQHMM_EWORKSPACE -3
+#define VQHMM_EUNSUPPORTED -4
+
+namespace vqhmm {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// One 16x16x4 fp32 MFMA step: lane l supplies A[l&15][l>>4] and B[l>>4][l&15];
+// C/D: lane l, reg v -> row (l>>4)*4 + v, col l&15.  Result is a k-ordered
+// fp32 fmaf chain (exact f32, no reduced-precision path on gfx950).
+__device__ __forceinline__ f32x4 mfma16x16x4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__host__ __device__ __forceinline__ int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Map a PCL row to (b, t); returns false for pad rows / out of range.
+__device__ __forceinline__ bool row_bt(int64_t r, int64_t R, int T, int64_t& b, int& t) {
+  if (r < 0 || r >= R) return false;
+  const int64_t Tp = (int64_t)T + 2;
+  b = r / Tp;
+  t = (int)(r - b * Tp) - 1;
+  return t >= 0 && t < T;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+}  // namespace vqhmm
+
+#define VQHMM_LAUNCH_CHECK()                                          \
+  do {                                                                \
+    if (hipGetLastError() != hipSuccess) return VQHMM_ELAUNCH;        \
+  } while (0)

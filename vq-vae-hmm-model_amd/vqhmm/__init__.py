@@ -1,0 +1,12 @@
+"""vqhmm — MI355X-native (gfx950) implementation of the VAE_HMM training hot path
+of yashnaray/VQ-VAE-HMM-model.
+
+Drop-in surface (VQ_VAE_HMM_fixed.py): VAE_HMM, Encoder, Prior, Decoder,
+train_model, RandomChunkDataset, collate_fn — plus the hard-regime kernels
+vq_argmin / forward_backward / viterbi.  All compute runs in hand-written HIP
+kernels in libvqhmm.so; there is no CPU fallback.
+"""
+from . import _ext  # noqa: F401
+from .hmm import quantize, vq_argmin  # noqa: F401
+
+__all__ = ["vq_argmin", "quantize"]

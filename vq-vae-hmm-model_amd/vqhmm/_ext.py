@@ -1,0 +1,81 @@
+"""ctypes binding of libvqhmm.so (the C-ABI declared in include/vqhmm.h).
+
+There is no fallback: if the library or a HIP device is missing, every op
+raises.  The library is built in-tree by `make -C vq-vae-hmm-model_amd`
+(or `__graft_entry__.build()`).
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libvqhmm.so")
+NPARAMS = 18
+ABI_VERSION = 1
+
+_ERRORS = {-1: "invalid argument", -2: "kernel launch failed", -3: "workspace too small",
+           -4: "unsupported shape"}
+
+_lib = None
+
+c_i64 = ctypes.c_int64
+c_i32 = ctypes.c_int32
+c_f32 = ctypes.c_float
+c_vp = ctypes.c_void_p
+c_sz = ctypes.c_size_t
+
+
+class Dims(ctypes.Structure):
+    """Mirror of vqhmm_dims_t."""
+    _fields_ = [("input_dim", c_i32), ("hidden_dim", c_i32), ("K", c_i32),
+                ("hidden_dim2", c_i32), ("u_dim", c_i32), ("trans_hidden", c_i32)]
+
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "vqhmm_abi_version": (c_i32, []),
+    "vqhmm_param_layout": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(c_i64)]),
+    "vqhmm_vq_argmin_f32": (ctypes.c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp]),
+}
+
+
+def load():
+    """Load and type the library (no GPU needed).  Raises if missing."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"vqhmm: native library not built ({LIB_PATH}); run `make -C {os.path.dirname(_HERE)}`")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.vqhmm_abi_version() != ABI_VERSION:
+            raise RuntimeError("vqhmm: ABI version mismatch; rebuild the library")
+        _lib = lib
+    return _lib
+
+
+def exported_symbols():
+    return list(_SIGS)
+
+
+def check(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"vqhmm: {what} failed: {_ERRORS.get(rc, rc)}")
+
+
+def require_device(*tensors):
+    """The product path is HIP-only: refuse CPU tensors loudly (no fallback)."""
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("vqhmm runs on MI355X (HIP) only: move tensors to a 'cuda' (ROCm) device")
+
+
+def stream_ptr(device=None):
+    return c_vp(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr(t):
+    return c_vp(t.data_ptr()) if t is not None else c_vp(0)

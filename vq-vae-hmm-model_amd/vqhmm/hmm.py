@@ -1,0 +1,49 @@
+"""Hard-regime kernels: VQ nearest-codeword argmin, HMM forward-backward and
+Viterbi over the Prior's tables.  HIP only (libvqhmm.so).
+
+The reference defines these only in prose:
+  VQ         pseudocode.txt:11-18 (`quantize`), hard regimes backtesting.py:154-155
+  fwd-bwd    math.md:23-67 with Prior.forward tables (VQ_VAE_HMM_fixed.py:59-71)
+  Viterbi    same tables, max-plus
+The exact numerical contracts are documented in include/vqhmm.h.
+"""
+import torch
+
+from . import _ext
+
+
+def vq_argmin(z, codebook, return_dist=False):
+    """z (B, Dv, T) channels-first, codebook (K, Dv) -> idx (B, T) int32 [, dmin (B, T)].
+
+    idx[b, t] = argmin_k sum_d (z[b, d, t] - codebook[k, d])^2, ties -> lowest k.
+    """
+    _ext.require_device(z, codebook)
+    if z.dim() != 3 or codebook.dim() != 2 or z.shape[1] != codebook.shape[1]:
+        raise ValueError(f"vq_argmin: expected z (B,Dv,T) and codebook (K,Dv), got {tuple(z.shape)} {tuple(codebook.shape)}")
+    z = z.contiguous().float()
+    codebook = codebook.contiguous().float()
+    B, Dv, T = z.shape
+    K = codebook.shape[0]
+    idx = torch.empty((B, T), dtype=torch.int32, device=z.device)
+    dmin = torch.empty((B, T), dtype=torch.float32, device=z.device) if return_dist else None
+    lib = _ext.load()
+    _ext.check(lib.vqhmm_vq_argmin_f32(_ext.ptr(z), B, Dv, T, _ext.ptr(codebook), K, _ext.ptr(idx),
+                                       _ext.ptr(dmin), _ext.stream_ptr(z.device)), "vq_argmin")
+    return (idx, dmin) if return_dist else idx
+
+
+def quantize(z, codebook, beta=0.25):
+    """VQ-VAE quantizer of pseudocode.txt:11-18 on channels-first z (B, Dv, T).
+
+    Returns (z_q_st, idx, commit_loss, codebook_loss):
+      z_q = codebook[idx] (B, Dv, T); z_q_st = z + (z_q - z).detach() (straight-through, :12);
+      commit = beta * MSE(z, sg(z_q)) (:16); codebook = MSE(z_q, sg(z)) (:17).
+    The argmin is the HIP kernel; the gather/MSE are small elementwise ops on
+    its output.
+    """
+    idx = vq_argmin(z.detach(), codebook.detach())
+    z_q = codebook[idx.long()].permute(0, 2, 1)
+    z_q_st = z + (z_q - z).detach()
+    commit = beta * torch.mean((z - z_q.detach()) ** 2)
+    cb_loss = torch.mean((z_q - z.detach()) ** 2)
+    return z_q_st, idx, commit, cb_loss
