@@ -69,6 +69,62 @@ int vqhmm_vq_argmin_f32(const float* z, int64_t B, int64_t Dv, int64_t T,
                         const float* codebook, int64_t K,
                         int32_t* idx, float* dmin, void* stream);
 
+
+/* ------------------------------------------------------- training step ----
+ * compute_loss forward + backward of VAE_HMM (VQ_VAE_HMM_fixed.py:106-137,
+ * autograd of :156) as one native executor over hand-written kernels.
+ *
+ * params: host array of VQHMM_NPARAMS device pointers in parameters() order
+ *   (shapes: the reference's nn.Conv1d / nn.Linear / nn.Embedding weights).
+ * x (B, D, T) CF; u (B, U, T) if u_layout == 0, (B, T, U) if u_layout == 1
+ *   (Prior.forward's permute rule, :64-65); lengths (B) int64 on device.
+ * Workspace: vqhmm_elbo_workspace_size(); the forward saves activations in it
+ * and the backward must get the same workspace, dims, B and T.
+ * loss: device fp32 scalar; loss_accum (nullable): device fp64 scalar += loss
+ *   (train_model's epoch_loss, :158, without a per-step host sync).
+ * need_grad = 0 computes only the loss.
+ * Backward: grad (flat fp32, vqhmm_param_layout order) = grad_scale * dloss/dparams,
+ *   grad_scale a device fp32 scalar (autograd's grad_output) or NULL for 1. */
+int vqhmm_elbo_workspace_size(const vqhmm_dims_t* dims, int64_t B, int64_t T, size_t* bytes);
+int vqhmm_elbo_fwd_f32(const vqhmm_dims_t* dims, const float* const* params, const float* x,
+                       const float* u, int u_layout, const int64_t* lengths, int64_t B, int64_t T,
+                       float beta, int need_grad, void* workspace, size_t ws_bytes,
+                       float* loss, double* loss_accum, void* stream);
+int vqhmm_elbo_bwd_f32(const vqhmm_dims_t* dims, const float* const* params, const float* x,
+                       int64_t B, int64_t T, float beta, const float* grad_scale,
+                       void* workspace, size_t ws_bytes, float* grad, void* stream);
+/* Device addresses (inside the workspace) of the last forward's loss and of its
+ * pieces [recon, prior, entropy] (for tests).  Host-only, no GPU access. */
+int vqhmm_elbo_pieces(const vqhmm_dims_t* dims, int64_t B, int64_t T, const void* workspace,
+                      const float** loss, const float** pieces);
+
+/* torch.optim.Adam step (no weight decay / amsgrad; train_model uses the
+ * defaults, :146) over n contiguous fp32 elements.  `step` is a DEVICE int64
+ * step counter that this call increments before the update (so a captured
+ * graph replays correct bias corrections); the gradient is multiplied by
+ * grad_scale first (1/world_size after a SUM all-reduce, else 1). */
+int vqhmm_adam_f32(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                   double lr, double beta1, double beta2, double eps, int64_t* step, float grad_scale,
+                   void* stream);
+
+/* ---------------------------------------------------------- inference ----
+ * VAE_HMM.encode (:100, Encoder.forward :38-41): x (B,D,T) -> logits (B,K,T)
+ * VAE_HMM.decode (:103, Decoder.forward :81-90): q (B,K,T) -> mu, logvar (B,D,T)
+ * VAE_HMM.forward (:139-143): x -> mu, logvar, q = softmax(logits, dim=1)
+ * Prior.forward (:59-71): u -> log_pi (K), log_A (B,T,K,K)
+ * Unused parameter pointers may be NULL (e.g. encode needs only the encoder's). */
+int vqhmm_infer_workspace_size(const vqhmm_dims_t* dims, int64_t B, int64_t T, size_t* bytes);
+int vqhmm_encode_f32(const vqhmm_dims_t* dims, const float* const* params, const float* x,
+                     int64_t B, int64_t T, float* logits, void* workspace, size_t ws_bytes, void* stream);
+int vqhmm_decode_f32(const vqhmm_dims_t* dims, const float* const* params, const float* q,
+                     int64_t B, int64_t T, float* mu, float* logvar, void* workspace, size_t ws_bytes,
+                     void* stream);
+int vqhmm_forward_f32(const vqhmm_dims_t* dims, const float* const* params, const float* x,
+                      int64_t B, int64_t T, float* mu, float* logvar, float* q, void* workspace,
+                      size_t ws_bytes, void* stream);
+int vqhmm_prior_f32(const vqhmm_dims_t* dims, const float* const* params, const float* u, int u_layout,
+                    int64_t B, int64_t T, float* log_pi, float* log_A, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

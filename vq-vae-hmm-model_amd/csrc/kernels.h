@@ -1,0 +1,117 @@
+// Internal interface between the kernel translation units and the executor
+// (api.hip).  Not part of the public C-ABI (include/vqhmm.h).
+#pragma once
+#include "common.h"
+
+namespace vqhmm {
+
+struct ConvArgs {
+  const float* src;  // input activations
+  int src_cf;        // 1: CF (B, Kc, T); 0: PCL (R, Kc)
+  int Kc;            // input channels (GEMM K per tap)
+  int64_t R;
+  int T;
+  int ks;            // 1 or 3
+  const float* W;
+  int w_dgrad;       // 0: W is (N, Kc, ks); 1: W is (Kc, N, ks) used transposed + flipped
+  const float* bias; // (N) or null
+  const float* scale;// device scalar multiplying the accumulator, or null
+  int N;             // output channels
+  int act;           // 0 none, 1 relu, 2 multiply by (aux > 0)
+  const float* aux;  // PCL (R, N) for act == 2
+  float* out;        // PCL (R, N) or null
+  float* out_cf;     // CF (B, N, T) or null
+  // fused 1x1 tail on the activated output (requires N <= BN)
+  const float* tW;   // (C2, N)
+  const float* tb;   // (C2)
+  int C2;
+  float* t_out;      // PCL (R, C2)
+  float* t_cf0;      // CF, channels [0, t_split)
+  float* t_cf1;      // CF, channels [t_split, C2)
+  int t_split;
+  float* q_out;      // PCL softmax of the tail
+  float* q_cf;       // CF softmax of the tail
+};
+
+struct WgradArgs {
+  const float* dy;   // PCL (R, N) output gradient (pad rows zero)
+  const float* x;    // layer input: PCL (R, C) or CF (B, C, T)
+  int x_cf;
+  int64_t R;
+  int T;
+  int N, C, ks;
+  int64_t rows_per_chunk;  // multiple of 64
+  float* slab;       // [nchunks][N][C][ks]
+  float* bias_slab;  // [nchunks][N] or null
+};
+
+struct HeadArgs {
+  int64_t B;
+  int T;
+  int64_t R;
+  int D, K, U, TH;
+  const float* x;        // CF (B, D, T)
+  const float* u;        // (B, U, T) with strides below
+  int64_t u_sc, u_st;    // u[b, c, t] = u[b*U*T + c*u_sc + t*u_st]
+  const int64_t* lengths;
+  const float* par;      // PCL (R, 2D): mu | logvar
+  const float* logits;   // PCL (R, K)
+  const float* q;        // PCL (R, K)
+  const float* W1;       // (TH, U)
+  const float* b1;       // (TH)
+  const float* W2;       // (K*K, TH)
+  const float* b2;       // (K*K)
+  const float* log_prior;// (K)
+  float beta;
+  int need_grad;
+  float* dpar;           // PCL (R, 2D)
+  float* dqx;            // PCL (R, K)  dL/dq from the prior term
+  float* dlx;            // PCL (R, K)  dL/dlogits from the entropy term
+  double* part;          // [gridDim.x][4]: recon_sum, init_sum, trans_sum, ent_sum
+  float* slab_W1;        // [grid][TH*U]
+  float* slab_b1;        // [grid][TH]
+  float* slab_W2;        // [grid][K*K*TH]
+  float* slab_b2;        // [grid][K*K]
+  float* slab_q0;        // [grid][K]  sum_b q[b, :, 0]
+  int64_t ntiles;
+};
+
+struct PriorArgs {
+  int64_t B;
+  int T, K, U, TH;
+  const float* u;
+  int64_t u_sc, u_st;
+  const float *W1, *b1, *W2, *b2;
+  float* log_A;  // (B, T, K, K)
+};
+
+struct SlabSeg {
+  const float* slab;   // [nchunks][len]
+  float* out;          // [len]
+  const float* scale;  // device scalar or null
+  int64_t nchunks, len;
+};
+
+int launch_vq_argmin(const float* z, int64_t B, int64_t Dv, int64_t T, const float* cb, int64_t K, int32_t* idx,
+                     float* dmin, hipStream_t s);
+int launch_conv(const ConvArgs& a, hipStream_t s);
+int launch_wgrad(const WgradArgs& a, hipStream_t s);
+int64_t wgrad_chunks(int64_t R, int64_t tiles);
+int head_grid(int64_t R);
+int launch_head(const HeadArgs& a, int grid, hipStream_t s);
+int launch_prior_fwd(const PriorArgs& p, hipStream_t s);
+int launch_reduce_slabs(const SlabSeg* segs, int n, hipStream_t s);
+int launch_finalize_loss(const double* part, int nblk, const int64_t* lengths, int64_t B, int T, int D, float beta,
+                         float* loss, double* accum, float* pieces, hipStream_t s);
+int launch_compose_fwd(const float* W, const float* E, int H, int K, float* Wc, hipStream_t s);
+int launch_compose_bwd(const float* dWc, const float* W, const float* E, int H, int K, float* dW, float* dE,
+                       hipStream_t s);
+int launch_logits_bwd(const float* q, const float* dq_dec, const float* dqx, const float* dlx, const float* scale,
+                      int64_t R, int K, float* dlog, hipStream_t s);
+int launch_log_prior_grad(const float* q0sum, const float* log_prior, int K, float c, const float* scale, float* out,
+                          hipStream_t s);
+int launch_log_softmax_vec(const float* x, int K, float* out, hipStream_t s);
+int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, double lr, double beta1, double beta2,
+                double eps, int64_t* step, float gmul, hipStream_t s);
+
+}  // namespace vqhmm

@@ -1,0 +1,238 @@
+// Small kernels of the training step:
+//   reduce_slabs     deterministic split-K reduction of per-workgroup gradient partials
+//                    into the flat gradient buffer (fixed chunk order, no atomics)
+//   finalize_loss    loss = recon + beta*(prior - entropy)  (VQ_VAE_HMM_fixed.py:137)
+//   compose_fwd/bwd  decoder embedding folded into decoder.conv1:
+//                    conv1(q^T E) == conv1'(q) with W'[o,k,tap] = sum_h W[o,h,tap] E[k,h]
+//   logits_bwd       softmax backward of q = softmax(logits) (:114) + entropy's direct term
+//   adam             torch.optim.Adam update (defaults of train_model, :146)
+#include "kernels.h"
+
+namespace vqhmm {
+
+// ------------------------------------------------------------ slab reduction
+constexpr int MAX_SEGS = 24;
+struct SlabSegs {
+  SlabSeg s[MAX_SEGS];
+  int64_t blk_start[MAX_SEGS + 1];  // prefix of column-blocks per segment
+  int nseg;
+};
+
+// One workgroup = 64 consecutive columns x all chunks; 4 chunk phases combined in fixed order.
+__global__ __launch_bounds__(256) void reduce_slabs_kernel(SlabSegs segs) {
+  __shared__ float part[4][64];
+  int si = 0;
+  while (si + 1 < segs.nseg && (int64_t)blockIdx.x >= segs.blk_start[si + 1]) ++si;
+  const SlabSeg& sg = segs.s[si];
+  const int64_t col = ((int64_t)blockIdx.x - segs.blk_start[si]) * 64 + (threadIdx.x & 63);
+  const int ph = threadIdx.x >> 6;
+  float acc = 0.f;
+  if (col < sg.len)
+    for (int64_t c = ph; c < sg.nchunks; c += 4) acc += sg.slab[c * sg.len + col];
+  part[ph][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (ph == 0 && col < sg.len) {
+    float v = ((part[0][threadIdx.x] + part[1][threadIdx.x]) + part[2][threadIdx.x]) + part[3][threadIdx.x];
+    if (sg.scale) v *= *sg.scale;
+    sg.out[col] = v;
+  }
+}
+
+int launch_reduce_slabs(const SlabSeg* segs, int n, hipStream_t s) {
+  if (n > MAX_SEGS) return VQHMM_EINVAL;
+  SlabSegs ss{};
+  ss.nseg = n;
+  ss.blk_start[0] = 0;
+  for (int i = 0; i < n; ++i) {
+    ss.s[i] = segs[i];
+    ss.blk_start[i + 1] = ss.blk_start[i] + cdiv(segs[i].len, 64);
+  }
+  if (ss.blk_start[n] == 0) return VQHMM_OK;
+  reduce_slabs_kernel<<<(unsigned)ss.blk_start[n], 256, 0, s>>>(ss);
+  VQHMM_LAUNCH_CHECK();
+  return VQHMM_OK;
+}
+
+// ------------------------------------------------------------ loss finalize
+// part[nblk][4] = recon_sum, init_sum, trans_sum, ent_sum (ent_sum = sum of -sum_k q log q).
+__global__ void finalize_loss_kernel(const double* part, int nblk, const int64_t* lengths, int64_t B, int T, int D,
+                                     float beta, float* loss, double* accum, float* pieces) {
+  __shared__ double red[5][256];
+  double v[5] = {0, 0, 0, 0, 0};
+  for (int i = threadIdx.x; i < nblk; i += 256)
+    for (int k = 0; k < 4; ++k) v[k] += part[i * 4 + k];
+  for (int64_t b = threadIdx.x; b < B; b += 256) {
+    const int64_t L = lengths[b];
+    v[4] += (double)(L <= 0 ? 0 : (L < T ? L : T));
+  }
+  for (int k = 0; k < 5; ++k) red[k][threadIdx.x] = v[k];
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if (threadIdx.x < st)
+      for (int k = 0; k < 5; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + st];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float ncount = fmaxf((float)(red[4][0] * D), 1.0f);
+    const float recon = (float)red[0][0] / ncount;
+    const float prior = -(float)((red[1][0] + red[2][0]) / (double)B);
+    const float ent = (float)(red[3][0] / (double)B);
+    const float l = recon + beta * (prior - ent);
+    *loss = l;
+    if (accum) *accum += (double)l;
+    if (pieces) { pieces[0] = recon; pieces[1] = prior; pieces[2] = ent; }
+  }
+}
+
+int launch_finalize_loss(const double* part, int nblk, const int64_t* lengths, int64_t B, int T, int D, float beta,
+                         float* loss, double* accum, float* pieces, hipStream_t s) {
+  finalize_loss_kernel<<<1, 256, 0, s>>>(part, nblk, lengths, B, T, D, beta, loss, accum, pieces);
+  VQHMM_LAUNCH_CHECK();
+  return VQHMM_OK;
+}
+
+// ------------------------------------------------------------ composed decoder conv1
+// Wc[o][k][tap] = sum_h W[o][h][tap] * E[k][h];  W (H,H,3), E (K,H), Wc (H,K,3)
+__global__ void compose_fwd_kernel(const float* W, const float* E, int H, int K, float* Wc) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= H * K * 3) return;
+  const int tap = i % 3, k = (i / 3) % K, o = i / (3 * K);
+  float s = 0.f;
+  for (int h = 0; h < H; ++h) s = fmaf(W[(o * H + h) * 3 + tap], E[k * H + h], s);
+  Wc[i] = s;
+}
+// dW[o][h][tap] = sum_k dWc[o][k][tap] E[k][h];  dE[k][h] = sum_{o,tap} dWc[o][k][tap] W[o][h][tap]
+__global__ void compose_bwd_kernel(const float* dWc, const float* W, const float* E, int H, int K, float* dW,
+                                   float* dE) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int n1 = H * H * 3;
+  if (i < n1) {
+    const int tap = i % 3, h = (i / 3) % H, o = i / (3 * H);
+    float s = 0.f;
+    for (int k = 0; k < K; ++k) s = fmaf(dWc[(o * K + k) * 3 + tap], E[k * H + h], s);
+    dW[i] = s;
+  } else if (i < n1 + K * H) {
+    const int j = i - n1;
+    const int h = j % H, k = j / H;
+    float s = 0.f;
+    for (int o = 0; o < H; ++o)
+      for (int tap = 0; tap < 3; ++tap) s = fmaf(dWc[(o * K + k) * 3 + tap], W[(o * H + h) * 3 + tap], s);
+    dE[j] = s;
+  }
+}
+
+int launch_compose_fwd(const float* W, const float* E, int H, int K, float* Wc, hipStream_t s) {
+  compose_fwd_kernel<<<(unsigned)cdiv((int64_t)H * K * 3, 256), 256, 0, s>>>(W, E, H, K, Wc);
+  VQHMM_LAUNCH_CHECK();
+  return VQHMM_OK;
+}
+int launch_compose_bwd(const float* dWc, const float* W, const float* E, int H, int K, float* dW, float* dE,
+                       hipStream_t s) {
+  compose_bwd_kernel<<<(unsigned)cdiv((int64_t)H * H * 3 + K * H, 256), 256, 0, s>>>(dWc, W, E, H, K, dW, dE);
+  VQHMM_LAUNCH_CHECK();
+  return VQHMM_OK;
+}
+
+// ------------------------------------------------------------ logits backward
+// dlog = q * (dq - <q, dq>) + scale * dlx,  dq = dq_dec + scale * dqx   (rows of the PCL layout)
+__global__ void logits_bwd_kernel(const float* q, const float* dq_dec, const float* dqx, const float* dlx,
+                                  const float* scale, int64_t R, int K, float* dlog) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= R) return;
+  const float sc = scale ? *scale : 1.f;
+  float s = 0.f;
+  for (int k = 0; k < K; ++k) {
+    const float dq = dq_dec[r * K + k] + sc * dqx[r * K + k];
+    s = fmaf(q[r * K + k], dq, s);
+  }
+  for (int k = 0; k < K; ++k) {
+    const float qk = q[r * K + k];
+    const float dq = dq_dec[r * K + k] + sc * dqx[r * K + k];
+    dlog[r * K + k] = qk * (dq - s) + sc * dlx[r * K + k];
+  }
+}
+
+int launch_logits_bwd(const float* q, const float* dq_dec, const float* dqx, const float* dlx, const float* scale,
+                      int64_t R, int K, float* dlog, hipStream_t s) {
+  if (R == 0) return VQHMM_OK;
+  logits_bwd_kernel<<<(unsigned)cdiv(R, 256), 256, 0, s>>>(q, dq_dec, dqx, dlx, scale, R, K, dlog);
+  VQHMM_LAUNCH_CHECK();
+  return VQHMM_OK;
+}
+
+// ------------------------------------------------------------ log_prior grad
+// dlog_prior = dlp - softmax(log_prior) * sum(dlp),  dlp = c * sum_b q[b,:,0],  c = -beta/B (:71,:123,:131)
+__global__ void log_prior_grad_kernel(const float* q0sum, const float* log_prior, int K, float c, const float* scale,
+                                      float* out) {
+  if (threadIdx.x != 0) return;
+  const float sc = scale ? *scale : 1.f;
+  float m = -__builtin_inff();
+  for (int k = 0; k < K; ++k) m = fmaxf(m, log_prior[k]);
+  float se = 0.f;
+  for (int k = 0; k < K; ++k) se += __expf(log_prior[k] - m);
+  float tot = 0.f;
+  for (int k = 0; k < K; ++k) tot += c * q0sum[k];
+  for (int k = 0; k < K; ++k) out[k] = sc * (c * q0sum[k] - __expf(log_prior[k] - m) / se * tot);
+}
+
+int launch_log_prior_grad(const float* q0sum, const float* log_prior, int K, float c, const float* scale, float* out,
+                          hipStream_t s) {
+  log_prior_grad_kernel<<<1, 64, 0, s>>>(q0sum, log_prior, K, c, scale, out);
+  VQHMM_LAUNCH_CHECK();
+  return VQHMM_OK;
+}
+
+// ------------------------------------------------------------ Adam
+// torch.optim.Adam (no weight decay, no amsgrad), as its foreach/fused CUDA path computes it:
+//   m = m + (1-b1)*(g-m);  v = b2*v + (1-b2)*g*g;
+//   denom = sqrt(v)/sqrt(1-b2^t) + eps;  p = p - (lr/(1-b1^t)) * m/denom
+// The step count t lives on the device (incremented by adam_step_kernel) so a
+// captured HIP graph replays correct bias corrections.  gmul scales the
+// gradient first (1/world_size after a SUM all-reduce).
+__global__ void adam_step_kernel(int64_t* step) { *step += 1; }
+
+__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                            float* __restrict__ v, int64_t n, double lr, double b1, double b2, double eps,
+                            const int64_t* __restrict__ step, float gmul) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const double t = (double)*step;
+  const float step_size = (float)(lr / (1.0 - pow(b1, t)));
+  const float bc2s = (float)sqrt(1.0 - pow(b2, t));
+  const float gi = g[i] * gmul;
+  const float mi = m[i] + (float)(1.0 - b1) * (gi - m[i]);
+  const float vi = v[i] * (float)b2 + (float)(1.0 - b2) * gi * gi;
+  m[i] = mi;
+  v[i] = vi;
+  const float denom = sqrtf(vi) / bc2s + (float)eps;
+  p[i] = p[i] + (-step_size) * (mi / denom);
+}
+
+int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, double lr, double beta1, double beta2,
+                double eps, int64_t* step, float gmul, hipStream_t s) {
+  adam_step_kernel<<<1, 1, 0, s>>>(step);
+  VQHMM_LAUNCH_CHECK();
+  if (n == 0) return VQHMM_OK;
+  adam_kernel<<<(unsigned)cdiv(n, 256), 256, 0, s>>>(p, g, m, v, n, lr, beta1, beta2, eps, step, gmul);
+  VQHMM_LAUNCH_CHECK();
+  return VQHMM_OK;
+}
+
+}  // namespace vqhmm
+
+namespace vqhmm {
+__global__ void log_softmax_vec_kernel(const float* x, int K, float* out) {
+  if (threadIdx.x != 0) return;
+  float m = -__builtin_inff();
+  for (int k = 0; k < K; ++k) m = fmaxf(m, x[k]);
+  float s = 0.f;
+  for (int k = 0; k < K; ++k) s += __expf(x[k] - m);
+  const float l = m + __logf(s);
+  for (int k = 0; k < K; ++k) out[k] = x[k] - l;
+}
+int launch_log_softmax_vec(const float* x, int K, float* out, hipStream_t s) {
+  log_softmax_vec_kernel<<<1, 64, 0, s>>>(x, K, out);
+  VQHMM_LAUNCH_CHECK();
+  return VQHMM_OK;
+}
+}  // namespace vqhmm

@@ -16,7 +16,7 @@
 //    (4 dims x 2 positions x {v_sub, v_fma});
 //  * per lane 2*KB independent fma chains give ILP; z for a 16-dim chunk
 //    stays in VGPRs and is reused across all KB codewords.
-#include "common.h"
+#include "kernels.h"
 
 namespace vqhmm {
 

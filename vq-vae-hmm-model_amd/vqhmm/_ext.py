@@ -37,6 +37,24 @@ _SIGS = {
     "vqhmm_abi_version": (c_i32, []),
     "vqhmm_param_layout": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(c_i64)]),
     "vqhmm_vq_argmin_f32": (ctypes.c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "vqhmm_elbo_workspace_size": (ctypes.c_int, [ctypes.POINTER(Dims), c_i64, c_i64, ctypes.POINTER(c_sz)]),
+    "vqhmm_elbo_fwd_f32": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(c_vp), c_vp, c_vp, ctypes.c_int,
+                                          c_vp, c_i64, c_i64, c_f32, ctypes.c_int, c_vp, c_sz, c_vp, c_vp, c_vp]),
+    "vqhmm_elbo_bwd_f32": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(c_vp), c_vp, c_i64, c_i64, c_f32,
+                                          c_vp, c_vp, c_sz, c_vp, c_vp]),
+    "vqhmm_elbo_pieces": (ctypes.c_int, [ctypes.POINTER(Dims), c_i64, c_i64, c_vp, ctypes.POINTER(c_vp),
+                                         ctypes.POINTER(c_vp)]),
+    "vqhmm_adam_f32": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.c_double, ctypes.c_double,
+                                      ctypes.c_double, ctypes.c_double, c_vp, c_f32, c_vp]),
+    "vqhmm_infer_workspace_size": (ctypes.c_int, [ctypes.POINTER(Dims), c_i64, c_i64, ctypes.POINTER(c_sz)]),
+    "vqhmm_encode_f32": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(c_vp), c_vp, c_i64, c_i64, c_vp,
+                                        c_vp, c_sz, c_vp]),
+    "vqhmm_decode_f32": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(c_vp), c_vp, c_i64, c_i64, c_vp,
+                                        c_vp, c_vp, c_sz, c_vp]),
+    "vqhmm_forward_f32": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(c_vp), c_vp, c_i64, c_i64, c_vp,
+                                         c_vp, c_vp, c_vp, c_sz, c_vp]),
+    "vqhmm_prior_f32": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(c_vp), c_vp, ctypes.c_int, c_i64,
+                                       c_i64, c_vp, c_vp, c_vp]),
 }
 
 

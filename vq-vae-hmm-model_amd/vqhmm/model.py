@@ -1,0 +1,296 @@
+"""Drop-in nn.Module surface of VQ_VAE_HMM_fixed.py, executed by libvqhmm.so.
+
+Same class names, constructor signatures, submodule names and parameter
+shapes as the reference, so `state_dict()` keys are identical and reference
+checkpoints (e.g. models/vae_hmm.pt) load unchanged:
+
+    Encoder(input_dim, hidden_dim, hidden_dim2, K)          VQ_VAE_HMM_fixed.py:31-41
+    Prior(K, u_dim=None, trans_hidden=128)                  :43-71
+    Decoder(K, latent_dim, hidden_dim, output_dim)          :73-90
+    VAE_HMM(input_dim, hidden_dim, K, hidden_dim2, u_dim=None, trans_hidden=128)   :92-143
+
+The parameters are ordinary nn.Parameters (nn.Conv1d / nn.Linear /
+nn.Embedding); only the compute is replaced: every forward/backward FLOP runs
+in the hand-written HIP kernels behind the C-ABI.  CPU tensors are refused
+(no fallback).  Error conventions of the reference are kept (ValueError for a
+missing u_dim / u / lengths).
+"""
+import ctypes
+
+import torch
+import torch.nn as nn
+
+from . import _ext
+
+PARAM_ORDER = (
+    "encoder.conv1.weight", "encoder.conv1.bias",
+    "encoder.conv2.weight", "encoder.conv2.bias",
+    "encoder.to_logits.weight", "encoder.to_logits.bias",
+    "prior.log_prior",
+    "prior.transition_net.0.weight", "prior.transition_net.0.bias",
+    "prior.transition_net.2.weight", "prior.transition_net.2.bias",
+    "decoder.embeddings.weight",
+    "decoder.conv1.weight", "decoder.conv1.bias",
+    "decoder.conv2.weight", "decoder.conv2.bias",
+    "decoder.to_params.weight", "decoder.to_params.bias",
+)
+
+_PtrArray = ctypes.c_void_p * _ext.NPARAMS
+
+
+def _no_grad_through(name, *tensors):
+    if torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in tensors):
+        raise RuntimeError(f"vqhmm: autograd through {name}() alone is not implemented; "
+                           "train through VAE_HMM.compute_loss (or call under torch.no_grad())")
+
+
+def _ptr_array(tensors):
+    arr = _PtrArray()
+    for i, t in enumerate(tensors):
+        if t is not None:
+            if t.dtype != torch.float32 or not t.is_contiguous():
+                raise ValueError("vqhmm: parameters must be contiguous float32")
+            arr[i] = t.data_ptr()
+    return arr
+
+
+def _workspace(device, nbytes):
+    return torch.empty(int(nbytes), dtype=torch.uint8, device=device)
+
+
+class Encoder(nn.Module):
+    """Conv1d(D->H,k3) ReLU Conv1d(H->H2,k3) ReLU Conv1d(H2->K,1)  (:31-41)."""
+
+    def __init__(self, input_dim, hidden_dim, hidden_dim2, K):
+        super().__init__()
+        self.conv1 = nn.Conv1d(input_dim, hidden_dim, 3, padding=1)
+        self.conv2 = nn.Conv1d(hidden_dim, hidden_dim2, 3, padding=1)
+        self.to_logits = nn.Conv1d(hidden_dim2, K, 1)
+
+    def _dims(self):
+        H, D, _ = self.conv1.weight.shape
+        H2 = self.conv2.weight.shape[0]
+        K = self.to_logits.weight.shape[0]
+        return _ext.Dims(D, H, K, H2, 1, 1)
+
+    def forward(self, x):
+        _ext.require_device(x)
+        _no_grad_through("Encoder.forward", x, self.conv1.weight)
+        if x.dim() != 3 or x.shape[1] != self.conv1.weight.shape[1]:
+            raise RuntimeError(f"Encoder: expected input (B, {self.conv1.weight.shape[1]}, T), got {tuple(x.shape)}")
+        x = x.contiguous().float()
+        B, _, T = x.shape
+        d = self._dims()
+        lib = _ext.load()
+        logits = torch.empty((B, d.K, T), device=x.device)
+        if B * T == 0:
+            return logits
+        nb = ctypes.c_size_t()
+        _ext.check(lib.vqhmm_infer_workspace_size(ctypes.byref(d), B, T, ctypes.byref(nb)), "workspace")
+        ws = _workspace(x.device, nb.value)
+        w = [None] * _ext.NPARAMS
+        w[0:6] = [self.conv1.weight, self.conv1.bias, self.conv2.weight, self.conv2.bias,
+                  self.to_logits.weight, self.to_logits.bias]
+        _ext.check(lib.vqhmm_encode_f32(ctypes.byref(d), _ptr_array(w), _ext.ptr(x), B, T, _ext.ptr(logits),
+                                        _ext.ptr(ws), nb.value, _ext.stream_ptr(x.device)), "encode")
+        return logits
+
+
+class Prior(nn.Module):
+    """Input-conditioned HMM prior: log_pi (K,), log_A (B,T,K,K)  (:43-71)."""
+
+    def __init__(self, K, u_dim=None, trans_hidden=128):
+        super().__init__()
+        self.K = K
+        self.u_dim = u_dim
+        self.log_prior = nn.Parameter(torch.zeros(K))
+        if u_dim is None:
+            raise ValueError('Stationary transitions not implemented')
+        self.transition_net = nn.Sequential(
+            nn.Linear(u_dim, trans_hidden),
+            nn.ReLU(),
+            nn.Linear(trans_hidden, K * K),
+        )
+
+    def u_layout(self, u):
+        """0 = (B, U, T) channels-first, 1 = (B, T, U) — the reference's rule (:64-65)."""
+        if u.dim() == 3 and u.shape[1] == self.u_dim:
+            return 0
+        if u.dim() == 3 and u.shape[2] == self.u_dim:
+            return 1
+        raise RuntimeError(f"Prior: expected u of shape (B, {self.u_dim}, T) or (B, T, {self.u_dim}), got {tuple(u.shape)}")
+
+    def forward(self, u=None):
+        if u is None:
+            raise ValueError('u required for non-stationary transitions')
+        _ext.require_device(u)
+        _no_grad_through("Prior.forward", u, self.log_prior)
+        lay = self.u_layout(u)
+        u = u.contiguous().float()
+        B = u.shape[0]
+        T = u.shape[2] if lay == 0 else u.shape[1]
+        K = self.K
+        lin0, lin2 = self.transition_net[0], self.transition_net[2]
+        d = _ext.Dims(1, 1, K, 1, self.u_dim, lin0.weight.shape[0])
+        log_pi = torch.empty(K, device=u.device)
+        log_A = torch.empty((B, T, K, K), device=u.device)
+        w = [None] * _ext.NPARAMS
+        w[6:11] = [self.log_prior, lin0.weight, lin0.bias, lin2.weight, lin2.bias]
+        _ext.check(_ext.load().vqhmm_prior_f32(ctypes.byref(d), _ptr_array(w), _ext.ptr(u), lay, B, T,
+                                               _ext.ptr(log_pi), _ext.ptr(log_A), _ext.stream_ptr(u.device)), "prior")
+        return log_pi, log_A
+
+
+class Decoder(nn.Module):
+    """Soft codebook embedding q^T E, then Conv1d x2 + 1x1 -> (mu, logvar)  (:73-90)."""
+
+    def __init__(self, K, latent_dim, hidden_dim, output_dim):
+        super().__init__()
+        self.embeddings = nn.Embedding(K, latent_dim)
+        self.conv1 = nn.Conv1d(latent_dim, hidden_dim, 3, padding=1)
+        self.conv2 = nn.Conv1d(hidden_dim, hidden_dim, 3, padding=1)
+        self.to_params = nn.Conv1d(hidden_dim, output_dim * 2, 1)
+
+    def _dims(self):
+        K, Hl = self.embeddings.weight.shape
+        H = self.conv1.weight.shape[0]
+        if Hl != H or self.conv2.weight.shape[0] != H:
+            raise RuntimeError("vqhmm: Decoder with latent_dim != hidden_dim is not supported "
+                               "(VAE_HMM always builds Decoder(K, H, H, D), :98)")
+        D = self.to_params.weight.shape[0] // 2
+        return _ext.Dims(D, H, K, 1, 1, 1)
+
+    def _ptrs(self):
+        w = [None] * _ext.NPARAMS
+        w[11:18] = [self.embeddings.weight, self.conv1.weight, self.conv1.bias, self.conv2.weight,
+                    self.conv2.bias, self.to_params.weight, self.to_params.bias]
+        return w
+
+    def forward(self, q):
+        _ext.require_device(q)
+        _no_grad_through("Decoder.forward", q, self.conv1.weight)
+        d = self._dims()
+        if q.dim() != 3 or q.shape[1] != d.K:
+            raise RuntimeError(f"Decoder: expected q of shape (B, {d.K}, T), got {tuple(q.shape)}")
+        q = q.contiguous().float()
+        B, _, T = q.shape
+        mu = torch.empty((B, d.input_dim, T), device=q.device)
+        logvar = torch.empty((B, d.input_dim, T), device=q.device)
+        if B * T == 0:
+            return mu, logvar
+        lib = _ext.load()
+        nb = ctypes.c_size_t()
+        _ext.check(lib.vqhmm_infer_workspace_size(ctypes.byref(d), B, T, ctypes.byref(nb)), "workspace")
+        ws = _workspace(q.device, nb.value)
+        _ext.check(lib.vqhmm_decode_f32(ctypes.byref(d), _ptr_array(self._ptrs()), _ext.ptr(q), B, T, _ext.ptr(mu),
+                                        _ext.ptr(logvar), _ext.ptr(ws), nb.value, _ext.stream_ptr(q.device)),
+                   "decode")
+        return mu, logvar
+
+
+class _ElboLoss(torch.autograd.Function):
+    """compute_loss as one autograd node: forward + backward are native executors."""
+
+    @staticmethod
+    def forward(ctx, model, x, u, lengths, beta, *params):
+        d = model._dims()
+        B, _, T = x.shape
+        lay = model.prior.u_layout(u)
+        lib = _ext.load()
+        nb = ctypes.c_size_t()
+        _ext.check(lib.vqhmm_elbo_workspace_size(ctypes.byref(d), B, T, ctypes.byref(nb)), "workspace")
+        ws = _workspace(x.device, nb.value)
+        loss = torch.empty((), device=x.device)
+        need_grad = any(ctx.needs_input_grad[5:])
+        ptrs = _ptr_array(params)
+        _ext.check(lib.vqhmm_elbo_fwd_f32(ctypes.byref(d), ptrs, _ext.ptr(x), _ext.ptr(u), lay, _ext.ptr(lengths),
+                                          B, T, float(beta), int(need_grad), _ext.ptr(ws), nb.value,
+                                          _ext.ptr(loss), None, _ext.stream_ptr(x.device)), "compute_loss forward")
+        ctx.state = (d, ws, nb.value, B, T, float(beta))
+        ctx.save_for_backward(x, *params)
+        return loss
+
+    @staticmethod
+    def backward(ctx, gloss):
+        d, ws, nbytes, B, T, beta = ctx.state
+        x, *params = ctx.saved_tensors
+        lib = _ext.load()
+        off = param_offsets(d)
+        grad = torch.empty(off[-1], device=x.device)
+        gl = gloss.contiguous().float()
+        _ext.check(lib.vqhmm_elbo_bwd_f32(ctypes.byref(d), _ptr_array(params), _ext.ptr(x), B, T, beta,
+                                          _ext.ptr(gl), _ext.ptr(ws), nbytes, _ext.ptr(grad),
+                                          _ext.stream_ptr(x.device)), "compute_loss backward")
+        grads = [grad[off[i]:off[i + 1]].view_as(p) for i, p in enumerate(params)]
+        return (None, None, None, None, None, *grads)
+
+
+def param_offsets(d):
+    off = (ctypes.c_int64 * (_ext.NPARAMS + 1))()
+    _ext.check(_ext.load().vqhmm_param_layout(ctypes.byref(d), off), "param_layout")
+    return list(off)
+
+
+class VAE_HMM(nn.Module):
+    """Mean-field VAE with an input-conditioned HMM prior (:92-143)."""
+
+    def __init__(self, input_dim, hidden_dim, K, hidden_dim2, u_dim=None, trans_hidden=128):
+        super().__init__()
+        self.K = K
+        self.encoder = Encoder(input_dim, hidden_dim, hidden_dim2, K)
+        self.prior = Prior(K, u_dim, trans_hidden)
+        self.decoder = Decoder(K, hidden_dim, hidden_dim, input_dim)
+
+    def _dims(self):
+        H, D, _ = self.encoder.conv1.weight.shape
+        return _ext.Dims(D, H, self.K, self.encoder.conv2.weight.shape[0], self.prior.u_dim,
+                         self.prior.transition_net[0].weight.shape[0])
+
+    def ordered_parameters(self):
+        named = dict(self.named_parameters())
+        return [named[n] for n in PARAM_ORDER]
+
+    def encode(self, x):
+        return self.encoder(x)
+
+    def decode(self, q):
+        return self.decoder(q)
+
+    def compute_loss(self, x, u=None, lengths=None, beta=1.0):
+        B, C, T = x.shape
+        if lengths is None:
+            raise ValueError('lengths required')
+        if u is None:
+            raise ValueError('u required for non-stationary transitions')
+        _ext.require_device(x, u)
+        if C != self.encoder.conv1.weight.shape[1]:
+            raise RuntimeError(f"compute_loss: x has {C} channels, model expects {self.encoder.conv1.weight.shape[1]}")
+        lay = self.prior.u_layout(u)
+        if u.shape[0] != B or (u.shape[2] if lay == 0 else u.shape[1]) != T:
+            raise RuntimeError(f"compute_loss: u {tuple(u.shape)} does not match x {tuple(x.shape)}")
+        x = x.contiguous().float()
+        u = u.contiguous().float()
+        lengths = torch.as_tensor(lengths).to(device=x.device, dtype=torch.int64, non_blocking=True).contiguous()
+        if lengths.shape != (B,):
+            raise RuntimeError(f"compute_loss: lengths must have shape ({B},)")
+        return _ElboLoss.apply(self, x, u, lengths, float(beta), *self.ordered_parameters())
+
+    def forward(self, x):
+        _ext.require_device(x)
+        _no_grad_through("VAE_HMM.forward", x, self.encoder.conv1.weight)
+        x = x.contiguous().float()
+        B, _, T = x.shape
+        d = self._dims()
+        mu = torch.empty((B, d.input_dim, T), device=x.device)
+        logvar = torch.empty_like(mu)
+        q = torch.empty((B, self.K, T), device=x.device)
+        if B * T == 0:
+            return (mu, logvar), q
+        lib = _ext.load()
+        nb = ctypes.c_size_t()
+        _ext.check(lib.vqhmm_infer_workspace_size(ctypes.byref(d), B, T, ctypes.byref(nb)), "workspace")
+        ws = _workspace(x.device, nb.value)
+        _ext.check(lib.vqhmm_forward_f32(ctypes.byref(d), _ptr_array(self.ordered_parameters()), _ext.ptr(x), B, T,
+                                         _ext.ptr(mu), _ext.ptr(logvar), _ext.ptr(q), _ext.ptr(ws), nb.value,
+                                         _ext.stream_ptr(x.device)), "forward")
+        return (mu, logvar), q

@@ -1,0 +1,150 @@
+"""Native training loop: train_model() (VQ_VAE_HMM_fixed.py:145-162) and the
+per-step executor it uses.
+
+TrainState owns, per model:
+  * one flat fp32 parameter buffer (the module's nn.Parameters become views of
+    it, so state_dict()/checkpoints are unchanged) and a flat gradient buffer
+    in vqhmm_param_layout order,
+  * Adam moments + a device step counter (torch.optim.Adam defaults, :146),
+  * a workspace per batch shape (B, T),
+  * a device fp64 epoch accumulator: the loss is summed on the GPU in step
+    order, so the epoch print needs ONE host sync per epoch instead of the
+    reference's loss.item() every step (:158) — the printed value is the same
+    double-precision sum of the same fp32 losses.
+
+One step = elbo forward (+loss accumulate) -> elbo backward -> [RCCL
+all-reduce of the flat gradient when torch.distributed is initialised] ->
+fused Adam.  Everything in the step is HIP kernels from libvqhmm.so plus the
+collective; nothing syncs the host, so a fixed-shape step can be captured in a
+HIP graph (`capture()`).
+"""
+import ctypes
+
+import torch
+
+from . import _ext
+from .model import _ptr_array, param_offsets
+
+
+class TrainState:
+    def __init__(self, model, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, process_group=None, distributed=None):
+        params = model.ordered_parameters()
+        dev = params[0].device
+        if dev.type != "cuda":
+            raise RuntimeError("vqhmm.train_model runs on MI355X (HIP) only: call model.to('cuda') first")
+        self.model = model
+        self.device = dev
+        self.dims = model._dims()
+        self.off = param_offsets(self.dims)
+        n = self.off[-1]
+        self.flat = torch.empty(n, device=dev)
+        with torch.no_grad():
+            for i, p in enumerate(params):
+                self.flat[self.off[i]:self.off[i + 1]].copy_(p.detach().reshape(-1))
+                p.data = self.flat[self.off[i]:self.off[i + 1]].view_as(p)
+        self.grad = torch.zeros(n, device=dev)
+        self.exp_avg = torch.zeros(n, device=dev)
+        self.exp_avg_sq = torch.zeros(n, device=dev)
+        self.step_dev = torch.zeros((), dtype=torch.int64, device=dev)
+        self.lr, self.betas, self.eps = float(lr), tuple(float(b) for b in betas), float(eps)
+        self.ptrs = _ptr_array(params)
+        self.loss = torch.zeros((), device=dev)
+        self.epoch_acc = torch.zeros((), dtype=torch.float64, device=dev)
+        self._ws = {}
+        self.lib = _ext.load()
+        if distributed is None:
+            distributed = torch.distributed.is_available() and torch.distributed.is_initialized()
+        self.distributed = bool(distributed)
+        self.pg = process_group
+        self.world = torch.distributed.get_world_size(process_group) if self.distributed else 1
+
+    # ----------------------------------------------------------------- helpers
+    def workspace(self, B, T):
+        key = (B, T)
+        ws = self._ws.get(key)
+        if ws is None:
+            nb = ctypes.c_size_t()
+            _ext.check(self.lib.vqhmm_elbo_workspace_size(ctypes.byref(self.dims), B, T, ctypes.byref(nb)),
+                       "workspace")
+            ws = torch.empty(nb.value, dtype=torch.uint8, device=self.device)
+            self._ws[key] = ws
+        return ws
+
+    def prepare(self, x, u, lengths):
+        dev = self.device
+        x = x.to(dev, torch.float32, non_blocking=True).contiguous()
+        u = u.to(dev, torch.float32, non_blocking=True).contiguous()
+        lengths = torch.as_tensor(lengths).to(dev, torch.int64, non_blocking=True).contiguous()
+        return x, u, lengths
+
+    # -------------------------------------------------------------- the step
+    def forward_backward(self, x, u, lengths, beta):
+        """Loss (accumulated into epoch_acc) and flat gradient of one batch."""
+        B, _, T = x.shape
+        lay = self.model.prior.u_layout(u)
+        ws = self.workspace(B, T)
+        st = _ext.stream_ptr(self.device)
+        d = ctypes.byref(self.dims)
+        _ext.check(self.lib.vqhmm_elbo_fwd_f32(d, self.ptrs, _ext.ptr(x), _ext.ptr(u), lay, _ext.ptr(lengths), B, T,
+                                               float(beta), 1, _ext.ptr(ws), ws.numel(), _ext.ptr(self.loss),
+                                               _ext.ptr(self.epoch_acc), st), "elbo forward")
+        _ext.check(self.lib.vqhmm_elbo_bwd_f32(d, self.ptrs, _ext.ptr(x), B, T, float(beta), None, _ext.ptr(ws),
+                                               ws.numel(), _ext.ptr(self.grad), st), "elbo backward")
+
+    def reduce_gradients(self):
+        if self.distributed and self.world > 1:
+            torch.distributed.all_reduce(self.grad, op=torch.distributed.ReduceOp.SUM, group=self.pg)
+
+    def apply_adam(self):
+        b1, b2 = self.betas
+        _ext.check(self.lib.vqhmm_adam_f32(_ext.ptr(self.flat), _ext.ptr(self.grad), _ext.ptr(self.exp_avg),
+                                           _ext.ptr(self.exp_avg_sq), self.flat.numel(), self.lr, b1, b2, self.eps,
+                                           _ext.ptr(self.step_dev), 1.0 / self.world, _ext.stream_ptr(self.device)),
+                   "adam")
+
+    def step(self, x, u, lengths, beta):
+        """zero_grad + compute_loss + backward + (all-reduce) + Adam.step (:154-157)."""
+        x, u, lengths = self.prepare(x, u, lengths)
+        self.forward_backward(x, u, lengths, beta)
+        self.reduce_gradients()
+        self.apply_adam()
+        return self.loss
+
+    def publish_grads(self):
+        """Leave the last step's gradients in p.grad, as the reference loop does."""
+        for i, p in enumerate(self.model.ordered_parameters()):
+            p.grad = self.grad[self.off[i]:self.off[i + 1]].view_as(p).clone()
+
+    def capture(self, x, u, lengths, beta, warmup=2):
+        """Capture one fixed-shape step (single process) into a HIP graph; returns a replay callable."""
+        if self.distributed and self.world > 1:
+            raise RuntimeError("capture(): multi-rank steps run eagerly")
+        x, u, lengths = self.prepare(x, u, lengths)
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self.forward_backward(x, u, lengths, beta)
+                self.apply_adam()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.forward_backward(x, u, lengths, beta)
+            self.apply_adam()
+        return g.replay
+
+
+def train_model(model, dataloader, num_epochs=10, lr=1e-3):
+    """Drop-in for VQ_VAE_HMM_fixed.train_model (:145-162): Adam(lr) with
+    default betas/eps, beta warm-up min(1, 2(ep+1)/E), same epoch print."""
+    state = TrainState(model, lr=lr)
+    model.train()
+    for ep in range(num_epochs):
+        state.epoch_acc.zero_()
+        beta = min(1.0, 2.0 * (ep + 1) / num_epochs)  # KL annealing
+        for x, u, lengths in dataloader:
+            state.step(x, u, lengths, beta)
+        epoch_loss = state.epoch_acc.item()
+        print(f"Epoch {ep+1}/{num_epochs}, Loss: {epoch_loss/len(dataloader):.4f}")
+    state.publish_grads()
+    return model
