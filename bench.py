@@ -1,0 +1,259 @@
+#!/usr/bin/env python3
+"""Headline benchmark: VAE_HMM train-step sequences/sec on MI355X.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
+        bench.py --gpus N --steps K --warmup W
+
+Workload (BASELINE.json configs[1], "cfg2"): VAE_HMM(K=3, input_dim=5,
+hidden_dim=64, hidden_dim2=32, u_dim=4, trans_hidden=128), batch 1024 x T=200
+per GPU, synthetic x/u ~ N(0,1) already resident in HBM, lengths = T, beta=1,
+Adam lr=1e-3.  A step = zero_grad + compute_loss + backward + [RCCL
+all-reduce of the flat gradient] + Adam, exactly the reference's train_model
+inner loop (VQ_VAE_HMM_fixed.py:154-157).  N ranks each process 1024
+sequences (weak scaling); `value` = N*1024*K / max-over-ranks wall time.
+
+Also reported (rank 0):
+  roofline      dominant kernel of the step, timed live with HIP events on the
+                launch stream over instrumented steps; achieved = algorithmic
+                FLOPs (or bytes) per launch / average launch duration
+                (vqhmm_elbo_stage_info); traffic = PMC HBM bytes per launch from
+                profiles/ when a matching measurement is committed, else null.
+  cpu_baseline  the CPU oracle (oracle/ref_model.py, a from-scratch restatement
+                pinned bit-exact to the reference) timed on this host's cores on
+                the same workload shape (N=1 only).
+"""
+import argparse
+import ctypes
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "vq-vae-hmm-model_amd"))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # name: (B per GPU, T, D, H, H2, K, U, TH)
+    "cfg2": (1024, 200, 5, 64, 32, 3, 4, 128),
+    "cfg4": (512, 512, 16, 64, 32, 8, 4, 128),
+}
+MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense FP32 (matrix = vector peak)
+HBM_PEAK_GBPS = 8000.0         # MI355X_MICROARCH.md: HBM3E spec peak
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
+    ap.add_argument("--no-graph", action="store_true", help="run the N=1 step eagerly instead of a HIP graph")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--profile-steps", type=int, default=5)
+    return ap.parse_args()
+
+
+def stage_timings(lib, st, x, u, L, B, T, beta, nsteps):
+    """Per-stage device time (us) inside real steps: events around each stage on the launch stream."""
+    from vqhmm import _ext
+    d = ctypes.byref(st.dims)
+    ws = st.workspace(B, T)
+    lay = st.model.prior.u_layout(u)
+    n = lib.vqhmm_elbo_num_stages()
+    stream = torch.cuda.current_stream()
+    sp = _ext.stream_ptr()
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(n + 1)] for _ in range(nsteps)]
+    for k in range(nsteps):
+        for s in range(n):
+            ev[k][s].record(stream)
+            _ext.check(lib.vqhmm_elbo_stage_f32(d, st.ptrs, _ext.ptr(x), _ext.ptr(u), lay, _ext.ptr(L), B, T,
+                                                float(beta), _ext.ptr(ws), ws.numel(), _ext.ptr(st.grad), s, sp),
+                       "stage")
+        ev[k][n].record(stream)
+        st.apply_adam()
+    torch.cuda.synchronize()
+    out = []
+    name = ctypes.create_string_buffer(64)
+    fl, by, mf = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
+    for s in range(n):
+        us = statistics.median(ev[k][s].elapsed_time(ev[k][s + 1]) * 1e3 for k in range(nsteps))
+        lib.vqhmm_elbo_stage_info(d, B, T, s, name, 64, ctypes.byref(fl), ctypes.byref(by), ctypes.byref(mf))
+        out.append(dict(stage=s, name=name.value.decode(), us=us, flops=fl.value, bytes=by.value,
+                        mfma=bool(mf.value)))
+    return out
+
+
+def traffic_for(kernel_name, cfg):
+    """PMC-measured HBM bytes per launch, if committed under profiles/ for this kernel + config."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            tab = json.load(f)
+        return tab.get(cfg, {}).get(kernel_name)
+    except (OSError, ValueError):
+        return None
+
+
+def vq_cfg3(lib):
+    """VQ L2-argmin at BASELINE cfg3 shape (K=32, Dv=64, B=2048, T=200): HBM roofline."""
+    from vqhmm import _ext
+    g = torch.Generator(device="cuda").manual_seed(1234)
+    B, Dv, T, K = 2048, 64, 200, 32
+    z = torch.randn(B, Dv, T, device="cuda", generator=g)
+    cb = torch.randn(K, Dv, device="cuda", generator=g)
+    idx = torch.empty(B, T, dtype=torch.int32, device="cuda")
+    sp = _ext.stream_ptr()
+    run = lambda: lib.vqhmm_vq_argmin_f32(_ext.ptr(z), B, Dv, T, _ext.ptr(cb), K, _ext.ptr(idx), None, sp)
+    for _ in range(5):
+        run()
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(20):
+        run()
+    e1.record(s)
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) / 20 * 1e3
+    byts = 4.0 * B * T * Dv + 4.0 * K * Dv + 4.0 * B * T
+    gbps = byts / (us * 1e-6) / 1e9
+    del z
+    return {"kernel": "vq_argmin_kernel", "bound": "hbm", "avg_us": round(us, 2), "achieved": round(gbps, 1),
+            "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(gbps / HBM_PEAK_GBPS, 4),
+            "traffic": traffic_for("vq_argmin_kernel", "vq_cfg3"), "shape": "B2048 Dv64 T200 K32"}
+
+
+def cpu_baseline(cfg, seconds):
+    """CPU oracle (oracle/ref_model.py) train step on the same shape, this host's cores."""
+    from oracle import ref_model as RM
+    import vqhmm
+    B, T, D, H, H2, K, U, TH = cfg
+    torch.manual_seed(0)
+    m = vqhmm.VAE_HMM(D, H, K, H2, u_dim=U, trans_hidden=TH)  # same init as the GPU run (CPU tensors)
+    p = {k: v.detach().clone().requires_grad_(True) for k, v in m.state_dict().items()}
+    gen = torch.Generator().manual_seed(1234)
+    x = torch.randn(B, D, T, generator=gen)
+    u = torch.randn(B, U, T, generator=gen)
+    L = torch.full((B,), T, dtype=torch.long)
+    opt = torch.optim.Adam([p[k] for k in RM.PARAM_ORDER], lr=1e-3)
+
+    def step():
+        opt.zero_grad()
+        RM.elbo(p, x, u, L, 1.0, K, U).backward()
+        opt.step()
+
+    step()
+    times = []
+    t_end = time.perf_counter() + seconds
+    while time.perf_counter() < t_end or len(times) < 3:
+        t0 = time.perf_counter()
+        step()
+        times.append(time.perf_counter() - t0)
+    med = statistics.median(times)
+    return {"value": round(B / med, 1), "unit": "sequences/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"{len(times)} full train steps (B={B}, T={T}, cfg2 shape) of the torch-CPU oracle, "
+                      f"median {med*1e3:.1f} ms/step"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    import vqhmm
+    from vqhmm import _ext
+    lib = _ext.load()
+
+    cfg = CONFIGS[a.config]
+    B, T, D, H, H2, K, U, TH = cfg
+    torch.manual_seed(0)
+    model = vqhmm.VAE_HMM(D, H, K, H2, u_dim=U, trans_hidden=TH).cuda()
+    st = vqhmm.TrainState(model, lr=1e-3)
+    g = torch.Generator(device="cuda").manual_seed(1234 + rank)
+    x = torch.randn(B, D, T, device="cuda", generator=g)
+    u = torch.randn(B, U, T, device="cuda", generator=g)
+    L = torch.full((B,), T, dtype=torch.int64, device="cuda")
+    beta = 1.0
+
+    use_graph = world == 1 and not a.no_graph
+    if use_graph:
+        step = st.capture(x, u, L, beta)
+    else:
+        step = lambda: st.step(x, u, L, beta)  # noqa: E731
+
+    for _ in range(a.warmup):
+        step()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = t.item()
+    ms_per_step = elapsed / a.steps * 1e3
+    value = world * B * a.steps / elapsed
+
+    roof = None
+    kernels = None
+    if rank == 0 and a.profile_steps > 0:
+        stages = stage_timings(lib, st, x, u, L, B, T, beta, a.profile_steps)
+        dom = max(stages, key=lambda s: s["us"])
+        dur = dom["us"] * 1e-6
+        if dom["mfma"]:
+            ach = dom["flops"] / dur / 1e12
+            roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(ach / MFMA_F32_PEAK_TFLOPS, 4)}
+        else:
+            ach = dom["bytes"] / dur / 1e9
+            roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBPS, 4)}
+        roof.update({"traffic": traffic_for(dom["name"], a.config), "kernel": dom["name"],
+                     "avg_us": round(dom["us"], 2)})
+        kernels = {s["name"]: round(s["us"], 2) for s in stages}
+    vq = vq_cfg3(lib) if rank == 0 else None
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(cfg, a.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": "VAE_HMM train-step sequences/sec (K=3, T=200, D=5) at 1/2/4/8 MI355X",
+            "value": round(value, 1), "unit": "sequences/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": f"{a.config}: VAE_HMM train step (compute_loss+backward+Adam)",
+                       "global_batch": world * B, "seq_len": T, "K": K, "input_dim": D, "hidden_dim": H,
+                       "hidden_dim2": H2, "u_dim": U, "trans_hidden": TH,
+                       "parallelism": f"dp{world}" if world > 1 else "single", "hip_graph": use_graph},
+            "roofline": roof, "cpu_baseline": cpu,
+            "step_kernels_us": kernels, "vq_cfg3": vq,
+        }
+        if cpu:
+            line["speedup_vs_cpu"] = round(value / cpu["value"], 1)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -98,6 +98,18 @@ int vqhmm_elbo_bwd_f32(const vqhmm_dims_t* dims, const float* const* params, con
 int vqhmm_elbo_pieces(const vqhmm_dims_t* dims, int64_t B, int64_t T, const void* workspace,
                       const float** loss, const float** pieces);
 
+/* Stage table of the training step (forward stages then backward stages, in
+ * launch order).  stage_info: name, algorithmic FLOPs and bytes of ONE launch
+ * (host-only); stage_f32 re-runs one stage on a workspace holding a completed
+ * forward/backward (per-kernel timing, ablation). */
+int vqhmm_elbo_num_stages(void);
+int vqhmm_elbo_stage_info(const vqhmm_dims_t* dims, int64_t B, int64_t T, int stage, char* name,
+                          size_t name_len, double* flops, double* bytes, int* mfma_bound);
+int vqhmm_elbo_stage_f32(const vqhmm_dims_t* dims, const float* const* params, const float* x,
+                         const float* u, int u_layout, const int64_t* lengths, int64_t B, int64_t T,
+                         float beta, void* workspace, size_t ws_bytes, float* grad, int stage,
+                         void* stream);
+
 /* torch.optim.Adam step (no weight decay / amsgrad; train_model uses the
  * defaults, :146) over n contiguous fp32 elements.  `step` is a DEVICE int64
  * step counter that this call increments before the update (so a captured

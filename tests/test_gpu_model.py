@@ -86,8 +86,8 @@ def test_grad_output_scaling():
     g1 = [p.grad.clone() for p in m.parameters()]
     m.zero_grad()
     m.compute_loss(x, u, L, 0.5).backward()
-    for a, b in zip(g1, m.parameters()):
-        assert torch.allclose(a, 3.0 * b.grad, rtol=1e-6, atol=1e-12)
+    for (name, b), a in zip(m.named_parameters(), g1):
+        assert_grad_close(a.cpu().numpy(), 3.0 * b.grad.cpu().numpy(), name)
 
 
 @pytest.mark.parametrize("case", GOLDEN_CASES)
@@ -129,9 +129,14 @@ def test_adam_steps_match_reference(case):
             for k in vqhmm.PARAM_ORDER:
                 ref = g[f"adam{step+1}/" + k]
                 init = g["w/" + k]
-                # the update itself must match; compare params relative to the step size
-                err = np.abs(sd[k].cpu().numpy() - ref).max()
-                assert err <= 2e-6 * max(1.0, np.abs(init).max()) + 1e-4 * 1e-3 * (step + 1), (k, step, err)
+                # Adam moves every element by <= ~lr per step whatever |g| is, so
+                # gradient noise of ~1e-6 on near-zero gradients shows up as a
+                # fraction of lr: bound the trajectory difference by 1% of the
+                # cumulative step size, and its mean by 1e-4 of it.
+                diff = np.abs(sd[k].cpu().numpy().astype(np.float64) - ref) - 2e-7 * np.abs(init)
+                lr_steps = 1e-3 * (step + 1)
+                assert diff.max() <= 1e-2 * lr_steps, (k, step, diff.max())
+                assert diff.mean() <= 1e-4 * lr_steps, (k, step, diff.mean())
 
 
 @pytest.mark.parametrize("case", ["cfg1_seeded", "cfg1_trained", "k8_d16", "smoke_tiny"])

@@ -5,6 +5,7 @@
 #include "vqhmm.h"
 
 #include <math.h>
+#include <string.h>
 
 #include "kernels.h"
 
@@ -154,6 +155,212 @@ int vqhmm_elbo_workspace_size(const vqhmm_dims_t* d, int64_t B, int64_t T, size_
   return VQHMM_OK;
 }
 
+}  // extern "C"
+
+// ------------------------------------------------------------------ stage table
+// The training step as an ordered list of kernel launches.  The forward and
+// backward entry points run their stages in order; vqhmm_elbo_stage_f32 runs
+// one (per-kernel timing / ablation), and vqhmm_elbo_stage_info describes it.
+namespace {
+
+enum Stage {
+  S_COMPOSE, S_ENC1, S_ENC2, S_DEC1, S_DEC2, S_HEAD, S_FINAL,                 // forward
+  S_PAR_DG, S_DEC2_DG, S_DEC1_DG, S_LOGIT_BWD, S_LOGIT_DG, S_ENC2_DG,         // backward data
+  S_W_PAR, S_W_DEC2, S_W_DEC1, S_W_LOGIT, S_W_ENC2, S_W_ENC1,                 // backward weights
+  S_REDUCE, S_COMPOSE_BWD, S_LOGPRIOR,                                         // reductions
+  S_COUNT
+};
+const int FWD_FIRST = S_COMPOSE, FWD_LAST = S_FINAL, BWD_FIRST = S_PAR_DG, BWD_LAST = S_LOGPRIOR;
+const char* kStageNames[S_COUNT] = {
+    "compose_fwd", "enc_conv1", "enc_conv2+to_logits", "dec_conv1(composed)", "dec_conv2+to_params",
+    "elbo_head", "finalize_loss", "to_params_dgrad", "dec_conv2_dgrad", "dec_conv1_dgrad", "logits_bwd",
+    "to_logits_dgrad", "enc_conv2_dgrad", "to_params_wgrad", "dec_conv2_wgrad", "dec_conv1_wgrad",
+    "to_logits_wgrad", "enc_conv2_wgrad", "enc_conv1_wgrad", "reduce_slabs", "compose_bwd", "log_prior_grad"};
+
+struct StepCtx {
+  const float* const* w;
+  const float* x;
+  const float* u;
+  int u_layout;
+  const int64_t* lengths;
+  float beta;
+  int need_grad;
+  float* loss;
+  double* loss_accum;
+  const float* gscale;
+  float* g;
+};
+
+ConvArgs conv_of(const ElboPlan& p, const float* const* wp, int st) {
+  static const float* const kNull[VQHMM_NPARAMS] = {};
+  const float* const* w = wp ? wp : kNull;  // stage_work() only needs the shapes
+  ConvArgs a = conv_base(p);
+  switch (st) {
+    case S_ENC1:
+      a.src_cf = 1; a.Kc = p.D; a.ks = 3; a.W = w[ENC1_W]; a.bias = w[ENC1_B]; a.N = p.H; a.act = 1; a.out = p.h1e;
+      break;
+    case S_ENC2:
+      a.src = p.h1e; a.Kc = p.H; a.ks = 3; a.W = w[ENC2_W]; a.bias = w[ENC2_B]; a.N = p.H2; a.act = 1; a.out = p.h2e;
+      a.tW = w[LOGIT_W]; a.tb = w[LOGIT_B]; a.C2 = p.K; a.t_out = p.logits; a.q_out = p.q;
+      break;
+    case S_DEC1:
+      a.src = p.q; a.Kc = p.K; a.ks = 3; a.W = p.Wc; a.bias = w[DEC1_B]; a.N = p.H; a.act = 1; a.out = p.g1;
+      break;
+    case S_DEC2:
+      a.src = p.g1; a.Kc = p.H; a.ks = 3; a.W = w[DEC2_W]; a.bias = w[DEC2_B]; a.N = p.H; a.act = 1; a.out = p.g2;
+      a.tW = w[PAR_W]; a.tb = w[PAR_B]; a.C2 = 2 * p.D; a.t_out = p.par;
+      break;
+    case S_PAR_DG:
+      a.src = p.dpar; a.Kc = 2 * p.D; a.ks = 1; a.W = w[PAR_W]; a.w_dgrad = 1; a.N = p.H; a.act = 2; a.aux = p.g2;
+      a.out = p.dg2;
+      break;
+    case S_DEC2_DG:
+      a.src = p.dg2; a.Kc = p.H; a.ks = 3; a.W = w[DEC2_W]; a.w_dgrad = 1; a.N = p.H; a.act = 2; a.aux = p.g1;
+      a.out = p.dg1;
+      break;
+    case S_DEC1_DG:
+      a.src = p.dg1; a.Kc = p.H; a.ks = 3; a.W = p.Wc; a.w_dgrad = 1; a.N = p.K; a.act = 0; a.out = p.dqd;
+      break;
+    case S_LOGIT_DG:
+      a.src = p.dlog; a.Kc = p.K; a.ks = 1; a.W = w[LOGIT_W]; a.w_dgrad = 1; a.N = p.H2; a.act = 2; a.aux = p.h2e;
+      a.out = p.dh2;
+      break;
+    case S_ENC2_DG:
+      a.src = p.dh2; a.Kc = p.H2; a.ks = 3; a.W = w[ENC2_W]; a.w_dgrad = 1; a.N = p.H; a.act = 2; a.aux = p.h1e;
+      a.out = p.dh1;
+      break;
+  }
+  return a;
+}
+
+int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
+  const float* const* w = c.w;
+  switch (st) {
+    case S_COMPOSE:
+      return launch_compose_fwd(w[DEC1_W], w[EMB], p.H, p.K, p.Wc, s);
+    case S_ENC1: {
+      ConvArgs a = conv_of(p, w, st);
+      a.src = c.x;
+      return launch_conv(a, s);
+    }
+    case S_ENC2: case S_DEC1: case S_DEC2: case S_DEC2_DG: case S_DEC1_DG: case S_LOGIT_DG: case S_ENC2_DG:
+      return launch_conv(conv_of(p, w, st), s);
+    case S_PAR_DG: {
+      ConvArgs a = conv_of(p, w, st);
+      a.scale = c.gscale;  // dpar is the head's gradient for dloss = 1
+      return launch_conv(a, s);
+    }
+    case S_HEAD: {
+      HeadArgs h{};
+      h.B = p.B; h.T = p.T; h.R = p.R; h.D = p.D; h.K = p.K; h.U = p.U; h.TH = p.TH;
+      h.x = c.x; h.u = c.u;
+      if (c.u_layout == 0) { h.u_sc = p.T; h.u_st = 1; } else { h.u_sc = 1; h.u_st = p.U; }
+      h.lengths = c.lengths; h.par = p.par; h.logits = p.logits; h.q = p.q;
+      h.W1 = w[TN0_W]; h.b1 = w[TN0_B]; h.W2 = w[TN2_W]; h.b2 = w[TN2_B]; h.log_prior = w[LOG_PRIOR];
+      h.beta = c.beta; h.need_grad = c.need_grad;
+      h.dpar = p.dpar; h.dqx = p.dqx; h.dlx = p.dlx; h.part = p.part;
+      h.slab_W1 = p.sW1; h.slab_b1 = p.sb1; h.slab_W2 = p.sW2; h.slab_b2 = p.sb2; h.slab_q0 = p.sq0;
+      return launch_head(h, p.hgrid, s);
+    }
+    case S_FINAL:
+      return launch_finalize_loss(p.part, p.hgrid, c.lengths, p.B, p.T, p.D, c.beta, c.loss, c.loss_accum,
+                                  p.pieces, s);
+    case S_LOGIT_BWD:
+      return launch_logits_bwd(p.q, p.dqd, p.dqx, p.dlx, c.gscale, p.R, p.K, p.dlog, s);
+    case S_W_PAR: case S_W_DEC2: case S_W_DEC1: case S_W_LOGIT: case S_W_ENC2: case S_W_ENC1: {
+      const int i = st - S_W_PAR;
+      const float* dys[6] = {p.dpar, p.dg2, p.dg1, p.dlog, p.dh2, p.dh1};
+      const float* xs[6] = {p.g2, p.g1, p.q, p.h2e, p.h1e, c.x};
+      const WLayer& L = p.wl[i];
+      WgradArgs wa{};
+      wa.dy = dys[i]; wa.x = xs[i]; wa.x_cf = (i == 5); wa.R = p.R; wa.T = p.T;
+      wa.N = L.N; wa.C = L.C; wa.ks = L.ks; wa.rows_per_chunk = L.rows; wa.slab = L.slab; wa.bias_slab = L.bslab;
+      return launch_wgrad(wa, s);
+    }
+    case S_REDUCE: {
+      int64_t off[VQHMM_NPARAMS + 1];
+      vqhmm_dims_t d{p.D, p.H, p.K, p.H2, p.U, p.TH};
+      vqhmm_param_layout(&d, off);
+      float* g = c.g;
+      const float* gs = c.gscale;
+      SlabSeg segs[18];
+      int n = 0;
+      auto seg = [&](const float* slab, int64_t nch, int64_t len, float* out, const float* scale) {
+        segs[n++] = SlabSeg{slab, out, scale, nch, len};
+      };
+      const WLayer* wl = p.wl;
+      seg(wl[0].slab, wl[0].nchunks, (int64_t)wl[0].N * wl[0].C, g + off[PAR_W], gs);  // dpar is unscaled
+      seg(wl[0].bslab, wl[0].nchunks, wl[0].N, g + off[PAR_B], gs);
+      seg(wl[1].slab, wl[1].nchunks, (int64_t)wl[1].N * wl[1].C * 3, g + off[DEC2_W], nullptr);
+      seg(wl[1].bslab, wl[1].nchunks, wl[1].N, g + off[DEC2_B], nullptr);
+      seg(wl[2].slab, wl[2].nchunks, (int64_t)wl[2].N * wl[2].C * 3, p.dWc, nullptr);
+      seg(wl[2].bslab, wl[2].nchunks, wl[2].N, g + off[DEC1_B], nullptr);
+      seg(wl[3].slab, wl[3].nchunks, (int64_t)wl[3].N * wl[3].C, g + off[LOGIT_W], nullptr);
+      seg(wl[3].bslab, wl[3].nchunks, wl[3].N, g + off[LOGIT_B], nullptr);
+      seg(wl[4].slab, wl[4].nchunks, (int64_t)wl[4].N * wl[4].C * 3, g + off[ENC2_W], nullptr);
+      seg(wl[4].bslab, wl[4].nchunks, wl[4].N, g + off[ENC2_B], nullptr);
+      seg(wl[5].slab, wl[5].nchunks, (int64_t)wl[5].N * wl[5].C * 3, g + off[ENC1_W], nullptr);
+      seg(wl[5].bslab, wl[5].nchunks, wl[5].N, g + off[ENC1_B], nullptr);
+      seg(p.sW1, p.hgrid, (int64_t)p.TH * p.U, g + off[TN0_W], gs);
+      seg(p.sb1, p.hgrid, p.TH, g + off[TN0_B], gs);
+      seg(p.sW2, p.hgrid, (int64_t)p.K * p.K * p.TH, g + off[TN2_W], gs);
+      seg(p.sb2, p.hgrid, (int64_t)p.K * p.K, g + off[TN2_B], gs);
+      seg(p.sq0, p.hgrid, p.K, p.q0sum, nullptr);
+      return launch_reduce_slabs(segs, n, s);
+    }
+    case S_COMPOSE_BWD: {
+      int64_t off[VQHMM_NPARAMS + 1];
+      vqhmm_dims_t d{p.D, p.H, p.K, p.H2, p.U, p.TH};
+      vqhmm_param_layout(&d, off);
+      return launch_compose_bwd(p.dWc, w[DEC1_W], w[EMB], p.H, p.K, c.g + off[DEC1_W], c.g + off[EMB], s);
+    }
+    case S_LOGPRIOR: {
+      int64_t off[VQHMM_NPARAMS + 1];
+      vqhmm_dims_t d{p.D, p.H, p.K, p.H2, p.U, p.TH};
+      vqhmm_param_layout(&d, off);
+      return launch_log_prior_grad(p.q0sum, w[LOG_PRIOR], p.K, -c.beta / (float)p.B, c.gscale, c.g + off[LOG_PRIOR],
+                                   s);
+    }
+  }
+  return VQHMM_EINVAL;
+}
+
+// Algorithmic work of one launch of a stage (what roofline.achieved is computed from).
+void stage_work(const ElboPlan& p, int st, double* flops, double* bytes, int* mfma) {
+  const double N = (double)p.B * p.T;  // valid positions
+  const double R = (double)p.R;
+  *flops = 0; *bytes = 0; *mfma = 0;
+  if (st == S_ENC1 || st == S_ENC2 || st == S_DEC1 || st == S_DEC2 || st == S_PAR_DG || st == S_DEC2_DG ||
+      st == S_DEC1_DG || st == S_LOGIT_DG || st == S_ENC2_DG) {
+    ConvArgs a = conv_of(p, nullptr, st);
+    *flops = 2.0 * N * a.N * a.Kc * a.ks + (a.tW ? 2.0 * N * a.C2 * a.N : 0.0);
+    *bytes = 4.0 * (R * a.Kc + R * a.N + (a.act == 2 ? R * a.N : 0) + (a.tW ? R * a.C2 * (a.q_out ? 2 : 1) : 0));
+    *mfma = 1;
+  } else if (st >= S_W_PAR && st <= S_W_ENC1) {
+    const WLayer& L = p.wl[st - S_W_PAR];
+    *flops = 2.0 * N * L.N * L.C * L.ks;
+    *bytes = 4.0 * (R * L.N + R * L.C + (double)L.nchunks * (L.N * L.C * L.ks + L.N));
+    *mfma = 1;
+  } else if (st == S_HEAD) {
+    const double KK = (double)p.K * p.K;
+    *flops = N * (2.0 * p.TH * p.U + 2.0 * p.TH * KK + 6.0 * p.TH * KK + 4.0 * p.TH * p.U + 20.0 * p.D + 12.0 * KK);
+    *bytes = 4.0 * R * (2 * p.D + p.D + p.U + 2 * p.K + 2 * p.D + 2 * p.K);
+  } else if (st == S_LOGIT_BWD) {
+    *bytes = 4.0 * R * 6 * p.K;
+    *flops = R * 8.0 * p.K;
+  } else if (st == S_REDUCE) {
+    double b = 0;
+    for (int i = 0; i < 6; ++i) b += (double)p.wl[i].nchunks * (p.wl[i].N * p.wl[i].C * p.wl[i].ks + p.wl[i].N);
+    b += (double)p.hgrid * ((double)p.TH * p.U + p.TH + (double)p.K * p.K * p.TH + p.K * p.K + p.K);
+    *bytes = 4.0 * b;
+    *flops = b;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
 int vqhmm_elbo_fwd_f32(const vqhmm_dims_t* d, const float* const* w, const float* x, const float* u, int u_layout,
                        const int64_t* lengths, int64_t B, int64_t T, float beta, int need_grad, void* ws,
                        size_t ws_bytes, float* loss, double* loss_accum, void* stream) {
@@ -162,41 +369,10 @@ int vqhmm_elbo_fwd_f32(const vqhmm_dims_t* d, const float* const* w, const float
     if (!w[i]) return VQHMM_EINVAL;
   ElboPlan p = plan_elbo(d, B, T, ws);
   if (ws_bytes < p.bytes) return VQHMM_EWORKSPACE;
-  hipStream_t s = (hipStream_t)stream;
-  int rc;
-  // F0: composed decoder conv1 weight
-  if ((rc = launch_compose_fwd(w[DEC1_W], w[EMB], p.H, p.K, p.Wc, s))) return rc;
-  // F1: encoder.conv1 + ReLU, x read channels-first
-  ConvArgs a = conv_base(p);
-  a.src = x; a.src_cf = 1; a.Kc = p.D; a.ks = 3; a.W = w[ENC1_W]; a.bias = w[ENC1_B]; a.N = p.H; a.act = 1;
-  a.out = p.h1e;
-  if ((rc = launch_conv(a, s))) return rc;
-  // F2: encoder.conv2 + ReLU, fused to_logits tail + softmax -> logits, q
-  a = conv_base(p);
-  a.src = p.h1e; a.Kc = p.H; a.ks = 3; a.W = w[ENC2_W]; a.bias = w[ENC2_B]; a.N = p.H2; a.act = 1; a.out = p.h2e;
-  a.tW = w[LOGIT_W]; a.tb = w[LOGIT_B]; a.C2 = p.K; a.t_out = p.logits; a.q_out = p.q;
-  if ((rc = launch_conv(a, s))) return rc;
-  // F3: decoder.conv1 on q with the composed weight + ReLU
-  a = conv_base(p);
-  a.src = p.q; a.Kc = p.K; a.ks = 3; a.W = p.Wc; a.bias = w[DEC1_B]; a.N = p.H; a.act = 1; a.out = p.g1;
-  if ((rc = launch_conv(a, s))) return rc;
-  // F4: decoder.conv2 + ReLU, fused to_params tail -> (mu | logvar)
-  a = conv_base(p);
-  a.src = p.g1; a.Kc = p.H; a.ks = 3; a.W = w[DEC2_W]; a.bias = w[DEC2_B]; a.N = p.H; a.act = 1; a.out = p.g2;
-  a.tW = w[PAR_W]; a.tb = w[PAR_B]; a.C2 = 2 * p.D; a.t_out = p.par;
-  if ((rc = launch_conv(a, s))) return rc;
-  // F5: fused ELBO head (+ its gradients when need_grad)
-  HeadArgs h{};
-  h.B = B; h.T = p.T; h.R = p.R; h.D = p.D; h.K = p.K; h.U = p.U; h.TH = p.TH;
-  h.x = x; h.u = u;
-  if (u_layout == 0) { h.u_sc = T; h.u_st = 1; } else { h.u_sc = 1; h.u_st = p.U; }
-  h.lengths = lengths; h.par = p.par; h.logits = p.logits; h.q = p.q;
-  h.W1 = w[TN0_W]; h.b1 = w[TN0_B]; h.W2 = w[TN2_W]; h.b2 = w[TN2_B]; h.log_prior = w[LOG_PRIOR];
-  h.beta = beta; h.need_grad = need_grad;
-  h.dpar = p.dpar; h.dqx = p.dqx; h.dlx = p.dlx; h.part = p.part;
-  h.slab_W1 = p.sW1; h.slab_b1 = p.sb1; h.slab_W2 = p.sW2; h.slab_b2 = p.sb2; h.slab_q0 = p.sq0;
-  if ((rc = launch_head(h, p.hgrid, s))) return rc;
-  return launch_finalize_loss(p.part, p.hgrid, lengths, B, p.T, p.D, beta, loss, loss_accum, p.pieces, s);
+  StepCtx c{w, x, u, u_layout, lengths, beta, need_grad, loss, loss_accum, nullptr, nullptr};
+  for (int st = FWD_FIRST; st <= FWD_LAST; ++st)
+    if (int rc = run_stage(p, c, st, (hipStream_t)stream)) return rc;
+  return VQHMM_OK;
 }
 
 int vqhmm_elbo_bwd_f32(const vqhmm_dims_t* d, const float* const* w, const float* x, int64_t B, int64_t T,
@@ -204,73 +380,39 @@ int vqhmm_elbo_bwd_f32(const vqhmm_dims_t* d, const float* const* w, const float
   if (!dims_ok(d) || !w || B <= 0 || T <= 0 || !x || !ws || !g) return VQHMM_EINVAL;
   ElboPlan p = plan_elbo(d, B, T, ws);
   if (ws_bytes < p.bytes) return VQHMM_EWORKSPACE;
-  hipStream_t s = (hipStream_t)stream;
-  int64_t off[VQHMM_NPARAMS + 1];
-  vqhmm_param_layout(d, off);
-  int rc;
-  // B1: to_params data grad (1x1, transposed) * ReLU'(g2), scaled by grad_scale
-  ConvArgs a = conv_base(p);
-  a.src = p.dpar; a.Kc = 2 * p.D; a.ks = 1; a.W = w[PAR_W]; a.w_dgrad = 1; a.scale = grad_scale; a.N = p.H;
-  a.act = 2; a.aux = p.g2; a.out = p.dg2;
-  if ((rc = launch_conv(a, s))) return rc;
-  // B2: decoder.conv2 data grad * ReLU'(g1)
-  a = conv_base(p);
-  a.src = p.dg2; a.Kc = p.H; a.ks = 3; a.W = w[DEC2_W]; a.w_dgrad = 1; a.N = p.H; a.act = 2; a.aux = p.g1;
-  a.out = p.dg1;
-  if ((rc = launch_conv(a, s))) return rc;
-  // B3: composed decoder.conv1 data grad -> dq (decoder path)
-  a = conv_base(p);
-  a.src = p.dg1; a.Kc = p.H; a.ks = 3; a.W = p.Wc; a.w_dgrad = 1; a.N = p.K; a.act = 0; a.out = p.dqd;
-  if ((rc = launch_conv(a, s))) return rc;
-  // B4: softmax backward (+ prior and entropy terms) -> dlogits
-  if ((rc = launch_logits_bwd(p.q, p.dqd, p.dqx, p.dlx, grad_scale, p.R, p.K, p.dlog, s))) return rc;
-  // B5: to_logits data grad * ReLU'(h2e)
-  a = conv_base(p);
-  a.src = p.dlog; a.Kc = p.K; a.ks = 1; a.W = w[LOGIT_W]; a.w_dgrad = 1; a.N = p.H2; a.act = 2; a.aux = p.h2e;
-  a.out = p.dh2;
-  if ((rc = launch_conv(a, s))) return rc;
-  // B6: encoder.conv2 data grad * ReLU'(h1e)
-  a = conv_base(p);
-  a.src = p.dh2; a.Kc = p.H2; a.ks = 3; a.W = w[ENC2_W]; a.w_dgrad = 1; a.N = p.H; a.act = 2; a.aux = p.h1e;
-  a.out = p.dh1;
-  if ((rc = launch_conv(a, s))) return rc;
-  // weight gradients (split-K partial slabs)
-  const float* dys[6] = {p.dpar, p.dg2, p.dg1, p.dlog, p.dh2, p.dh1};
-  const float* xs[6] = {p.g2, p.g1, p.q, p.h2e, p.h1e, x};
-  for (int i = 0; i < 6; ++i) {
-    const WLayer& L = p.wl[i];
-    WgradArgs wa{};
-    wa.dy = dys[i]; wa.x = xs[i]; wa.x_cf = (i == 5); wa.R = p.R; wa.T = p.T;
-    wa.N = L.N; wa.C = L.C; wa.ks = L.ks; wa.rows_per_chunk = L.rows; wa.slab = L.slab; wa.bias_slab = L.bslab;
-    if ((rc = launch_wgrad(wa, s))) return rc;
+  StepCtx c{w, x, nullptr, 0, nullptr, beta, 1, nullptr, nullptr, grad_scale, g};
+  for (int st = BWD_FIRST; st <= BWD_LAST; ++st)
+    if (int rc = run_stage(p, c, st, (hipStream_t)stream)) return rc;
+  return VQHMM_OK;
+}
+
+int vqhmm_elbo_num_stages(void) { return S_COUNT; }
+
+int vqhmm_elbo_stage_info(const vqhmm_dims_t* d, int64_t B, int64_t T, int stage, char* name, size_t name_len,
+                          double* flops, double* bytes, int* mfma_bound) {
+  if (!dims_ok(d) || stage < 0 || stage >= S_COUNT || B <= 0 || T <= 0) return VQHMM_EINVAL;
+  ElboPlan p = plan_elbo(d, B, T, nullptr);
+  if (name && name_len) {
+    strncpy(name, kStageNames[stage], name_len - 1);
+    name[name_len - 1] = 0;
   }
-  // reduce every slab into the flat gradient (fixed order)
-  SlabSeg segs[18];
-  int n = 0;
-  auto seg = [&](const float* slab, int64_t nch, int64_t len, float* out, const float* scale) {
-    segs[n++] = SlabSeg{slab, out, scale, nch, len};
-  };
-  const WLayer* wl = p.wl;
-  seg(wl[0].slab, wl[0].nchunks, (int64_t)wl[0].N * wl[0].C, g + off[PAR_W], grad_scale);  // dpar is unscaled
-  seg(wl[0].bslab, wl[0].nchunks, wl[0].N, g + off[PAR_B], grad_scale);
-  seg(wl[1].slab, wl[1].nchunks, (int64_t)wl[1].N * wl[1].C * 3, g + off[DEC2_W], nullptr);
-  seg(wl[1].bslab, wl[1].nchunks, wl[1].N, g + off[DEC2_B], nullptr);
-  seg(wl[2].slab, wl[2].nchunks, (int64_t)wl[2].N * wl[2].C * 3, p.dWc, nullptr);
-  seg(wl[2].bslab, wl[2].nchunks, wl[2].N, g + off[DEC1_B], nullptr);
-  seg(wl[3].slab, wl[3].nchunks, (int64_t)wl[3].N * wl[3].C, g + off[LOGIT_W], nullptr);
-  seg(wl[3].bslab, wl[3].nchunks, wl[3].N, g + off[LOGIT_B], nullptr);
-  seg(wl[4].slab, wl[4].nchunks, (int64_t)wl[4].N * wl[4].C * 3, g + off[ENC2_W], nullptr);
-  seg(wl[4].bslab, wl[4].nchunks, wl[4].N, g + off[ENC2_B], nullptr);
-  seg(wl[5].slab, wl[5].nchunks, (int64_t)wl[5].N * wl[5].C * 3, g + off[ENC1_W], nullptr);
-  seg(wl[5].bslab, wl[5].nchunks, wl[5].N, g + off[ENC1_B], nullptr);
-  seg(p.sW1, p.hgrid, (int64_t)p.TH * p.U, g + off[TN0_W], grad_scale);
-  seg(p.sb1, p.hgrid, p.TH, g + off[TN0_B], grad_scale);
-  seg(p.sW2, p.hgrid, (int64_t)p.K * p.K * p.TH, g + off[TN2_W], grad_scale);
-  seg(p.sb2, p.hgrid, (int64_t)p.K * p.K, g + off[TN2_B], grad_scale);
-  seg(p.sq0, p.hgrid, p.K, p.q0sum, nullptr);
-  if ((rc = launch_reduce_slabs(segs, n, s))) return rc;
-  if ((rc = launch_compose_bwd(p.dWc, w[DEC1_W], w[EMB], p.H, p.K, g + off[DEC1_W], g + off[EMB], s))) return rc;
-  return launch_log_prior_grad(p.q0sum, w[LOG_PRIOR], p.K, -beta / (float)B, grad_scale, g + off[LOG_PRIOR], s);
+  double f, b;
+  int m;
+  stage_work(p, stage, &f, &b, &m);
+  if (flops) *flops = f;
+  if (bytes) *bytes = b;
+  if (mfma_bound) *mfma_bound = m;
+  return VQHMM_OK;
+}
+
+int vqhmm_elbo_stage_f32(const vqhmm_dims_t* d, const float* const* w, const float* x, const float* u, int u_layout,
+                         const int64_t* lengths, int64_t B, int64_t T, float beta, void* ws, size_t ws_bytes,
+                         float* grad, int stage, void* stream) {
+  if (!dims_ok(d) || !w || !ws || stage < 0 || stage >= S_COUNT) return VQHMM_EINVAL;
+  ElboPlan p = plan_elbo(d, B, T, ws);
+  if (ws_bytes < p.bytes) return VQHMM_EWORKSPACE;
+  StepCtx c{w, x, u, u_layout, lengths, beta, 1, p.loss, nullptr, nullptr, grad};
+  return run_stage(p, c, stage, (hipStream_t)stream);
 }
 
 int vqhmm_elbo_pieces(const vqhmm_dims_t* d, int64_t B, int64_t T, const void* ws, const float** loss,

@@ -64,7 +64,6 @@ __global__ __launch_bounds__(256) void elbo_head_kernel(HeadArgs a) {
 
   const int tid = threadIdx.x;
   const int K = a.K, KK = K * K, D = a.D;
-  const int64_t Tp = (int64_t)a.T + 2;
   const float cpri = -a.beta / (float)a.B;  // d loss / d (init + trans)[b]
   const float cent = a.beta / (float)a.B;   // d loss / d (sum q*log q)
 

@@ -46,6 +46,12 @@ _SIGS = {
                                          ctypes.POINTER(c_vp)]),
     "vqhmm_adam_f32": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.c_double, ctypes.c_double,
                                       ctypes.c_double, ctypes.c_double, c_vp, c_f32, c_vp]),
+    "vqhmm_elbo_num_stages": (ctypes.c_int, []),
+    "vqhmm_elbo_stage_info": (ctypes.c_int, [ctypes.POINTER(Dims), c_i64, c_i64, ctypes.c_int, ctypes.c_char_p, c_sz,
+                                             ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                             ctypes.POINTER(ctypes.c_int)]),
+    "vqhmm_elbo_stage_f32": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(c_vp), c_vp, c_vp, ctypes.c_int,
+                                            c_vp, c_i64, c_i64, c_f32, c_vp, c_sz, c_vp, ctypes.c_int, c_vp]),
     "vqhmm_infer_workspace_size": (ctypes.c_int, [ctypes.POINTER(Dims), c_i64, c_i64, ctypes.POINTER(c_sz)]),
     "vqhmm_encode_f32": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(c_vp), c_vp, c_i64, c_i64, c_vp,
                                         c_vp, c_sz, c_vp]),
