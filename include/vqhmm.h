@@ -70,6 +70,30 @@ int vqhmm_vq_argmin_f32(const float* z, int64_t B, int64_t Dv, int64_t T,
                         int32_t* idx, float* dmin, void* stream);
 
 
+/* ------------------------------------------------------------ Viterbi ----
+ * MAP state path (semantics math.md:23-67 over Prior.forward's
+ * tables VQ_VAE_HMM_fixed.py:59-71 — no reference code).  log_pi (K),
+ * log_A (B,T,K,K) [t = transition t-1 -> t], em (B,T,K) emission log-potentials,
+ * lengths (B) int64 -> path (B,T) int32 (-1 at t >= length), score (B) fp32.
+ * d_t[j] = (max_i d_{t-1}[i] + log_A[t,i,j]) + em[t,j] in fp32, ties -> lowest i;
+ * last state = first argmax.  Bit-exact vs oracle/c/hmm_oracle.c.  K <= 8.
+ * Workspace: 0 bytes when a sequence's backpointers fit in LDS, else the size
+ * returned by vqhmm_viterbi_workspace_size. */
+size_t vqhmm_viterbi_workspace_size(int64_t B, int64_t T, int64_t K);
+int vqhmm_viterbi_f32(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths,
+                      int64_t B, int64_t T, int64_t K, int32_t* path, float* score, void* workspace,
+                      size_t ws_bytes, void* stream);
+
+/* --------------------------------------------------- forward-backward ----
+ * Posterior marginals: same inputs as Viterbi ->
+ * gamma (B,T,K) fp32 (0 at t >= length), logZ (B) fp32 (NaN if length 0).
+ * Log-space alpha/beta, normalised every step by the max over states.
+ * Accuracy target vs the fp64 oracle: |gamma| abs 1e-5, logZ rel 1e-5.  K <= 8. */
+size_t vqhmm_fwdbwd_workspace_size(int64_t B, int64_t T, int64_t K);
+int vqhmm_fwdbwd_f32(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths,
+                     int64_t B, int64_t T, int64_t K, float* gamma, float* logZ, void* workspace,
+                     size_t ws_bytes, void* stream);
+
 /* ------------------------------------------------------- training step ----
  * compute_loss forward + backward of VAE_HMM (VQ_VAE_HMM_fixed.py:106-137,
  * autograd of :156) as one native executor over hand-written kernels.

@@ -48,6 +48,55 @@ def bench_vq(a):
                       "GBps": byts / t / 1e9, "frac_hbm": byts / t / HBM_PEAK}))
 
 
+def hmm_tables(B, T, K, seed=7):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    log_pi = torch.log_softmax(torch.randn(K, device="cuda", generator=g), -1)
+    log_A = torch.log_softmax(torch.randn(B, T, K, K, device="cuda", generator=g), -1)
+    em = torch.log_softmax(torch.randn(B, T, K, device="cuda", generator=g), -1)
+    L = torch.full((B,), T, dtype=torch.int64, device="cuda")
+    return log_pi, log_A, em, L
+
+
+def bench_viterbi(a):
+    B, T, K = a.B, a.T, a.K
+    log_pi, log_A, em, L = hmm_tables(B, T, K)
+    lib = vqhmm._ext.load()
+    P = vqhmm._ext.ptr
+    st = vqhmm._ext.stream_ptr()
+    path = torch.empty(B, T, dtype=torch.int32, device="cuda")
+    score = torch.empty(B, device="cuda")
+    nb = lib.vqhmm_viterbi_workspace_size(B, T, K)
+    ws = torch.empty(max(nb, 1), dtype=torch.uint8, device="cuda")
+
+    def fn():
+        lib.vqhmm_viterbi_f32(P(log_pi), P(log_A), P(em), P(L), B, T, K, P(path), P(score), P(ws), nb, st)
+
+    t = time_fn(fn, iters=5, warmup=2)
+    byts = B * (4 * T * K * K + 4 * T * K + 4 * T) + 4 * K
+    print(json.dumps({"kernel": "viterbi", "B": B, "T": T, "K": K, "us": t * 1e6, "GBps": byts / t / 1e9,
+                      "frac_hbm": byts / t / HBM_PEAK}))
+
+
+def bench_fwdbwd(a):
+    B, T, K = a.B, a.T, a.K
+    log_pi, log_A, em, L = hmm_tables(B, T, K)
+    lib = vqhmm._ext.load()
+    P = vqhmm._ext.ptr
+    st = vqhmm._ext.stream_ptr()
+    gamma = torch.empty(B, T, K, device="cuda")
+    logZ = torch.empty(B, device="cuda")
+    nb = lib.vqhmm_fwdbwd_workspace_size(B, T, K)
+    ws = torch.empty(max(nb, 1), dtype=torch.uint8, device="cuda")
+
+    def fn():
+        lib.vqhmm_fwdbwd_f32(P(log_pi), P(log_A), P(em), P(L), B, T, K, P(gamma), P(logZ), P(ws), nb, st)
+
+    t = time_fn(fn, iters=5, warmup=2)
+    byts = B * (4 * T * K * K + 4 * T * K + 4 * T * K) + 4 * K
+    print(json.dumps({"kernel": "fwdbwd", "B": B, "T": T, "K": K, "us": t * 1e6, "GBps": byts / t / 1e9,
+                      "frac_hbm": byts / t / HBM_PEAK}))
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("what")
@@ -56,4 +105,4 @@ if __name__ == "__main__":
     ap.add_argument("--T", type=int, default=200)
     ap.add_argument("--K", type=int, default=32)
     a = ap.parse_args()
-    {"vq": bench_vq}[a.what](a)
+    {"vq": bench_vq, "viterbi": bench_viterbi, "fwdbwd": bench_fwdbwd}[a.what](a)

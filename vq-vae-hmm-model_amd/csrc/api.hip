@@ -149,6 +149,31 @@ int vqhmm_vq_argmin_f32(const float* z, int64_t B, int64_t Dv, int64_t T, const 
   return launch_vq_argmin(z, B, Dv, T, codebook, K, idx, dmin, (hipStream_t)stream);
 }
 
+size_t vqhmm_viterbi_workspace_size(int64_t B, int64_t T, int64_t K) {
+  return (B < 0 || T < 0 || K < 1) ? 0 : viterbi_ws_bytes(B, T, K);
+}
+
+int vqhmm_viterbi_f32(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths, int64_t B,
+                      int64_t T, int64_t K, int32_t* path, float* score, void* ws, size_t ws_bytes, void* stream) {
+  if (B < 0 || T < 0 || K < 1 || (B > 0 && (!log_pi || !log_A || !em || !lengths || !path || !score)))
+    return VQHMM_EINVAL;
+  if (B == 0 || T == 0) return VQHMM_OK;
+  return launch_viterbi(log_pi, log_A, em, lengths, B, T, K, path, score, ws, ws_bytes, (hipStream_t)stream);
+}
+
+size_t vqhmm_fwdbwd_workspace_size(int64_t B, int64_t T, int64_t K) {
+  return (B < 0 || T < 0 || K < 1) ? 0 : (size_t)B * T * K * sizeof(float);
+}
+
+int vqhmm_fwdbwd_f32(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths, int64_t B,
+                     int64_t T, int64_t K, float* gamma, float* logZ, void* ws, size_t ws_bytes, void* stream) {
+  if (B < 0 || T < 0 || K < 1 || (B > 0 && (!log_pi || !log_A || !em || !lengths || !gamma || !logZ)))
+    return VQHMM_EINVAL;
+  if (B == 0 || T == 0) return VQHMM_OK;
+  if (!ws) return VQHMM_EWORKSPACE;
+  return launch_fwdbwd(log_pi, log_A, em, lengths, B, T, K, gamma, logZ, ws, ws_bytes, (hipStream_t)stream);
+}
+
 int vqhmm_elbo_workspace_size(const vqhmm_dims_t* d, int64_t B, int64_t T, size_t* bytes) {
   if (!dims_ok(d) || B < 0 || T < 0 || !bytes) return VQHMM_EINVAL;
   *bytes = plan_elbo(d, B, T, nullptr).bytes;

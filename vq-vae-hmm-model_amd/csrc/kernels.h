@@ -111,6 +111,11 @@ int launch_logits_bwd(const float* q, const float* dq_dec, const float* dqx, con
 int launch_log_prior_grad(const float* q0sum, const float* log_prior, int K, float c, const float* scale, float* out,
                           hipStream_t s);
 int launch_log_softmax_vec(const float* x, int K, float* out, hipStream_t s);
+size_t viterbi_ws_bytes(int64_t B, int64_t T, int64_t K);
+int launch_viterbi(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths, int64_t B,
+                   int64_t T, int64_t K, int32_t* path, float* score, void* ws, size_t ws_bytes, hipStream_t s);
+int launch_fwdbwd(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths, int64_t B,
+                  int64_t T, int64_t K, float* gamma, float* logZ, void* ws, size_t ws_bytes, hipStream_t s);
 int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, double lr, double beta1, double beta2,
                 double eps, int64_t* step, float gmul, hipStream_t s);
 

@@ -8,9 +8,9 @@ kernels in libvqhmm.so; there is no CPU fallback.
 """
 from . import _ext  # noqa: F401
 from .data import RandomChunkDataset, collate_fn  # noqa: F401
-from .hmm import quantize, vq_argmin  # noqa: F401
+from .hmm import forward_backward, quantize, viterbi, vq_argmin  # noqa: F401
 from .model import PARAM_ORDER, VAE_HMM, Decoder, Encoder, Prior  # noqa: F401
 from .train import TrainState, train_model  # noqa: F401
 
 __all__ = ["VAE_HMM", "Encoder", "Prior", "Decoder", "train_model", "TrainState", "RandomChunkDataset",
-           "collate_fn", "vq_argmin", "quantize", "PARAM_ORDER"]
+           "collate_fn", "vq_argmin", "quantize", "viterbi", "forward_backward", "PARAM_ORDER"]

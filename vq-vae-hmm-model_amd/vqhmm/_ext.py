@@ -37,6 +37,10 @@ _SIGS = {
     "vqhmm_abi_version": (c_i32, []),
     "vqhmm_param_layout": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(c_i64)]),
     "vqhmm_vq_argmin_f32": (ctypes.c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "vqhmm_viterbi_workspace_size": (c_sz, [c_i64, c_i64, c_i64]),
+    "vqhmm_viterbi_f32": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_sz, c_vp]),
+    "vqhmm_fwdbwd_workspace_size": (c_sz, [c_i64, c_i64, c_i64]),
+    "vqhmm_fwdbwd_f32": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "vqhmm_elbo_workspace_size": (ctypes.c_int, [ctypes.POINTER(Dims), c_i64, c_i64, ctypes.POINTER(c_sz)]),
     "vqhmm_elbo_fwd_f32": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(c_vp), c_vp, c_vp, ctypes.c_int,
                                           c_vp, c_i64, c_i64, c_f32, ctypes.c_int, c_vp, c_sz, c_vp, c_vp, c_vp]),

@@ -47,3 +47,50 @@ def quantize(z, codebook, beta=0.25):
     commit = beta * torch.mean((z - z_q.detach()) ** 2)
     cb_loss = torch.mean((z_q - z.detach()) ** 2)
     return z_q_st, idx, commit, cb_loss
+
+
+def _hmm_inputs(log_pi, log_A, em, lengths):
+    _ext.require_device(log_pi, log_A, em)
+    if log_A.dim() != 4 or em.dim() != 3 or log_A.shape[:2] != em.shape[:2] or log_A.shape[2:] != (em.shape[2],) * 2:
+        raise ValueError(f"expected log_A (B,T,K,K) and em (B,T,K), got {tuple(log_A.shape)} {tuple(em.shape)}")
+    B, T, K = em.shape
+    if log_pi.shape != (K,):
+        raise ValueError(f"log_pi must have shape ({K},)")
+    if lengths is None:
+        lengths = torch.full((B,), T, dtype=torch.int64, device=em.device)
+    lengths = torch.as_tensor(lengths).to(em.device, torch.int64).contiguous()
+    return (log_pi.contiguous().float(), log_A.contiguous().float(), em.contiguous().float(), lengths, B, T, K)
+
+
+def viterbi(log_pi, log_A, em, lengths=None):
+    """MAP state path under the Prior's tables.
+
+    log_pi (K,), log_A (B,T,K,K) with log_A[:, t] the t-1 -> t transition
+    (as Prior.forward returns it, VQ_VAE_HMM_fixed.py:69-71), em (B,T,K)
+    emission log-potentials, lengths (B,) -> path (B,T) int32 (-1 past the
+    length), score (B,) fp32.  Bit-exact vs the fp32 oracle contract.
+    """
+    log_pi, log_A, em, lengths, B, T, K = _hmm_inputs(log_pi, log_A, em, lengths)
+    path = torch.empty((B, T), dtype=torch.int32, device=em.device)
+    score = torch.empty((B,), dtype=torch.float32, device=em.device)
+    lib = _ext.load()
+    nb = lib.vqhmm_viterbi_workspace_size(B, T, K)
+    ws = torch.empty(max(nb, 1), dtype=torch.uint8, device=em.device)
+    _ext.check(lib.vqhmm_viterbi_f32(_ext.ptr(log_pi), _ext.ptr(log_A), _ext.ptr(em), _ext.ptr(lengths), B, T, K,
+                                     _ext.ptr(path), _ext.ptr(score), _ext.ptr(ws), nb, _ext.stream_ptr(em.device)),
+               "viterbi")
+    return path, score
+
+
+def forward_backward(log_pi, log_A, em, lengths=None):
+    """Posterior state marginals gamma (B,T,K) and log-partition logZ (B,)."""
+    log_pi, log_A, em, lengths, B, T, K = _hmm_inputs(log_pi, log_A, em, lengths)
+    gamma = torch.empty((B, T, K), dtype=torch.float32, device=em.device)
+    logZ = torch.empty((B,), dtype=torch.float32, device=em.device)
+    lib = _ext.load()
+    nb = lib.vqhmm_fwdbwd_workspace_size(B, T, K)
+    ws = torch.empty(max(nb, 1), dtype=torch.uint8, device=em.device)
+    _ext.check(lib.vqhmm_fwdbwd_f32(_ext.ptr(log_pi), _ext.ptr(log_A), _ext.ptr(em), _ext.ptr(lengths), B, T, K,
+                                    _ext.ptr(gamma), _ext.ptr(logZ), _ext.ptr(ws), nb, _ext.stream_ptr(em.device)),
+               "forward_backward")
+    return gamma, logZ
