@@ -101,7 +101,7 @@ ElboPlan plan_elbo(const vqhmm_dims_t* d, int64_t B, int64_t T, void* ws) {
     WLayer& w = p.wl[i];
     w.N = shapes[i][0]; w.C = shapes[i][1]; w.ks = shapes[i][2];
     const int64_t tiles = cdiv(w.N, 64) * cdiv(w.C, 64);
-    w.rows = wgrad_chunks(R, tiles);
+    w.rows = (w.N <= 64 && w.C <= 64) ? wgrad2_rows(R, w.N, w.C, w.ks) : wgrad_chunks(R, tiles);
     w.nchunks = cdiv(R, w.rows);
     w.slab = c.take<float>((size_t)w.nchunks * w.N * w.C * w.ks);
     w.bslab = c.take<float>((size_t)w.nchunks * w.N);

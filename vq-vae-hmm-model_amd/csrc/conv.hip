@@ -234,6 +234,7 @@ static int launch_conv_cfg(const ConvArgs& a, hipStream_t s) {
 int launch_conv(const ConvArgs& a, hipStream_t s) {
   if (a.R == 0) return VQHMM_OK;
   if (!a.src || !a.W || a.Kc <= 0 || a.N <= 0 || (a.ks != 1 && a.ks != 3)) return VQHMM_EINVAL;
+  if (conv2_supported(a)) return launch_conv2(a, s);
   const bool wide = a.Kc > 16;
   if (a.N <= 16) return wide ? launch_conv_cfg<4, 1, 4, 1, 32>(a, s) : launch_conv_cfg<4, 1, 4, 1, 16>(a, s);
   if (a.N <= 32) return wide ? launch_conv_cfg<4, 1, 4, 2, 32>(a, s) : launch_conv_cfg<4, 1, 4, 2, 16>(a, s);
@@ -363,6 +364,7 @@ int launch_wgrad(const WgradArgs& a0, hipStream_t s) {
   WgradArgs a = a0;
   if (a.R == 0) return VQHMM_OK;
   if (!a.dy || !a.x || !a.slab || (a.ks != 1 && a.ks != 3) || a.rows_per_chunk % 64) return VQHMM_EINVAL;
+  if (wgrad2_supported(a)) return launch_wgrad2(a, s);
   const int64_t nchunks = cdiv(a.R, a.rows_per_chunk);
   constexpr int TN = 64, TC = 64;
   const dim3 grid((unsigned)(cdiv(a.N, TN) * cdiv(a.C, TC)), (unsigned)nchunks);

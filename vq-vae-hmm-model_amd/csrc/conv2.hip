@@ -1,0 +1,318 @@
+// Conv1d forward / data-gradient for the small-channel regime of the training
+// path (N <= 64 output channels, Kc <= 64 input channels: BASELINE cfg2, cfg4),
+// replacing the generic conv_mm_kernel there.
+//
+//  * Persistent workgroups: the whole (tap, n, c) weight tile is staged in LDS
+//    ONCE per workgroup (transposed/flipped for the data gradient) and the
+//    workgroup walks row tiles of 4*PB*16 PCL rows with stride gridDim.x.
+//  * The next tile's input rows are prefetched into registers (float4 loads,
+//    clamped + selected, no branches) while the MFMAs of the current tile run.
+//  * The product is computed transposed, Y^T (N x rows) = W (N x 3Kc) @ Xwin^T,
+//    so an accumulator fragment holds 4 consecutive channels of one row:
+//    epilogue stores are float4, and the fused 1x1 tail (to_logits /
+//    to_params, + softmax) consumes the fragments directly as its MFMA B
+//    operand (contraction over the fragment's row index), with no LDS round trip.
+#include "kernels.h"
+
+namespace vqhmm {
+
+namespace {
+
+template <int NB, int KCP, int KS, int PB>
+struct C2Cfg {
+  static constexpr int BM = 4 * PB * 16;       // rows per tile
+  static constexpr int KCW = KCP * 16;         // padded input channels
+  static constexpr int LDX = KCW + 4;          // LDS row stride (conflict-free float4 reads)
+  static constexpr int NW = NB * 16;           // padded output channels
+  static constexpr int XROWS = BM + 2;
+  static constexpr int XF4 = XROWS * KCW / 4;  // float4 slots of one X tile
+  static constexpr int PF = (XF4 + 255) / 256; // float4 slots per thread
+  static constexpr size_t W_FLOATS = (size_t)KS * NW * LDX;
+  static constexpr size_t X_FLOATS = (size_t)XROWS * LDX;
+  static constexpr size_t LDS = (W_FLOATS + X_FLOATS) * 4;
+};
+
+// Gather the float4 slot `s` of an X tile starting at PCL row m0-1 (zeros outside / in padding).
+__device__ __forceinline__ float4 x_slot(const ConvArgs& a, int64_t m0, int s, int kcw, bool vec) {
+  const int q4 = kcw / 4;
+  const int row = s / q4, c = (s - row * q4) * 4;
+  const int64_t r = m0 - 1 + row;
+  const bool rin = r >= 0 && r < a.R;
+  const int64_t rc = rin ? r : 0;
+  float4 v;
+  if (a.src_cf) {
+    const int64_t Tp = (int64_t)a.T + 2;
+    const int64_t b = rc / Tp;
+    const int t = (int)(rc - b * Tp) - 1;
+    const bool tin = rin && t >= 0 && t < a.T;
+    const int tc = tin ? t : 0;
+    float e[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const bool ok = tin && c + k < a.Kc;
+      const float val = a.src[(b * a.Kc + (ok ? c + k : 0)) * a.T + tc];
+      e[k] = ok ? val : 0.f;
+    }
+    v = make_float4(e[0], e[1], e[2], e[3]);
+  } else if (vec) {
+    const bool ok = rin && c < a.Kc;
+    const float4 val = *reinterpret_cast<const float4*>(a.src + rc * a.Kc + (ok ? c : 0));
+    v = ok ? val : make_float4(0.f, 0.f, 0.f, 0.f);
+  } else {
+    float e[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const bool ok = rin && c + k < a.Kc;
+      const float val = a.src[rc * a.Kc + (ok ? c + k : 0)];
+      e[k] = ok ? val : 0.f;
+    }
+    v = make_float4(e[0], e[1], e[2], e[3]);
+  }
+  return v;
+}
+
+}  // namespace
+
+template <int NB, int KCP, int KS, int PB>
+__global__ __launch_bounds__(256, 1) void conv2_kernel(ConvArgs a, int64_t ntiles) {
+  using C = C2Cfg<NB, KCP, KS, PB>;
+  extern __shared__ float4 smem4[];
+  float* Ws = reinterpret_cast<float*>(smem4);  // [KS][NW][LDX]
+  float* Xs = Ws + C::W_FLOATS;                 // [XROWS][LDX]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lg4 = lane >> 4, l16 = lane & 15;
+  const bool vec = !a.src_cf && (a.Kc % 4 == 0);
+
+  // ---- weights once: Ws[tap][n][c] = Weff(n, c, tap)
+  for (int i = tid; i < KS * C::NW * C::KCW; i += 256) {
+    const int c = i % C::KCW, n = (i / C::KCW) % C::NW, tap = i / (C::KCW * C::NW);
+    float v = 0.f;
+    if (n < a.N && c < a.Kc)
+      v = a.w_dgrad ? a.W[((int64_t)c * a.N + n) * KS + (KS - 1 - tap)] : a.W[((int64_t)n * a.Kc + c) * KS + tap];
+    Ws[(tap * C::NW + n) * C::LDX + c] = v;
+  }
+  // ---- per-lane epilogue constants
+  float bias_r[NB][4];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int n = nb * 16 + 4 * lg4 + v;
+      bias_r[nb][v] = (a.bias && n < a.N) ? a.bias[n] : 0.f;
+    }
+  const bool tail = a.tW != nullptr;
+  float tw[NB][4];
+  f32x4 tb0 = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (tail) {
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int n = nb * 16 + 4 * lg4 + v;
+        tw[nb][v] = (l16 < a.C2 && n < a.N) ? a.tW[(int64_t)l16 * a.N + n] : 0.f;
+      }
+#pragma unroll
+    for (int v = 0; v < 4; ++v) tb0[v] = (a.tb && 4 * lg4 + v < a.C2) ? a.tb[4 * lg4 + v] : 0.f;
+  }
+  const float sc = a.scale ? *a.scale : 1.0f;
+
+  int64_t tile = blockIdx.x;
+  float4 pf[C::PF];
+#pragma unroll
+  for (int k = 0; k < C::PF; ++k) {
+    const int s = tid + k * 256;
+    pf[k] = (s < C::XF4) ? x_slot(a, tile * C::BM, s < C::XF4 ? s : 0, C::KCW, vec) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  while (tile < ntiles) {
+    const int64_t m0 = tile * C::BM;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < C::PF; ++k) {
+      const int s = tid + k * 256;
+      if (s < C::XF4) {
+        const int row = s / (C::KCW / 4), c = (s - row * (C::KCW / 4)) * 4;
+        *reinterpret_cast<float4*>(Xs + row * C::LDX + c) = pf[k];
+      }
+    }
+    __syncthreads();
+    // epilogue operands of THIS tile first (older than the prefetch in the vmcnt order)
+    float4 auxv[NB][PB];
+    if (a.act == 2) {
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+        for (int pb = 0; pb < PB; ++pb) {
+          const int64_t r = m0 + (wave * PB + pb) * 16 + l16;
+          const int n0 = nb * 16 + 4 * lg4;
+          const bool ok = r < a.R && n0 < a.N;
+          auxv[nb][pb] = *reinterpret_cast<const float4*>(a.aux + (ok ? r : 0) * a.N + (ok ? n0 : 0));
+        }
+    }
+    const int64_t next = tile + gridDim.x;
+    if (next < ntiles) {
+#pragma unroll
+      for (int k = 0; k < C::PF; ++k) {
+        const int s = tid + k * 256;
+        if (s < C::XF4) pf[k] = x_slot(a, next * C::BM, s, C::KCW, vec);
+      }
+    }
+    // ---- MFMA: acc[nb][pb] = Y^T block (16 n x 16 rows)
+    f32x4 acc[NB][PB];
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int pb = 0; pb < PB; ++pb) acc[nb][pb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int tap = 0; tap < KS; ++tap) {
+      const int rowoff = (KS == 3) ? tap : 1;
+#pragma unroll
+      for (int kk = 0; kk < KCP; ++kk) {
+        const int col = kk * 16 + 4 * lg4;
+        float4 av[NB], bv[PB];
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+          av[nb] = *reinterpret_cast<const float4*>(Ws + (tap * C::NW + nb * 16 + l16) * C::LDX + col);
+#pragma unroll
+        for (int pb = 0; pb < PB; ++pb)
+          bv[pb] = *reinterpret_cast<const float4*>(Xs + ((wave * PB + pb) * 16 + l16 + rowoff) * C::LDX + col);
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+          for (int pb = 0; pb < PB; ++pb) {
+            acc[nb][pb] = mfma16x16x4(av[nb].x, bv[pb].x, acc[nb][pb]);
+            acc[nb][pb] = mfma16x16x4(av[nb].y, bv[pb].y, acc[nb][pb]);
+            acc[nb][pb] = mfma16x16x4(av[nb].z, bv[pb].z, acc[nb][pb]);
+            acc[nb][pb] = mfma16x16x4(av[nb].w, bv[pb].w, acc[nb][pb]);
+          }
+      }
+    }
+    // ---- epilogue: lane (lg4, l16) holds channels nb*16 + 4*lg4 + v of row m0 + (wave*PB+pb)*16 + l16
+#pragma unroll
+    for (int pb = 0; pb < PB; ++pb) {
+      const int64_t r = m0 + (wave * PB + pb) * 16 + l16;
+      int64_t b;
+      int t;
+      const bool valid = row_bt(r, a.R, a.T, b, t);
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        f32x4 y;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          float yy = acc[nb][pb][v] * sc + bias_r[nb][v];
+          if (a.act == 1) yy = fmaxf(yy, 0.f);
+          else if (a.act == 2) yy = (v == 0 ? auxv[nb][pb].x : v == 1 ? auxv[nb][pb].y : v == 2 ? auxv[nb][pb].z
+                                                                                                 : auxv[nb][pb].w) > 0.f
+                                        ? yy
+                                        : 0.f;
+          y[v] = valid ? yy : 0.f;
+        }
+        acc[nb][pb] = y;
+        const int n0 = nb * 16 + 4 * lg4;
+        if (a.out && r < a.R) {
+          if ((a.N & 3) == 0) {
+            if (n0 < a.N) *reinterpret_cast<f32x4*>(a.out + r * a.N + n0) = y;
+          } else {
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+              if (n0 + v < a.N) a.out[r * a.N + n0 + v] = y[v];
+          }
+        }
+        if (a.out_cf && valid) {
+#pragma unroll
+          for (int v = 0; v < 4; ++v)
+            if (n0 + v < a.N) a.out_cf[(b * a.N + n0 + v) * a.T + t] = y[v];
+        }
+      }
+      if (tail) {
+        // z^T (16 c2 x 16 rows) = tW (16 x N) @ Y^T: B operand = the fragments above
+        f32x4 z = tb0;
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) z = mfma16x16x4(tw[nb][v], acc[nb][pb][v], z);
+        // lane holds c2 = 4*lg4 + v of row r
+        const int c0 = 4 * lg4;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) z[v] = valid ? z[v] : 0.f;
+        if (a.t_out && r < a.R) {
+#pragma unroll
+          for (int v = 0; v < 4; ++v)
+            if (c0 + v < a.C2) a.t_out[r * a.C2 + c0 + v] = z[v];
+        }
+        if (a.t_cf0 && valid) {
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            const int c2 = c0 + v;
+            if (c2 < a.t_split) a.t_cf0[(b * a.t_split + c2) * a.T + t] = z[v];
+            else if (c2 < a.C2) a.t_cf1[(b * (a.C2 - a.t_split) + c2 - a.t_split) * a.T + t] = z[v];
+          }
+        }
+        if (a.q_out || a.q_cf) {
+          float m = -__builtin_inff();
+#pragma unroll
+          for (int v = 0; v < 4; ++v)
+            if (c0 + v < a.C2) m = fmaxf(m, z[v]);
+          m = fmaxf(m, __shfl_xor(m, 16));
+          m = fmaxf(m, __shfl_xor(m, 32));
+          float e[4], s = 0.f;
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            e[v] = (c0 + v < a.C2) ? __expf(z[v] - m) : 0.f;
+            s += e[v];
+          }
+          s += __shfl_xor(s, 16);
+          s += __shfl_xor(s, 32);
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            const int c2 = c0 + v;
+            if (c2 < a.C2) {
+              const float qv = valid ? e[v] / s : 0.f;
+              if (a.q_out && r < a.R) a.q_out[r * a.C2 + c2] = qv;
+              if (a.q_cf && valid) a.q_cf[(b * a.C2 + c2) * a.T + t] = qv;
+            }
+          }
+        }
+      }
+    }
+    tile = next;
+  }
+}
+
+bool conv2_supported(const ConvArgs& a) {
+  return a.N <= 64 && a.Kc <= 64 && (a.tW == nullptr || a.C2 <= 16);
+}
+
+template <int NB, int KCP, int KS>
+static int launch_c2(const ConvArgs& a, hipStream_t s) {
+  constexpr int PB = 2;
+  using C = C2Cfg<NB, KCP, KS, PB>;
+  const int64_t ntiles = cdiv(a.R, C::BM);
+  int per_cu = (int)((160 * 1024) / C::LDS);
+  if (per_cu < 1) return VQHMM_EUNSUPPORTED;
+  if (per_cu > 2) per_cu = 2;
+  const int64_t grid = ntiles < 256LL * per_cu ? ntiles : 256LL * per_cu;
+  conv2_kernel<NB, KCP, KS, PB><<<(unsigned)grid, 256, C::LDS, s>>>(a, ntiles);
+  VQHMM_LAUNCH_CHECK();
+  return VQHMM_OK;
+}
+
+template <int NB, int KS>
+static int launch_c2_k(const ConvArgs& a, hipStream_t s) {
+  if (a.Kc <= 16) return launch_c2<NB, 1, KS>(a, s);
+  if (a.Kc <= 32) return launch_c2<NB, 2, KS>(a, s);
+  return launch_c2<NB, 4, KS>(a, s);
+}
+
+template <int KS>
+static int launch_c2_n(const ConvArgs& a, hipStream_t s) {
+  if (a.N <= 16) return launch_c2_k<1, KS>(a, s);
+  if (a.N <= 32) return launch_c2_k<2, KS>(a, s);
+  return launch_c2_k<4, KS>(a, s);
+}
+
+int launch_conv2(const ConvArgs& a, hipStream_t s) {
+  if (a.R == 0) return VQHMM_OK;
+  return a.ks == 3 ? launch_c2_n<3>(a, s) : launch_c2_n<1>(a, s);
+}
+
+}  // namespace vqhmm

@@ -370,13 +370,14 @@ __global__ __launch_bounds__(256) void elbo_head_kernel(HeadArgs a) {
 
 int head_grid(int64_t R) {
   const int64_t ntiles = cdiv(R, HP);
-  return (int)(ntiles < 512 ? ntiles : 512);
+  return (int)(ntiles < 256 ? ntiles : 256);
 }
 
 int launch_head(const HeadArgs& a0, int grid, hipStream_t s) {
   HeadArgs a = a0;
   a.ntiles = cdiv(a.R, HP);
   if (a.R == 0) return VQHMM_OK;
+  if (head_mfma_supported(a)) return launch_head_mfma(a, grid, s);
   if (a.K > 8 || a.U > 8 || a.TH > 256 || a.D > 16) return VQHMM_EUNSUPPORTED;
   if (a.K <= 4)
     elbo_head_kernel<4, 8><<<grid, 256, 0, s>>>(a);

@@ -1,0 +1,443 @@
+// Fused ELBO head, MFMA version (K <= 4, TH in {64, 128}, U <= 7): the same
+// math as head.hip (VQ_VAE_HMM_fixed.py:59-71 Prior MLP, :106-137 loss) with
+// the Prior MLP forward and backward on v_mfma_f32_16x16x4_f32.
+//
+// Tile = 256 PCL rows (255 owned + 1 halo row whose log_A the last owned row
+// needs for its t -> t+1 transition); 4 waves, wave w owns row blocks
+// 4w..4w+3 of 16 rows.  Per 16-row block:
+//   phase A  hid^T (TH x 16) = relu(W1' (TH x 8) @ u'^T (8 x 16))      u' = [u, 1], W1' = [W1, b1]
+//            lg^T  (16 x 16) = W2 (16 x TH) @ hid^T + b2               (hid^T accumulator
+//            fragments are the B operand as they stand: rows h = 4*(l>>4)+v)
+//   phase B  VALU, thread per row: log_softmax -> log_A, recon NLL, entropy,
+//            init/transition terms, dq, d log_A -> d lg (log_softmax backward)
+//   phase C  dhid^T = W2^T @ dlg^T, masked by relu'(hid^T);
+//            gW2' (16 x TH+16) += dlg^T @ [hid | 1]   (the ones column gives db2)
+//            gW1' (TH x 16)   += dhid^T @ u'           (column U gives db1)
+//            hid and dhid cross LDS once (a 16-row transpose) for the two
+//            contractions over rows.
+// Weight-gradient accumulators stay in registers across all tiles of the
+// workgroup; the 4 waves are summed in fixed order at the end (deterministic).
+#include "kernels.h"
+
+namespace vqhmm {
+
+namespace {
+constexpr int MP = 256;   // rows per tile (incl. halo)
+constexpr int MOWN = 255; // owned rows
+
+template <int K, int HB>
+struct HeadLds {
+  static constexpr int TH = HB * 16;
+  static constexpr int LDW2 = TH + 4;   // W2S row stride: 4*LDW2 = 16 (mod 32) -> conflict-free
+  static constexpr int LDH = TH + 16;   // hS / dhS row stride (= 16 mod 32)
+  float W2S[16 * LDW2];
+  float uS[MP * 8];
+  float lgS[MP * 16];
+  float dlgS[MP * 16];
+  float qS[(MP + 2) * 4];
+  int wS[MP + 2];
+  float hS[4][16 * LDH];
+  float dhS[4][16 * LDH];
+  float lpS[4];
+  unsigned long long cnt;
+};
+}  // namespace
+
+template <int K, int HB>
+__global__ __launch_bounds__(256, 1) void elbo_head_mfma_kernel(HeadArgs a) {
+  constexpr int KK = K * K;
+  constexpr int TH = HB * 16;
+  using S = HeadLds<K, HB>;
+  extern __shared__ float4 smem4[];
+  S& sh = *reinterpret_cast<S*>(smem4);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lg4 = lane >> 4, l16 = lane & 15;
+  const int U = a.U, D = a.D;
+  const float cpri = -a.beta / (float)a.B;
+  const float cent = a.beta / (float)a.B;
+
+  // ---- one-time: weights to LDS / registers, log_pi, valid count
+  for (int i = tid; i < 16 * S::LDW2; i += 256) {
+    const int ij = i / S::LDW2, h = i - ij * S::LDW2;
+    sh.W2S[i] = (ij < KK && h < TH) ? a.W2[ij * TH + h] : 0.f;
+  }
+  if (tid == 0) {
+    float m = -__builtin_inff();
+    for (int k = 0; k < K; ++k) m = fmaxf(m, a.log_prior[k]);
+    float s = 0.f;
+    for (int k = 0; k < K; ++k) s += __expf(a.log_prior[k] - m);
+    const float l = m + __logf(s);
+    for (int k = 0; k < K; ++k) sh.lpS[k] = a.log_prior[k] - l;
+    sh.cnt = 0;
+  }
+  // A fragments of W1' (hid^T = W1' u'^T): lane (i = h, k = c')   [2 k-steps of 4]
+  float w1f[HB][2];
+#pragma unroll
+  for (int hb = 0; hb < HB; ++hb)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int h = hb * 16 + l16, c = ks * 4 + lg4;
+      w1f[hb][ks] = c < U ? a.W1[h * U + c] : (c == U ? a.b1[h] : 0.f);
+    }
+  // A fragments of W2 for lg^T: lane (i = ij, k = h = hb*16 + 4*lg4 + v)
+  float w2f[HB][4];
+#pragma unroll
+  for (int hb = 0; hb < HB; ++hb)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) w2f[hb][v] = l16 < KK ? a.W2[l16 * TH + hb * 16 + 4 * lg4 + v] : 0.f;
+  f32x4 b2f;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) b2f[v] = (4 * lg4 + v) < KK ? a.b2[4 * lg4 + v] : 0.f;
+  __syncthreads();
+  {
+    unsigned long long c = 0;
+    for (int64_t b = tid; b < a.B; b += 256) {
+      const int64_t L = a.lengths[b];
+      c += (unsigned long long)(L <= 0 ? 0 : (L < a.T ? L : a.T));
+    }
+    atomicAdd(&sh.cnt, c);
+  }
+  // per-wave constant ones block of hS (h in [TH, TH+16): column TH = 1)
+  for (int i = lane; i < 16 * 16; i += 64) sh.hS[wave][(i >> 4) * S::LDH + TH + (i & 15)] = (i & 15) == 0 ? 1.f : 0.f;
+  __syncthreads();
+  const float inv_n = 1.0f / fmaxf((float)(sh.cnt * (unsigned long long)D), 1.0f);
+
+  float s_rec = 0.f, s_ent = 0.f, s_tr = 0.f, s_init = 0.f;
+  float q0acc[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) q0acc[k] = 0.f;
+  f32x4 gW2[HB + 1], gW1[HB];
+#pragma unroll
+  for (int i = 0; i <= HB; ++i) gW2[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < HB; ++i) gW1[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int64_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+    const int64_t r0 = tile * MOWN;
+    __syncthreads();
+    // ---------------- L: per-row loads (thread = row r0 + tid)
+    {
+      const int64_t r = r0 + tid;
+      int64_t b;
+      int t;
+      const bool valid = row_bt(r, a.R, a.T, b, t);
+      const int64_t L = valid ? a.lengths[b] : 0;
+      sh.wS[tid + 1] = (valid && t >= 1 && t < L) ? 1 : 0;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        float v = 0.f;
+        if (c < U) v = valid ? a.u[b * (int64_t)U * a.T + c * a.u_sc + t * a.u_st] : 0.f;
+        if (c == U) v = 1.f;
+        sh.uS[tid * 8 + c] = v;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) sh.qS[(tid + 1) * 4 + k] = (valid && k < K) ? a.q[r * K + k] : 0.f;
+      if (tid == 0) {
+        const int64_t rp = r0 - 1;
+        int64_t bp;
+        int tp;
+        const bool vp = row_bt(rp, a.R, a.T, bp, tp);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) sh.qS[k] = (vp && k < K) ? a.q[rp * K + k] : 0.f;
+        sh.wS[0] = (vp && tp >= 1 && tp < a.lengths[bp]) ? 1 : 0;
+      }
+    }
+    __syncthreads();
+    // ---------------- A: MLP forward (MFMA), lg^T -> lgS[p][ij]
+    for (int pbi = 0; pbi < 4; ++pbi) {
+      const int p0 = (wave * 4 + pbi) * 16;
+      const float ub0 = sh.uS[(p0 + l16) * 8 + lg4];
+      const float ub1 = sh.uS[(p0 + l16) * 8 + 4 + lg4];
+      f32x4 lg = b2f;
+#pragma unroll
+      for (int hb = 0; hb < HB; ++hb) {
+        f32x4 h = f32x4{0.f, 0.f, 0.f, 0.f};
+        h = mfma16x16x4(w1f[hb][0], ub0, h);
+        h = mfma16x16x4(w1f[hb][1], ub1, h);
+#pragma unroll
+        for (int v = 0; v < 4; ++v) h[v] = fmaxf(h[v], 0.f);
+#pragma unroll
+        for (int v = 0; v < 4; ++v) lg = mfma16x16x4(w2f[hb][v], h[v], lg);
+      }
+      *reinterpret_cast<f32x4*>(&sh.lgS[(p0 + l16) * 16 + 4 * lg4]) = lg;
+    }
+    __syncthreads();
+    // ---------------- B1: log_softmax rows -> log_A (in place); recon, entropy, init
+    {
+      const int p = tid;
+      const int64_t r = r0 + p;
+      int64_t b;
+      int t;
+      const bool valid = row_bt(r, a.R, a.T, b, t);
+      float* la = &sh.lgS[p * 16];
+#pragma unroll
+      for (int i = 0; i < K; ++i) {
+        float m = la[i * K];
+#pragma unroll
+        for (int j = 1; j < K; ++j) m = fmaxf(m, la[i * K + j]);
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < K; ++j) s += __expf(la[i * K + j] - m);
+        const float ls = m + __logf(s);
+#pragma unroll
+        for (int j = 0; j < K; ++j) la[i * K + j] -= ls;
+      }
+      if (p < MOWN && r < a.R) {
+        const int64_t L = valid ? a.lengths[b] : 0;
+        const bool m = valid && t < L;
+        for (int c = 0; c < D; ++c) {
+          float dmu = 0.f, dlv = 0.f;
+          if (m) {
+            const float mu = a.par[r * 2 * D + c];
+            const float lv = a.par[r * 2 * D + D + c];
+            const float xv = a.x[(b * D + c) * a.T + t];
+            const float ev = __expf(lv);
+            const float var = fmaxf(ev, 1e-8f);
+            const float df = mu - xv;
+            const float r2 = df * df / var;
+            s_rec += 0.5f * (__logf(6.2831855f * var) + r2);
+            dmu = df / var * inv_n;
+            dlv = (ev >= 1e-8f) ? 0.5f * (1.f - r2) * inv_n : 0.f;
+          }
+          if (a.need_grad) {
+            a.dpar[r * 2 * D + c] = dmu;
+            a.dpar[r * 2 * D + D + c] = dlv;
+          }
+        }
+        float lgv[K], qv[K];
+        float mx = -__builtin_inff();
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          lgv[k] = valid ? a.logits[r * K + k] : 0.f;
+          qv[k] = sh.qS[(p + 1) * 4 + k];
+          mx = fmaxf(mx, lgv[k]);
+        }
+        float se = 0.f;
+#pragma unroll
+        for (int k = 0; k < K; ++k) se += __expf(lgv[k] - mx);
+        const float lse = mx + __logf(se);
+        float f = 0.f;
+#pragma unroll
+        for (int k = 0; k < K; ++k) f = fmaf(qv[k], lgv[k] - lse, f);
+        if (m) s_ent -= f;
+        if (a.need_grad) {
+#pragma unroll
+          for (int k = 0; k < K; ++k) a.dlx[r * K + k] = m ? cent * qv[k] * ((lgv[k] - lse) - f) : 0.f;
+        }
+        if (valid && t == 0) {
+#pragma unroll
+          for (int k = 0; k < K; ++k) {
+            s_init = fmaf(qv[k], sh.lpS[k], s_init);
+            q0acc[k] += qv[k];
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // ---------------- B2: transitions, dq, d lg (log_softmax backward) -> dlgS
+    {
+      const int p = tid;
+      const int64_t r = r0 + p;
+      float* dl = &sh.dlgS[p * 16];
+      if (p < MOWN && r < a.R) {
+        const float* qp = &sh.qS[p * 4];
+        const float* qc = &sh.qS[(p + 1) * 4];
+        const float* qn = &sh.qS[(p + 2) * 4];
+        const float* la = &sh.lgS[p * 16];
+        const float* lan = &sh.lgS[(p + 1) * 16];
+        const float w = (float)sh.wS[p + 1];
+        const float wn = (float)sh.wS[p + 2];
+        float tr = 0.f;
+        float dq[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) dq[j] = 0.f;
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+          float rs = 0.f;
+          float dla[K];
+#pragma unroll
+          for (int j = 0; j < K; ++j) {
+            const float l = la[i * K + j];
+            tr = fmaf(qp[i] * qc[j], l, tr);
+            dq[j] = fmaf(qp[i], l, dq[j]);
+            dla[j] = cpri * w * qp[i] * qc[j];
+            rs += dla[j];
+          }
+#pragma unroll
+          for (int j = 0; j < K; ++j) dl[i * K + j] = dla[j] - __expf(la[i * K + j]) * rs;
+        }
+#pragma unroll
+        for (int ij = KK; ij < 16; ++ij) dl[ij] = 0.f;
+        s_tr += w * tr;
+        if (a.need_grad) {
+          int64_t b;
+          int t;
+          const bool valid = row_bt(r, a.R, a.T, b, t);
+#pragma unroll
+          for (int j = 0; j < K; ++j) {
+            float nx = 0.f;
+#pragma unroll
+            for (int jj = 0; jj < K; ++jj) nx = fmaf(qn[jj], lan[j * K + jj], nx);
+            float v = cpri * (w * dq[j] + wn * nx);
+            if (valid && t == 0) v = fmaf(cpri, sh.lpS[j], v);
+            a.dqx[r * K + j] = valid ? v : 0.f;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int ij = 0; ij < 16; ++ij) dl[ij] = 0.f;
+      }
+    }
+    if (!a.need_grad) continue;
+    __syncthreads();
+    // ---------------- C: MLP backward (MFMA)
+    float* hS = sh.hS[wave];
+    float* dhS = sh.dhS[wave];
+    for (int pbi = 0; pbi < 4; ++pbi) {
+      const int p0 = (wave * 4 + pbi) * 16;
+      const float ub0 = sh.uS[(p0 + l16) * 8 + lg4];
+      const float ub1 = sh.uS[(p0 + l16) * 8 + 4 + lg4];
+      const f32x4 dlb = *reinterpret_cast<const f32x4*>(&sh.dlgS[(p0 + l16) * 16 + 4 * lg4]);
+#pragma unroll
+      for (int hb = 0; hb < HB; ++hb) {
+        f32x4 h = f32x4{0.f, 0.f, 0.f, 0.f};
+        h = mfma16x16x4(w1f[hb][0], ub0, h);
+        h = mfma16x16x4(w1f[hb][1], ub1, h);
+        // dhid^T block: A[i = h][k = ij = 4*lg4 + s] = W2[ij][h], B[k][j = p] = dlg[p][ij]
+        f32x4 dh = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          dh = mfma16x16x4(sh.W2S[(4 * lg4 + s) * S::LDW2 + hb * 16 + l16], dlb[s], dh);
+        f32x4 hr, dm;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          hr[v] = fmaxf(h[v], 0.f);
+          dm[v] = h[v] > 0.f ? dh[v] : 0.f;
+        }
+        *reinterpret_cast<f32x4*>(&hS[l16 * S::LDH + hb * 16 + 4 * lg4]) = hr;
+        *reinterpret_cast<f32x4*>(&dhS[l16 * S::LDH + hb * 16 + 4 * lg4]) = dm;
+      }
+      // contractions over the 16 rows of the block (k = p = 4*s + lg4)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int pr = 4 * s + lg4;
+        const float dla = sh.dlgS[(p0 + pr) * 16 + l16];
+        const float ua = l16 < 8 ? sh.uS[(p0 + pr) * 8 + (l16 & 7)] : 0.f;
+#pragma unroll
+        for (int hb = 0; hb <= HB; ++hb) gW2[hb] = mfma16x16x4(dla, hS[pr * S::LDH + hb * 16 + l16], gW2[hb]);
+#pragma unroll
+        for (int hb = 0; hb < HB; ++hb) gW1[hb] = mfma16x16x4(dhS[pr * S::LDH + hb * 16 + l16], ua, gW1[hb]);
+      }
+    }
+  }
+
+  // ---------------- epilogue: loss partials, q0 sums, weight-gradient partials
+  __syncthreads();
+  double* red = reinterpret_cast<double*>(sh.lgS);  // 4 x 256 doubles = 8 KB (lgS is 16 KB)
+  red[0 * 256 + tid] = s_rec;
+  red[1 * 256 + tid] = s_init;
+  red[2 * 256 + tid] = s_tr;
+  red[3 * 256 + tid] = s_ent;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if (tid < st)
+      for (int i = 0; i < 4; ++i) red[i * 256 + tid] += red[i * 256 + tid + st];
+    __syncthreads();
+  }
+  if (tid < 4) a.part[blockIdx.x * 4 + tid] = red[tid * 256];
+  if (!a.need_grad) return;
+  float* qr = sh.dlgS;  // [K][256]
+#pragma unroll
+  for (int k = 0; k < K; ++k) qr[k * 256 + tid] = q0acc[k];
+  __syncthreads();
+  if (tid < K) {
+    float s = 0.f;
+    for (int i = 0; i < 256; ++i) s += qr[tid * 256 + i];
+    a.slab_q0[blockIdx.x * K + tid] = s;
+  }
+  // weight grads: waves 1..3 add into wave 0 in order through LDS (uS region: 8 KB = 2048 floats)
+  float* xch = sh.uS;
+  constexpr int NV = (2 * HB + 1) * 4;  // floats per lane
+  static_assert(NV * 64 <= MP * 8 + MP * 16, "exchange buffer");
+  float* xbuf = sh.uS;  // uS (2048) followed by lgS (4096) are contiguous in HeadLds
+  (void)xch;
+  for (int w = 1; w < 4; ++w) {
+    __syncthreads();
+    if (wave == w) {
+#pragma unroll
+      for (int hb = 0; hb <= HB; ++hb)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) xbuf[(hb * 4 + v) * 64 + lane] = gW2[hb][v];
+#pragma unroll
+      for (int hb = 0; hb < HB; ++hb)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) xbuf[((HB + 1 + hb) * 4 + v) * 64 + lane] = gW1[hb][v];
+    }
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+      for (int hb = 0; hb <= HB; ++hb)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) gW2[hb][v] += xbuf[(hb * 4 + v) * 64 + lane];
+#pragma unroll
+      for (int hb = 0; hb < HB; ++hb)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) gW1[hb][v] += xbuf[((HB + 1 + hb) * 4 + v) * 64 + lane];
+    }
+  }
+  if (wave == 0) {
+    // gW2' block hb: lane -> ij = 4*lg4 + v, h = hb*16 + l16 (h == TH is db2)
+    float* sW2 = a.slab_W2 + (int64_t)blockIdx.x * KK * TH;
+    float* sb2 = a.slab_b2 + (int64_t)blockIdx.x * KK;
+#pragma unroll
+    for (int hb = 0; hb <= HB; ++hb)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int ij = 4 * lg4 + v, h = hb * 16 + l16;
+        if (ij < KK) {
+          if (h < TH) sW2[ij * TH + h] = gW2[hb][v];
+          else if (h == TH) sb2[ij] = gW2[hb][v];
+        }
+      }
+    // gW1' block hb: lane -> h = hb*16 + 4*lg4 + v, c' = l16 (c' == U is db1)
+    float* sW1 = a.slab_W1 + (int64_t)blockIdx.x * TH * U;
+    float* sb1 = a.slab_b1 + (int64_t)blockIdx.x * TH;
+#pragma unroll
+    for (int hb = 0; hb < HB; ++hb)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int h = hb * 16 + 4 * lg4 + v;
+        if (l16 < U) sW1[h * U + l16] = gW1[hb][v];
+        else if (l16 == U) sb1[h] = gW1[hb][v];
+      }
+  }
+}
+
+bool head_mfma_supported(const HeadArgs& a) {
+  return a.K >= 1 && a.K <= 4 && a.U <= 7 && (a.TH == 64 || a.TH == 128);
+}
+
+int launch_head_mfma(const HeadArgs& a, int grid, hipStream_t s) {
+#define VQHMM_HM(KV, HBV)                                                                    \
+  {                                                                                          \
+    const size_t lds = sizeof(HeadLds<KV, HBV>);                                             \
+    elbo_head_mfma_kernel<KV, HBV><<<grid, 256, lds, s>>>(a);                                \
+  }
+  const int HB = a.TH / 16;
+  switch (a.K * 10 + HB) {
+    case 14: VQHMM_HM(1, 4) break;
+    case 18: VQHMM_HM(1, 8) break;
+    case 24: VQHMM_HM(2, 4) break;
+    case 28: VQHMM_HM(2, 8) break;
+    case 34: VQHMM_HM(3, 4) break;
+    case 38: VQHMM_HM(3, 8) break;
+    case 44: VQHMM_HM(4, 4) break;
+    case 48: VQHMM_HM(4, 8) break;
+    default: return VQHMM_EUNSUPPORTED;
+  }
+#undef VQHMM_HM
+  VQHMM_LAUNCH_CHECK();
+  return VQHMM_OK;
+}
+
+}  // namespace vqhmm

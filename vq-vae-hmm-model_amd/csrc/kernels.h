@@ -95,9 +95,16 @@ struct SlabSeg {
 int launch_vq_argmin(const float* z, int64_t B, int64_t Dv, int64_t T, const float* cb, int64_t K, int32_t* idx,
                      float* dmin, hipStream_t s);
 int launch_conv(const ConvArgs& a, hipStream_t s);
+bool conv2_supported(const ConvArgs& a);
+int launch_conv2(const ConvArgs& a, hipStream_t s);
 int launch_wgrad(const WgradArgs& a, hipStream_t s);
 int64_t wgrad_chunks(int64_t R, int64_t tiles);
+bool wgrad2_supported(const WgradArgs& a);
+int64_t wgrad2_rows(int64_t R, int N, int C, int ks);
+int launch_wgrad2(const WgradArgs& a, hipStream_t s);
 int head_grid(int64_t R);
+bool head_mfma_supported(const HeadArgs& a);
+int launch_head_mfma(const HeadArgs& a, int grid, hipStream_t s);
 int launch_head(const HeadArgs& a, int grid, hipStream_t s);
 int launch_prior_fwd(const PriorArgs& p, hipStream_t s);
 int launch_reduce_slabs(const SlabSeg* segs, int n, hipStream_t s);

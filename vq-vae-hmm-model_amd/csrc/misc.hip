@@ -26,9 +26,16 @@ __global__ __launch_bounds__(256) void reduce_slabs_kernel(SlabSegs segs) {
   const SlabSeg& sg = segs.s[si];
   const int64_t col = ((int64_t)blockIdx.x - segs.blk_start[si]) * 64 + (threadIdx.x & 63);
   const int ph = threadIdx.x >> 6;
-  float acc = 0.f;
-  if (col < sg.len)
-    for (int64_t c = ph; c < sg.nchunks; c += 4) acc += sg.slab[c * sg.len + col];
+  float p8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (col < sg.len) {
+    int64_t c = ph;
+    for (; c + 28 < sg.nchunks; c += 32) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) p8[k] += sg.slab[(c + 4 * k) * sg.len + col];
+    }
+    for (int k = 0; c < sg.nchunks; c += 4, ++k) p8[k & 7] += sg.slab[c * sg.len + col];
+  }
+  const float acc = ((p8[0] + p8[1]) + (p8[2] + p8[3])) + ((p8[4] + p8[5]) + (p8[6] + p8[7]));
   part[ph][threadIdx.x & 63] = acc;
   __syncthreads();
   if (ph == 0 && col < sg.len) {
@@ -92,43 +99,71 @@ int launch_finalize_loss(const double* part, int nblk, const int64_t* lengths, i
 }
 
 // ------------------------------------------------------------ composed decoder conv1
-// Wc[o][k][tap] = sum_h W[o][h][tap] * E[k][h];  W (H,H,3), E (K,H), Wc (H,K,3)
-__global__ void compose_fwd_kernel(const float* W, const float* E, int H, int K, float* Wc) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= H * K * 3) return;
-  const int tap = i % 3, k = (i / 3) % K, o = i / (3 * K);
-  float s = 0.f;
-  for (int h = 0; h < H; ++h) s = fmaf(W[(o * H + h) * 3 + tap], E[k * H + h], s);
-  Wc[i] = s;
+// Wc[o][k][tap] = sum_h W[o][h][tap] * E[k][h];  W (H,H,3), E (K,H), Wc (H,K,3).
+// One block per output channel o; W[o] and E staged in LDS.
+__global__ __launch_bounds__(256) void compose_fwd_kernel(const float* W, const float* E, int H, int K, float* Wc) {
+  extern __shared__ float cs[];
+  float* wo = cs;          // [H*3]
+  float* es = cs + H * 3;  // [K*H]
+  const int o = blockIdx.x;
+  for (int i = threadIdx.x; i < H * 3; i += 256) wo[i] = W[(int64_t)o * H * 3 + i];
+  for (int i = threadIdx.x; i < K * H; i += 256) es[i] = E[i];
+  __syncthreads();
+  for (int i = threadIdx.x; i < K * 3; i += 256) {
+    const int k = i / 3, tap = i % 3;
+    float s = 0.f;
+    for (int h = 0; h < H; ++h) s = fmaf(wo[h * 3 + tap], es[k * H + h], s);
+    Wc[(int64_t)o * K * 3 + i] = s;
+  }
 }
-// dW[o][h][tap] = sum_k dWc[o][k][tap] E[k][h];  dE[k][h] = sum_{o,tap} dWc[o][k][tap] W[o][h][tap]
-__global__ void compose_bwd_kernel(const float* dWc, const float* W, const float* E, int H, int K, float* dW,
-                                   float* dE) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  const int n1 = H * H * 3;
-  if (i < n1) {
-    const int tap = i % 3, h = (i / 3) % H, o = i / (3 * H);
-    float s = 0.f;
-    for (int k = 0; k < K; ++k) s = fmaf(dWc[(o * K + k) * 3 + tap], E[k * H + h], s);
-    dW[i] = s;
-  } else if (i < n1 + K * H) {
-    const int j = i - n1;
-    const int h = j % H, k = j / H;
-    float s = 0.f;
-    for (int o = 0; o < H; ++o)
-      for (int tap = 0; tap < 3; ++tap) s = fmaf(dWc[(o * K + k) * 3 + tap], W[(o * H + h) * 3 + tap], s);
-    dE[j] = s;
+// dW[o][h][tap] = sum_k dWc[o][k][tap] E[k][h]       (blocks 0..H-1, one per o)
+// dE[k][h] = sum_{o,tap} dWc[o][k][tap] W[o][h][tap]  (blocks H..H+K-1, one per k;
+//            4 thread groups split o, combined in fixed order)
+__global__ __launch_bounds__(256) void compose_bwd_kernel(const float* dWc, const float* W, const float* E, int H,
+                                                          int K, float* dW, float* dE) {
+  extern __shared__ float cs[];
+  if ((int)blockIdx.x < H) {
+    const int o = blockIdx.x;
+    float* dwo = cs;           // [K*3]
+    float* es = cs + K * 3;    // [K*H]
+    for (int i = threadIdx.x; i < K * 3; i += 256) dwo[i] = dWc[(int64_t)o * K * 3 + i];
+    for (int i = threadIdx.x; i < K * H; i += 256) es[i] = E[i];
+    __syncthreads();
+    for (int i = threadIdx.x; i < H * 3; i += 256) {
+      const int h = i / 3, tap = i % 3;
+      float s = 0.f;
+      for (int k = 0; k < K; ++k) s = fmaf(dwo[k * 3 + tap], es[k * H + h], s);
+      dW[(int64_t)o * H * 3 + i] = s;
+    }
+  } else {
+    const int k = blockIdx.x - H;
+    float* part = cs;  // [4][H]
+    const int g = threadIdx.x >> 6;
+    for (int h = threadIdx.x & 63; h < H; h += 64) {
+      float s = 0.f;
+      for (int o = g; o < H; o += 4)
+#pragma unroll
+        for (int tap = 0; tap < 3; ++tap)
+          s = fmaf(dWc[((int64_t)o * K + k) * 3 + tap], W[((int64_t)o * H + h) * 3 + tap], s);
+      part[g * H + h] = s;
+    }
+    __syncthreads();
+    for (int h = threadIdx.x; h < H; h += 256)
+      dE[(int64_t)k * H + h] = ((part[h] + part[H + h]) + part[2 * H + h]) + part[3 * H + h];
   }
 }
 
 int launch_compose_fwd(const float* W, const float* E, int H, int K, float* Wc, hipStream_t s) {
-  compose_fwd_kernel<<<(unsigned)cdiv((int64_t)H * K * 3, 256), 256, 0, s>>>(W, E, H, K, Wc);
+  const size_t lds = (size_t)(H * 3 + K * H) * 4;
+  compose_fwd_kernel<<<(unsigned)H, 256, lds, s>>>(W, E, H, K, Wc);
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
 }
 int launch_compose_bwd(const float* dWc, const float* W, const float* E, int H, int K, float* dW, float* dE,
                        hipStream_t s) {
-  compose_bwd_kernel<<<(unsigned)cdiv((int64_t)H * H * 3 + K * H, 256), 256, 0, s>>>(dWc, W, E, H, K, dW, dE);
+  size_t lds = (size_t)(K * 3 + K * H) * 4;
+  if ((size_t)4 * H * 4 > lds) lds = (size_t)4 * H * 4;
+  compose_bwd_kernel<<<(unsigned)(H + K), 256, lds, s>>>(dWc, W, E, H, K, dW, dE);
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
 }

@@ -1,0 +1,262 @@
+// Weight/bias gradient of the small-channel convolutions (N, C <= 64), the
+// split-K GEMM dW[n][c][tap] = sum_r dY[r][n] * X[r + tap - 1][c] over all PCL
+// rows (pad rows of dY are zero, so the sum needs no masks).
+//
+//  * Persistent workgroups, one contiguous row chunk each; the chunk is walked
+//    in 64-row stages whose dY / X tiles are prefetched into registers (float4
+//    where the channel count allows, clamped + selected, no branches) while the
+//    MFMAs of the previous stage run.
+//  * The 4 waves split the work WN x WC x WR = 4 ways over (n-blocks, c-blocks,
+//    16-row slices of each stage): large outputs (64x64x3) split the output
+//    blocks, tiny ones (3x32, 10x64) also split the rows and add the partials
+//    of the WR row-waves in a fixed order at the end.
+//  * Per workgroup the partial dW (and dbias) goes to a slab; reduce_slabs sums
+//    the slabs in a fixed order (deterministic, no atomics).
+#include "kernels.h"
+
+namespace vqhmm {
+
+namespace {
+constexpr int RT = 64;  // rows per stage
+}
+
+template <int NBW, int CBW, int KS, int NPAD, int CPAD>
+__global__ __launch_bounds__(256) void wgrad2_kernel(WgradArgs a, int WN, int WC, int WR) {
+  constexpr int LDA = NPAD + 4, LDB = CPAD + 4;  // 4*LD = 16 (mod 32): conflict-free b32 column reads
+  constexpr int DY4 = RT * NPAD / 4;             // float4 slots of the dY stage
+  constexpr int X4 = (RT + 2) * CPAD / 4;        // float4 slots of the X stage
+  constexpr int PD = (DY4 + 255) / 256, PX = (X4 + 255) / 256;
+  __shared__ float dys[RT * LDA];
+  __shared__ float xs[(RT + 2) * LDB];
+  __shared__ float bred[256];
+  __shared__ float xbuf[1536];  // row-wave exchange (WR > 1 only with NBW = CBW = 1)
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lg4 = lane >> 4, l16 = lane & 15;
+  const int wr = wave % WR, wc = (wave / WR) % WC, wn = wave / (WR * WC);
+  const int64_t chunk = blockIdx.x;
+  const int64_t rbeg = chunk * a.rows_per_chunk;
+  const int64_t rend = min(a.R, rbeg + a.rows_per_chunk);
+  const int64_t Tp = (int64_t)a.T + 2;
+  const bool vdy = (a.N % 4) == 0;
+  const bool vx = !a.x_cf && (a.C % 4) == 0;
+
+  auto load_dy = [&](int64_t r0, float4* p) {
+#pragma unroll
+    for (int k = 0; k < PD; ++k) {
+      const int s = tid + k * 256;
+      const int row = s / (NPAD / 4), c = (s - row * (NPAD / 4)) * 4;
+      const int64_t r = r0 + row;
+      const bool rin = s < DY4 && r < rend;
+      const int64_t rc = rin ? r : rbeg;
+      if (vdy) {
+        const bool ok = rin && c < a.N;
+        const float4 v = *reinterpret_cast<const float4*>(a.dy + rc * a.N + (ok ? c : 0));
+        p[k] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {
+        float e[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const bool ok = rin && c + q < a.N;
+          const float v = a.dy[rc * a.N + (ok ? c + q : 0)];
+          e[q] = ok ? v : 0.f;
+        }
+        p[k] = make_float4(e[0], e[1], e[2], e[3]);
+      }
+    }
+  };
+  auto load_x = [&](int64_t r0, float4* p) {
+#pragma unroll
+    for (int k = 0; k < PX; ++k) {
+      const int s = tid + k * 256;
+      const int row = s / (CPAD / 4), c = (s - row * (CPAD / 4)) * 4;
+      const int64_t r = r0 - 1 + row;
+      const bool rin = s < X4 && r >= 0 && r < a.R;
+      const int64_t rc = rin ? r : 0;
+      if (a.x_cf) {
+        const int64_t b = rc / Tp;
+        const int t = (int)(rc - b * Tp) - 1;
+        const bool tin = rin && t >= 0 && t < a.T;
+        float e[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const bool ok = tin && c + q < a.C;
+          const float v = a.x[(b * a.C + (ok ? c + q : 0)) * a.T + (tin ? t : 0)];
+          e[q] = ok ? v : 0.f;
+        }
+        p[k] = make_float4(e[0], e[1], e[2], e[3]);
+      } else if (vx) {
+        const bool ok = rin && c < a.C;
+        const float4 v = *reinterpret_cast<const float4*>(a.x + rc * a.C + (ok ? c : 0));
+        p[k] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {
+        float e[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const bool ok = rin && c + q < a.C;
+          const float v = a.x[rc * a.C + (ok ? c + q : 0)];
+          e[q] = ok ? v : 0.f;
+        }
+        p[k] = make_float4(e[0], e[1], e[2], e[3]);
+      }
+    }
+  };
+
+  f32x4 acc[KS][NBW][CBW];
+#pragma unroll
+  for (int tp = 0; tp < KS; ++tp)
+#pragma unroll
+    for (int i = 0; i < NBW; ++i)
+#pragma unroll
+      for (int j = 0; j < CBW; ++j) acc[tp][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bacc = 0.f;
+  const int bcol = tid % NPAD, brow0 = tid / NPAD, bstep = 256 / NPAD;
+
+  float4 pdy[PD], px[PX];
+  load_dy(rbeg, pdy);
+  load_x(rbeg, px);
+  for (int64_t r0 = rbeg; r0 < rend; r0 += RT) {
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PD; ++k) {
+      const int s = tid + k * 256;
+      if (s < DY4) {
+        const int row = s / (NPAD / 4), c = (s - row * (NPAD / 4)) * 4;
+        *reinterpret_cast<float4*>(dys + row * LDA + c) = pdy[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < PX; ++k) {
+      const int s = tid + k * 256;
+      if (s < X4) {
+        const int row = s / (CPAD / 4), c = (s - row * (CPAD / 4)) * 4;
+        *reinterpret_cast<float4*>(xs + row * LDB + c) = px[k];
+      }
+    }
+    __syncthreads();
+    if (r0 + RT < rend) {
+      load_dy(r0 + RT, pdy);
+      load_x(r0 + RT, px);
+    }
+    if (a.bias_slab) {
+      for (int row = brow0; row < RT; row += bstep) bacc += dys[row * LDA + bcol];
+    }
+    // this wave's 16-row slices of the stage
+    for (int sl = wr; sl < RT / 16; sl += WR) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int rr = sl * 16 + 4 * lg4 + e;
+        float av[NBW];
+#pragma unroll
+        for (int i = 0; i < NBW; ++i) av[i] = dys[rr * LDA + (wn + i * WN) * 16 + l16];
+#pragma unroll
+        for (int tp = 0; tp < KS; ++tp) {
+          const int xrow = rr + (KS == 3 ? tp : 1);
+#pragma unroll
+          for (int j = 0; j < CBW; ++j) {
+            const float bv = xs[xrow * LDB + (wc + j * WC) * 16 + l16];
+#pragma unroll
+            for (int i = 0; i < NBW; ++i) acc[tp][i][j] = mfma16x16x4(av[i], bv, acc[tp][i][j]);
+          }
+        }
+      }
+    }
+  }
+  // ---- combine the WR row-waves (fixed order), then write the partial
+  float* xch = xbuf;
+  for (int w = 1; w < WR; ++w) {
+    __syncthreads();
+    if (wr == w) {
+#pragma unroll
+      for (int tp = 0; tp < KS; ++tp)
+#pragma unroll
+        for (int i = 0; i < NBW; ++i)
+#pragma unroll
+          for (int j = 0; j < CBW; ++j)
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+              xch[(wave / WR) * (KS * NBW * CBW * 4 * 64) + (((tp * NBW + i) * CBW + j) * 4 + v) * 64 + lane] =
+                  acc[tp][i][j][v];
+    }
+    __syncthreads();
+    if (wr == 0) {
+#pragma unroll
+      for (int tp = 0; tp < KS; ++tp)
+#pragma unroll
+        for (int i = 0; i < NBW; ++i)
+#pragma unroll
+          for (int j = 0; j < CBW; ++j)
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+              acc[tp][i][j][v] +=
+                  xch[(wave / WR) * (KS * NBW * CBW * 4 * 64) + (((tp * NBW + i) * CBW + j) * 4 + v) * 64 + lane];
+    }
+  }
+  if (wr == 0) {
+    float* out = a.slab + chunk * (int64_t)a.N * a.C * KS;
+#pragma unroll
+    for (int tp = 0; tp < KS; ++tp)
+#pragma unroll
+      for (int i = 0; i < NBW; ++i)
+#pragma unroll
+        for (int j = 0; j < CBW; ++j)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            const int n = (wn + i * WN) * 16 + 4 * lg4 + v;
+            const int c = (wc + j * WC) * 16 + l16;
+            if (n < a.N && c < a.C) out[((int64_t)n * a.C + c) * KS + tp] = acc[tp][i][j][v];
+          }
+  }
+  if (a.bias_slab) {
+    __syncthreads();
+    bred[tid] = bacc;
+    __syncthreads();
+    if (tid < NPAD && tid < a.N) {
+      float s = 0.f;
+      for (int k = 0; k < bstep; ++k) s += bred[k * NPAD + tid];
+      a.bias_slab[chunk * a.N + tid] = s;
+    }
+  }
+}
+
+bool wgrad2_supported(const WgradArgs& a) { return a.N <= 64 && a.C <= 64; }
+
+int64_t wgrad2_rows(int64_t R, int N, int C, int ks) {
+  // big outputs: one chunk per CU (small slabs); small outputs: 2 per CU
+  const int64_t chunks = ((int64_t)N * C * ks >= 4096) ? 256 : 512;
+  int64_t rows = cdiv(R, chunks);
+  return cdiv(rows, RT) * RT;
+}
+
+template <int NBW, int CBW, int KS, int NPAD, int CPAD>
+static int launch_w2(const WgradArgs& a, int WN, int WC, int WR, hipStream_t s) {
+  const int64_t nchunks = cdiv(a.R, a.rows_per_chunk);
+  if (WR > 1 && (NBW * CBW != 1 || KS * 4 * 64 * (4 / WR) > 1536)) return VQHMM_EUNSUPPORTED;
+  wgrad2_kernel<NBW, CBW, KS, NPAD, CPAD><<<(unsigned)nchunks, 256, 0, s>>>(a, WN, WC, WR);
+  VQHMM_LAUNCH_CHECK();
+  return VQHMM_OK;
+}
+
+template <int KS>
+static int launch_w2_ks(const WgradArgs& a, hipStream_t s) {
+  const int nbn = (int)cdiv(a.N, 16), nbc = (int)cdiv(a.C, 16);
+  // choose the wave split: prefer output blocks, then rows
+  if (nbn == 4 && nbc == 4) return launch_w2<4, 1, KS, 64, 64>(a, 1, 4, 1, s);
+  if (nbn == 2 && nbc == 4) return launch_w2<2, 1, KS, 32, 64>(a, 1, 4, 1, s);
+  if (nbn == 4 && nbc == 2) return launch_w2<1, 2, KS, 64, 32>(a, 4, 1, 1, s);
+  if (nbn == 1 && nbc == 4) return launch_w2<1, 1, KS, 16, 64>(a, 1, 4, 1, s);
+  if (nbn == 4 && nbc == 1) return launch_w2<1, 1, KS, 64, 16>(a, 4, 1, 1, s);
+  if (nbn == 1 && nbc == 2) return launch_w2<1, 1, KS, 16, 32>(a, 1, 2, 2, s);
+  if (nbn == 2 && nbc == 1) return launch_w2<1, 1, KS, 32, 16>(a, 2, 1, 2, s);
+  if (nbn == 2 && nbc == 2) return launch_w2<1, 1, KS, 32, 32>(a, 2, 2, 1, s);
+  if (nbn == 1 && nbc == 1) return launch_w2<1, 1, KS, 16, 16>(a, 1, 1, 4, s);
+  if (nbn <= 4 && nbc <= 4) return launch_w2<4, 1, KS, 64, 64>(a, 1, 4, 1, s);
+  return VQHMM_EUNSUPPORTED;
+}
+
+int launch_wgrad2(const WgradArgs& a, hipStream_t s) {
+  if (a.R == 0) return VQHMM_OK;
+  return a.ks == 3 ? launch_w2_ks<3>(a, s) : launch_w2_ks<1>(a, s);
+}
+
+}  // namespace vqhmm
