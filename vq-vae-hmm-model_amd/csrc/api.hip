@@ -48,7 +48,8 @@ struct ElboPlan {
   int64_t B, R;
   int T, D, H, H2, K, U, TH;
   int hgrid;
-  // forward
+  // forward (PCL buffers, row stride ld4(channels))
+  float *xp, *up;
   float *h1e, *h2e, *logits, *q, *g1, *g2, *par, *Wc;
   // head
   float *dpar, *dqx, *dlx;
@@ -68,18 +69,20 @@ ElboPlan plan_elbo(const vqhmm_dims_t* d, int64_t B, int64_t T, void* ws) {
   const int64_t R = p.R;
   const int H = p.H, H2 = p.H2, K = p.K, D = p.D;
   Carver c{reinterpret_cast<char*>(ws)};
-  p.h1e = c.take<float>(R * H);
-  p.h2e = c.take<float>(R * H2);
-  p.logits = c.take<float>(R * K);
-  p.q = c.take<float>(R * K);
-  p.g1 = c.take<float>(R * H);
-  p.g2 = c.take<float>(R * H);
-  p.par = c.take<float>(R * 2 * D);
+  p.xp = c.take<float>(R * ld4(D));
+  p.up = c.take<float>(R * ld4(p.U));
+  p.h1e = c.take<float>(R * ld4(H));
+  p.h2e = c.take<float>(R * ld4(H2));
+  p.logits = c.take<float>(R * ld4(K));
+  p.q = c.take<float>(R * ld4(K));
+  p.g1 = c.take<float>(R * ld4(H));
+  p.g2 = c.take<float>(R * ld4(H));
+  p.par = c.take<float>(R * ld4(2 * D));
   p.Wc = c.take<float>((size_t)H * K * 3);
   p.hgrid = head_grid(R);
-  p.dpar = c.take<float>(R * 2 * D);
-  p.dqx = c.take<float>(R * K);
-  p.dlx = c.take<float>(R * K);
+  p.dpar = c.take<float>(R * ld4(2 * D));
+  p.dqx = c.take<float>(R * ld4(K));
+  p.dlx = c.take<float>(R * ld4(K));
   p.part = c.take<double>((size_t)p.hgrid * 4);
   p.sW1 = c.take<float>((size_t)p.hgrid * p.TH * p.U);
   p.sb1 = c.take<float>((size_t)p.hgrid * p.TH);
@@ -88,12 +91,12 @@ ElboPlan plan_elbo(const vqhmm_dims_t* d, int64_t B, int64_t T, void* ws) {
   p.sq0 = c.take<float>((size_t)p.hgrid * K);
   p.loss = c.take<float>(1);
   p.pieces = c.take<float>(4);
-  p.dg2 = c.take<float>(R * H);
-  p.dg1 = c.take<float>(R * H);
-  p.dqd = c.take<float>(R * K);
-  p.dlog = c.take<float>(R * K);
-  p.dh2 = c.take<float>(R * H2);
-  p.dh1 = c.take<float>(R * H);
+  p.dg2 = c.take<float>(R * ld4(H));
+  p.dg1 = c.take<float>(R * ld4(H));
+  p.dqd = c.take<float>(R * ld4(K));
+  p.dlog = c.take<float>(R * ld4(K));
+  p.dh2 = c.take<float>(R * ld4(H2));
+  p.dh1 = c.take<float>(R * ld4(H));
   p.dWc = c.take<float>((size_t)H * K * 3);
   p.q0sum = c.take<float>(K);
   const int shapes[6][3] = {{2 * D, H, 1}, {H, H, 3}, {H, K, 3}, {K, H2, 1}, {H2, H, 3}, {H, D, 3}};
@@ -189,15 +192,15 @@ int vqhmm_elbo_workspace_size(const vqhmm_dims_t* d, int64_t B, int64_t T, size_
 namespace {
 
 enum Stage {
-  S_COMPOSE, S_ENC1, S_ENC2, S_DEC1, S_DEC2, S_HEAD, S_FINAL,                 // forward
+  S_TOPCL, S_COMPOSE, S_ENC1, S_ENC2, S_DEC1, S_DEC2, S_HEAD, S_FINAL,                 // forward
   S_PAR_DG, S_DEC2_DG, S_DEC1_DG, S_LOGIT_BWD, S_LOGIT_DG, S_ENC2_DG,         // backward data
   S_W_PAR, S_W_DEC2, S_W_DEC1, S_W_LOGIT, S_W_ENC2, S_W_ENC1,                 // backward weights
   S_REDUCE, S_COMPOSE_BWD, S_LOGPRIOR,                                         // reductions
   S_COUNT
 };
-const int FWD_FIRST = S_COMPOSE, FWD_LAST = S_FINAL, BWD_FIRST = S_PAR_DG, BWD_LAST = S_LOGPRIOR;
+const int FWD_FIRST = S_TOPCL, FWD_LAST = S_FINAL, BWD_FIRST = S_PAR_DG, BWD_LAST = S_LOGPRIOR;
 const char* kStageNames[S_COUNT] = {
-    "compose_fwd", "enc_conv1", "enc_conv2+to_logits", "dec_conv1(composed)", "dec_conv2+to_params",
+    "inputs_to_pcl", "compose_fwd", "enc_conv1", "enc_conv2+to_logits", "dec_conv1(composed)", "dec_conv2+to_params",
     "elbo_head", "finalize_loss", "to_params_dgrad", "dec_conv2_dgrad", "dec_conv1_dgrad", "logits_bwd",
     "to_logits_dgrad", "enc_conv2_dgrad", "to_params_wgrad", "dec_conv2_wgrad", "dec_conv1_wgrad",
     "to_logits_wgrad", "enc_conv2_wgrad", "enc_conv1_wgrad", "reduce_slabs", "compose_bwd", "log_prior_grad"};
@@ -222,7 +225,7 @@ ConvArgs conv_of(const ElboPlan& p, const float* const* wp, int st) {
   ConvArgs a = conv_base(p);
   switch (st) {
     case S_ENC1:
-      a.src_cf = 1; a.Kc = p.D; a.ks = 3; a.W = w[ENC1_W]; a.bias = w[ENC1_B]; a.N = p.H; a.act = 1; a.out = p.h1e;
+      a.src = p.xp; a.Kc = p.D; a.ks = 3; a.W = w[ENC1_W]; a.bias = w[ENC1_B]; a.N = p.H; a.act = 1; a.out = p.h1e;
       break;
     case S_ENC2:
       a.src = p.h1e; a.Kc = p.H; a.ks = 3; a.W = w[ENC2_W]; a.bias = w[ENC2_B]; a.N = p.H2; a.act = 1; a.out = p.h2e;
@@ -261,14 +264,14 @@ ConvArgs conv_of(const ElboPlan& p, const float* const* wp, int st) {
 int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
   const float* const* w = c.w;
   switch (st) {
+    case S_TOPCL: {
+      if (int rc = launch_to_pcl(c.x, p.D, p.B, p.T, p.T, 1, p.xp, s)) return rc;
+      const int64_t sc = c.u_layout == 0 ? p.T : 1, stt = c.u_layout == 0 ? 1 : p.U;
+      return launch_to_pcl(c.u, p.U, p.B, p.T, sc, stt, p.up, s);
+    }
     case S_COMPOSE:
       return launch_compose_fwd(w[DEC1_W], w[EMB], p.H, p.K, p.Wc, s);
-    case S_ENC1: {
-      ConvArgs a = conv_of(p, w, st);
-      a.src = c.x;
-      return launch_conv(a, s);
-    }
-    case S_ENC2: case S_DEC1: case S_DEC2: case S_DEC2_DG: case S_DEC1_DG: case S_LOGIT_DG: case S_ENC2_DG:
+    case S_ENC1: case S_ENC2: case S_DEC1: case S_DEC2: case S_DEC2_DG: case S_DEC1_DG: case S_LOGIT_DG: case S_ENC2_DG:
       return launch_conv(conv_of(p, w, st), s);
     case S_PAR_DG: {
       ConvArgs a = conv_of(p, w, st);
@@ -278,8 +281,7 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
     case S_HEAD: {
       HeadArgs h{};
       h.B = p.B; h.T = p.T; h.R = p.R; h.D = p.D; h.K = p.K; h.U = p.U; h.TH = p.TH;
-      h.x = c.x; h.u = c.u;
-      if (c.u_layout == 0) { h.u_sc = p.T; h.u_st = 1; } else { h.u_sc = 1; h.u_st = p.U; }
+      h.x = p.xp; h.u = p.up;
       h.lengths = c.lengths; h.par = p.par; h.logits = p.logits; h.q = p.q;
       h.W1 = w[TN0_W]; h.b1 = w[TN0_B]; h.W2 = w[TN2_W]; h.b2 = w[TN2_B]; h.log_prior = w[LOG_PRIOR];
       h.beta = c.beta; h.need_grad = c.need_grad;
@@ -295,10 +297,10 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
     case S_W_PAR: case S_W_DEC2: case S_W_DEC1: case S_W_LOGIT: case S_W_ENC2: case S_W_ENC1: {
       const int i = st - S_W_PAR;
       const float* dys[6] = {p.dpar, p.dg2, p.dg1, p.dlog, p.dh2, p.dh1};
-      const float* xs[6] = {p.g2, p.g1, p.q, p.h2e, p.h1e, c.x};
+      const float* xs[6] = {p.g2, p.g1, p.q, p.h2e, p.h1e, p.xp};
       const WLayer& L = p.wl[i];
       WgradArgs wa{};
-      wa.dy = dys[i]; wa.x = xs[i]; wa.x_cf = (i == 5); wa.R = p.R; wa.T = p.T;
+      wa.dy = dys[i]; wa.x = xs[i]; wa.x_cf = 0; wa.R = p.R; wa.T = p.T;
       wa.N = L.N; wa.C = L.C; wa.ks = L.ks; wa.rows_per_chunk = L.rows; wa.slab = L.slab; wa.bias_slab = L.bslab;
       return launch_wgrad(wa, s);
     }
@@ -370,6 +372,8 @@ void stage_work(const ElboPlan& p, int st, double* flops, double* bytes, int* mf
     const double KK = (double)p.K * p.K;
     *flops = N * (2.0 * p.TH * p.U + 2.0 * p.TH * KK + 6.0 * p.TH * KK + 4.0 * p.TH * p.U + 20.0 * p.D + 12.0 * KK);
     *bytes = 4.0 * R * (2 * p.D + p.D + p.U + 2 * p.K + 2 * p.D + 2 * p.K);
+  } else if (st == S_TOPCL) {
+    *bytes = 4.0 * (N * (p.D + p.U) + R * (ld4(p.D) + ld4(p.U)));
   } else if (st == S_LOGIT_BWD) {
     *bytes = 4.0 * R * 6 * p.K;
     *flops = R * 8.0 * p.K;
@@ -460,23 +464,28 @@ int vqhmm_adam_f32(float* param, const float* grad, float* exp_avg, float* exp_a
 int vqhmm_infer_workspace_size(const vqhmm_dims_t* d, int64_t B, int64_t T, size_t* bytes) {
   if (!dims_ok(d) || B < 0 || T < 0 || !bytes) return VQHMM_EINVAL;
   const int64_t R = B * (T + 2);
+  const int hw = ld4(d->hidden_dim > d->hidden_dim2 ? d->hidden_dim : d->hidden_dim2);
   Carver c{nullptr};
-  c.take<float>(R * d->hidden_dim);
-  c.take<float>(R * d->hidden_dim);
-  c.take<float>(R * d->K);
+  c.take<float>(R * hw);
+  c.take<float>(R * hw);
+  c.take<float>(R * ld4(d->K));
+  c.take<float>(R * ld4(d->input_dim > d->K ? d->input_dim : d->K));
   c.take<float>((size_t)d->hidden_dim * d->K * 3);
   *bytes = c.off + 256;
   return VQHMM_OK;
 }
 
+// x is CF (B, D, T); it is first copied into the padded PCL buffer xin.
 static int encode_impl(const vqhmm_dims_t* d, const float* const* w, const float* x, int64_t B, int64_t T,
-                       float* logits_cf, float* q_cf, float* q_pcl, float* bufA, float* bufB, hipStream_t s) {
+                       float* logits_cf, float* q_cf, float* q_pcl, float* xin, float* bufA, float* bufB,
+                       hipStream_t s) {
   const int64_t R = B * (T + 2);
+  int rc;
+  if ((rc = launch_to_pcl(x, d->input_dim, B, (int)T, T, 1, xin, s))) return rc;
   ConvArgs a{};
   a.R = R; a.T = (int)T;
-  a.src = x; a.src_cf = 1; a.Kc = d->input_dim; a.ks = 3; a.W = w[ENC1_W]; a.bias = w[ENC1_B];
+  a.src = xin; a.Kc = d->input_dim; a.ks = 3; a.W = w[ENC1_W]; a.bias = w[ENC1_B];
   a.N = d->hidden_dim; a.act = 1; a.out = bufA;
-  int rc;
   if ((rc = launch_conv(a, s))) return rc;
   a = ConvArgs{};
   a.R = R; a.T = (int)T;
@@ -490,14 +499,18 @@ static int encode_impl(const vqhmm_dims_t* d, const float* const* w, const float
   return launch_conv(a, s);
 }
 
+// q is either CF (B, K, T) (q_cf = 1: copied into the PCL buffer qin first) or
+// already PCL (q_cf = 0, q == qin).
 static int decode_impl(const vqhmm_dims_t* d, const float* const* w, const float* q, int q_cf, int64_t B,
-                       int64_t T, float* mu, float* logvar, float* bufA, float* bufB, float* Wc, hipStream_t s) {
+                       int64_t T, float* mu, float* logvar, float* qin, float* bufA, float* bufB, float* Wc,
+                       hipStream_t s) {
   const int64_t R = B * (T + 2);
   int rc;
   if ((rc = launch_compose_fwd(w[DEC1_W], w[EMB], d->hidden_dim, d->K, Wc, s))) return rc;
+  if (q_cf && (rc = launch_to_pcl(q, d->K, B, (int)T, T, 1, qin, s))) return rc;
   ConvArgs a{};
   a.R = R; a.T = (int)T;
-  a.src = q; a.src_cf = q_cf; a.Kc = d->K; a.ks = 3; a.W = Wc; a.bias = w[DEC1_B]; a.N = d->hidden_dim;
+  a.src = qin; a.Kc = d->K; a.ks = 3; a.W = Wc; a.bias = w[DEC1_B]; a.N = d->hidden_dim;
   a.act = 1; a.out = bufA;
   if ((rc = launch_conv(a, s))) return rc;
   a = ConvArgs{};
@@ -509,14 +522,16 @@ static int decode_impl(const vqhmm_dims_t* d, const float* const* w, const float
   return launch_conv(a, s);
 }
 
-struct InferBufs { float *A, *B, *q, *Wc; };
+struct InferBufs { float *A, *B, *q, *in, *Wc; };
 static InferBufs carve_infer(const vqhmm_dims_t* d, int64_t B, int64_t T, void* ws) {
   const int64_t R = B * (T + 2);
+  const int hw = ld4(d->hidden_dim > d->hidden_dim2 ? d->hidden_dim : d->hidden_dim2);
   Carver c{reinterpret_cast<char*>(ws)};
   InferBufs b;
-  b.A = c.take<float>(R * d->hidden_dim);
-  b.B = c.take<float>(R * d->hidden_dim);
-  b.q = c.take<float>(R * d->K);
+  b.A = c.take<float>(R * hw);
+  b.B = c.take<float>(R * hw);
+  b.q = c.take<float>(R * ld4(d->K));
+  b.in = c.take<float>(R * ld4(d->input_dim > d->K ? d->input_dim : d->K));
   b.Wc = c.take<float>((size_t)d->hidden_dim * d->K * 3);
   return b;
 }
@@ -529,7 +544,7 @@ int vqhmm_encode_f32(const vqhmm_dims_t* d, const float* const* w, const float* 
   vqhmm_infer_workspace_size(d, B, T, &need);
   if (ws_bytes < need) return VQHMM_EWORKSPACE;
   InferBufs b = carve_infer(d, B, T, ws);
-  return encode_impl(d, w, x, B, T, logits, nullptr, nullptr, b.A, b.B, (hipStream_t)stream);
+  return encode_impl(d, w, x, B, T, logits, nullptr, nullptr, b.in, b.A, b.B, (hipStream_t)stream);
 }
 
 int vqhmm_decode_f32(const vqhmm_dims_t* d, const float* const* w, const float* q, int64_t B, int64_t T, float* mu,
@@ -540,7 +555,7 @@ int vqhmm_decode_f32(const vqhmm_dims_t* d, const float* const* w, const float* 
   vqhmm_infer_workspace_size(d, B, T, &need);
   if (ws_bytes < need) return VQHMM_EWORKSPACE;
   InferBufs b = carve_infer(d, B, T, ws);
-  return decode_impl(d, w, q, 1, B, T, mu, logvar, b.A, b.B, b.Wc, (hipStream_t)stream);
+  return decode_impl(d, w, q, 1, B, T, mu, logvar, b.in, b.A, b.B, b.Wc, (hipStream_t)stream);
 }
 
 int vqhmm_forward_f32(const vqhmm_dims_t* d, const float* const* w, const float* x, int64_t B, int64_t T, float* mu,
@@ -553,8 +568,8 @@ int vqhmm_forward_f32(const vqhmm_dims_t* d, const float* const* w, const float*
   InferBufs b = carve_infer(d, B, T, ws);
   hipStream_t s = (hipStream_t)stream;
   int rc;
-  if ((rc = encode_impl(d, w, x, B, T, nullptr, q, b.q, b.A, b.B, s))) return rc;
-  return decode_impl(d, w, b.q, 0, B, T, mu, logvar, b.A, b.B, b.Wc, s);
+  if ((rc = encode_impl(d, w, x, B, T, nullptr, q, b.q, b.in, b.A, b.B, s))) return rc;
+  return decode_impl(d, w, b.q, 0, B, T, mu, logvar, b.q, b.A, b.B, b.Wc, s);
 }
 
 int vqhmm_prior_f32(const vqhmm_dims_t* d, const float* const* w, const float* u, int u_layout, int64_t B, int64_t T,

@@ -5,7 +5,11 @@
 // holds time step t of sequence b; rows b*(T+2) and b*(T+2) + T + 1 are kept
 // all-zero, so a k=3 convolution never needs a boundary test: the zero rows
 // ARE the Conv1d zero padding of the reference (padding=1,
-// VQ_VAE_HMM_fixed.py:34-35,77-78).  Row stride = channel count (dense).
+// VQ_VAE_HMM_fixed.py:34-35,77-78).
+//
+// Channel stride: a PCL tensor with C channels has row stride ld4(C) = C rounded
+// up to a multiple of 4, and its pad channels are kept zero by every producer,
+// so every PCL row access is an aligned float4.
 //
 // "CF" = the reference's channels-first (B, C, T) layout, used at the
 // module boundary (x, u, logits, mu, logvar).
@@ -31,6 +35,7 @@ __device__ __forceinline__ f32x4 mfma16x16x4(float a, float b, f32x4 c) {
 }
 
 __host__ __device__ __forceinline__ int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+__host__ __device__ __forceinline__ int ld4(int c) { return (c + 3) & ~3; }
 
 // Map a PCL row to (b, t); returns false for pad rows / out of range.
 __device__ __forceinline__ bool row_bt(int64_t r, int64_t R, int T, int64_t& b, int& t) {

@@ -54,7 +54,8 @@ __global__ __launch_bounds__(256) void conv_mm_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < WN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const bool vec_src = !a.src_cf && (a.Kc % 4 == 0);
+  const bool vec_src = !a.src_cf;  // PCL rows have stride ld4(Kc): always float4-aligned
+  const int lds = ld4(a.Kc);
   for (int c0 = 0; c0 < a.Kc; c0 += KCH) {
     __syncthreads();
     // ---- stage input rows [m0-1, m0+BM] x channels [c0, c0+KCH)
@@ -75,7 +76,7 @@ __global__ __launch_bounds__(256) void conv_mm_kernel(ConvArgs a) {
         const int row = i / (KCH / 4), c = (i - row * (KCH / 4)) * 4;
         const int64_t r = m0 - 1 + row;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (r >= 0 && r < a.R && c0 + c < a.Kc) v = *reinterpret_cast<const float4*>(a.src + r * a.Kc + c0 + c);
+        if (r >= 0 && r < a.R && c0 + c < lds) v = *reinterpret_cast<const float4*>(a.src + r * lds + c0 + c);
         *reinterpret_cast<float4*>(Xs + row * LDX + c) = v;
       }
     } else {
@@ -83,7 +84,7 @@ __global__ __launch_bounds__(256) void conv_mm_kernel(ConvArgs a) {
         const int row = i / KCH, c = i - row * KCH;
         const int64_t r = m0 - 1 + row;
         float v = 0.f;
-        if (r >= 0 && r < a.R && c0 + c < a.Kc) v = a.src[r * a.Kc + c0 + c];
+        if (r >= 0 && r < a.R && c0 + c < a.Kc) v = a.src[r * lds + c0 + c];
         Xs[row * LDX + c] = v;
       }
     }
@@ -147,10 +148,10 @@ __global__ __launch_bounds__(256) void conv_mm_kernel(ConvArgs a) {
       y = Ys[row * LDY + col] * sc;
       if (a.bias) y += a.bias[n];
       if (a.act == 1) y = fmaxf(y, 0.f);
-      else if (a.act == 2) y = a.aux[r * a.N + n] > 0.f ? y : 0.f;
+      else if (a.act == 2) y = a.aux[r * ld4(a.N) + n] > 0.f ? y : 0.f;
     }
     Ys[row * LDY + col] = y;
-    if (a.out && n < a.N && r < a.R) a.out[r * a.N + n] = y;
+    if (a.out && n < ld4(a.N) && r < a.R) a.out[r * ld4(a.N) + n] = y;
   }
   if (a.out_cf || a.tW) __syncthreads();
   if (a.out_cf) {
@@ -182,14 +183,18 @@ __global__ __launch_bounds__(256) void conv_mm_kernel(ConvArgs a) {
       }
       Zs[row * LDZ + c2] = z;
       mx = fmaxf(mx, z);
-      if (a.t_out && r < a.R) a.t_out[r * a.C2 + c2] = z;
+      if (a.t_out && r < a.R) a.t_out[r * ld4(a.C2) + c2] = z;
+    }
+    for (int c2 = a.C2; c2 < ld4(a.C2); ++c2) {
+      if (a.t_out && r < a.R) a.t_out[r * ld4(a.C2) + c2] = 0.f;
+      if (a.q_out && r < a.R) a.q_out[r * ld4(a.C2) + c2] = 0.f;
     }
     if (a.q_out || a.q_cf) {
       float s = 0.f;
       for (int c2 = 0; c2 < a.C2; ++c2) s += __expf(Zs[row * LDZ + c2] - mx);
       for (int c2 = 0; c2 < a.C2; ++c2) {
         const float q = valid ? __expf(Zs[row * LDZ + c2] - mx) / s : 0.f;
-        if (a.q_out && r < a.R) a.q_out[r * a.C2 + c2] = q;
+        if (a.q_out && r < a.R) a.q_out[r * ld4(a.C2) + c2] = q;
         if (a.q_cf) Zs[row * LDZ + c2] = q;
       }
     }
@@ -280,7 +285,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
     for (int i = tid; i < RT * TN; i += 256) {
       const int row = i / TN, n = i - row * TN;
       const int64_t r = r0 + row;
-      dys[row * LDA + n] = (r < rend && n0 + n < a.N) ? a.dy[r * a.N + n0 + n] : 0.f;
+      dys[row * LDA + n] = (r < rend && n0 + n < a.N) ? a.dy[r * ld4(a.N) + n0 + n] : 0.f;
     }
     if (a.x_cf) {
       for (int i = tid; i < (RT + 2) * TC; i += 256) {
@@ -298,7 +303,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradArgs a) {
       for (int i = tid; i < (RT + 2) * TC; i += 256) {
         const int row = i / TC, c = i - row * TC;
         const int64_t r = r0 - 1 + row;
-        xs[row * LDB + c] = (r >= 0 && r < a.R && c0 + c < a.C) ? a.x[r * a.C + c0 + c] : 0.f;
+        xs[row * LDB + c] = (r >= 0 && r < a.R && c0 + c < a.C) ? a.x[r * ld4(a.C) + c0 + c] : 0.f;
       }
     }
     __syncthreads();

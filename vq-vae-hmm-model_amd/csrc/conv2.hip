@@ -12,6 +12,8 @@
 //    epilogue stores are float4, and the fused 1x1 tail (to_logits /
 //    to_params, + softmax) consumes the fragments directly as its MFMA B
 //    operand (contraction over the fragment's row index), with no LDS round trip.
+#include <stdlib.h>
+
 #include "kernels.h"
 
 namespace vqhmm {
@@ -32,46 +34,111 @@ struct C2Cfg {
   static constexpr size_t LDS = (W_FLOATS + X_FLOATS) * 4;
 };
 
-// Gather the float4 slot `s` of an X tile starting at PCL row m0-1 (zeros outside / in padding).
-__device__ __forceinline__ float4 x_slot(const ConvArgs& a, int64_t m0, int s, int kcw, bool vec) {
+// Raw float4 slot `s` of an X tile starting at PCL row m0-1 (row stride
+// ld4(Kc)): the address is clamped in range and x_mask() zeroes what lies
+// outside the tile's rows / the row's channels afterwards — keeping the select
+// away from the load lets the prefetch stay in flight across the MFMA loop.
+__device__ __forceinline__ float4 x_raw(const ConvArgs& a, int64_t m0, int s, int kcw) {
+  const int q4 = kcw / 4, ld = ld4(a.Kc);
+  const int row = s / q4, c = (s - row * q4) * 4;
+  int64_t r = m0 - 1 + row;
+  r = r < 0 ? 0 : (r >= a.R ? a.R - 1 : r);
+  return *reinterpret_cast<const float4*>(a.src + r * ld + min(c, ld - 4));
+}
+
+__device__ __forceinline__ float4 x_mask(const ConvArgs& a, int64_t m0, int s, int kcw, float4 v) {
   const int q4 = kcw / 4;
   const int row = s / q4, c = (s - row * q4) * 4;
   const int64_t r = m0 - 1 + row;
-  const bool rin = r >= 0 && r < a.R;
-  const int64_t rc = rin ? r : 0;
-  float4 v;
-  if (a.src_cf) {
-    const int64_t Tp = (int64_t)a.T + 2;
-    const int64_t b = rc / Tp;
-    const int t = (int)(rc - b * Tp) - 1;
-    const bool tin = rin && t >= 0 && t < a.T;
-    const int tc = tin ? t : 0;
-    float e[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const bool ok = tin && c + k < a.Kc;
-      const float val = a.src[(b * a.Kc + (ok ? c + k : 0)) * a.T + tc];
-      e[k] = ok ? val : 0.f;
-    }
-    v = make_float4(e[0], e[1], e[2], e[3]);
-  } else if (vec) {
-    const bool ok = rin && c < a.Kc;
-    const float4 val = *reinterpret_cast<const float4*>(a.src + rc * a.Kc + (ok ? c : 0));
-    v = ok ? val : make_float4(0.f, 0.f, 0.f, 0.f);
-  } else {
-    float e[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const bool ok = rin && c + k < a.Kc;
-      const float val = a.src[rc * a.Kc + (ok ? c + k : 0)];
-      e[k] = ok ? val : 0.f;
-    }
-    v = make_float4(e[0], e[1], e[2], e[3]);
-  }
-  return v;
+  const bool ok = r >= 0 && r < a.R && c < ld4(a.Kc);  // pad channels inside the row are already 0
+  return ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
 }  // namespace
+
+// Epilogue of one tile (ACT: 0 none, 1 ReLU, 2 ReLU-backward mask by aux).
+template <int NB, int PB, int ACT>
+__device__ __forceinline__ void conv2_epilogue(const ConvArgs& a, int64_t m0, int wave, int lg4, int l16,
+                                               f32x4 (&acc)[NB][PB], const float4 (&auxv)[NB][PB],
+                                               const float (&bias_r)[NB][4], const float (&tw)[NB][4],
+                                               f32x4 tb0, float sc, bool tail) {
+  // lane (lg4, l16) holds channels nb*16 + 4*lg4 + v of row m0 + (wave*PB+pb)*16 + l16
+#pragma unroll
+    for (int pb = 0; pb < PB; ++pb) {
+      const int64_t r = m0 + (wave * PB + pb) * 16 + l16;
+      int64_t b;
+      int t;
+      const bool valid = row_bt(r, a.R, a.T, b, t);
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        f32x4 y;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          float yy = acc[nb][pb][v] * sc + bias_r[nb][v];
+          if (ACT == 1) yy = fmaxf(yy, 0.f);
+          if (ACT == 2) {
+            const float av = v == 0 ? auxv[nb][pb].x : v == 1 ? auxv[nb][pb].y : v == 2 ? auxv[nb][pb].z : auxv[nb][pb].w;
+            yy = av > 0.f ? yy : 0.f;
+          }
+          y[v] = valid ? yy : 0.f;
+        }
+        acc[nb][pb] = y;
+        const int n0 = nb * 16 + 4 * lg4;
+        if (a.out && r < a.R && n0 < ld4(a.N)) *reinterpret_cast<f32x4*>(a.out + r * ld4(a.N) + n0) = y;
+        if (a.out_cf && valid) {
+#pragma unroll
+          for (int v = 0; v < 4; ++v)
+            if (n0 + v < a.N) a.out_cf[(b * a.N + n0 + v) * a.T + t] = y[v];
+        }
+      }
+      if (tail) {
+        // z^T (16 c2 x 16 rows) = tW (16 x N) @ Y^T: B operand = the fragments above
+        f32x4 z = tb0;
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) z = mfma16x16x4(tw[nb][v], acc[nb][pb][v], z);
+        // lane holds c2 = 4*lg4 + v of row r
+        const int c0 = 4 * lg4;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) z[v] = valid ? z[v] : 0.f;
+        if (a.t_out && r < a.R && c0 < ld4(a.C2)) *reinterpret_cast<f32x4*>(a.t_out + r * ld4(a.C2) + c0) = z;
+        if (a.t_cf0 && valid) {
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            const int c2 = c0 + v;
+            if (c2 < a.t_split) a.t_cf0[(b * a.t_split + c2) * a.T + t] = z[v];
+            else if (c2 < a.C2) a.t_cf1[(b * (a.C2 - a.t_split) + c2 - a.t_split) * a.T + t] = z[v];
+          }
+        }
+        if (a.q_out || a.q_cf) {
+          float m = -__builtin_inff();
+#pragma unroll
+          for (int v = 0; v < 4; ++v)
+            if (c0 + v < a.C2) m = fmaxf(m, z[v]);
+          m = fmaxf(m, __shfl_xor(m, 16));
+          m = fmaxf(m, __shfl_xor(m, 32));
+          float e[4], s = 0.f;
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            e[v] = (c0 + v < a.C2) ? __expf(z[v] - m) : 0.f;
+            s += e[v];
+          }
+          s += __shfl_xor(s, 16);
+          s += __shfl_xor(s, 32);
+          f32x4 qv;
+#pragma unroll
+          for (int v = 0; v < 4; ++v) qv[v] = valid ? e[v] / s : 0.f;  // 0 in pad channels (e = 0)
+          if (a.q_out && r < a.R && c0 < ld4(a.C2)) *reinterpret_cast<f32x4*>(a.q_out + r * ld4(a.C2) + c0) = qv;
+          if (a.q_cf && valid) {
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+              if (c0 + v < a.C2) a.q_cf[(b * a.C2 + c0 + v) * a.T + t] = qv[v];
+          }
+        }
+      }
+    }
+}
 
 template <int NB, int KCP, int KS, int PB>
 __global__ __launch_bounds__(256, 1) void conv2_kernel(ConvArgs a, int64_t ntiles) {
@@ -81,7 +148,6 @@ __global__ __launch_bounds__(256, 1) void conv2_kernel(ConvArgs a, int64_t ntile
   float* Xs = Ws + C::W_FLOATS;                 // [XROWS][LDX]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lg4 = lane >> 4, l16 = lane & 15;
-  const bool vec = !a.src_cf && (a.Kc % 4 == 0);
 
   // ---- weights once: Ws[tap][n][c] = Weff(n, c, tap)
   for (int i = tid; i < KS * C::NW * C::KCW; i += 256) {
@@ -121,7 +187,7 @@ __global__ __launch_bounds__(256, 1) void conv2_kernel(ConvArgs a, int64_t ntile
 #pragma unroll
   for (int k = 0; k < C::PF; ++k) {
     const int s = tid + k * 256;
-    pf[k] = (s < C::XF4) ? x_slot(a, tile * C::BM, s < C::XF4 ? s : 0, C::KCW, vec) : make_float4(0.f, 0.f, 0.f, 0.f);
+    pf[k] = x_raw(a, tile * C::BM, s < C::XF4 ? s : 0, C::KCW);
   }
   while (tile < ntiles) {
     const int64_t m0 = tile * C::BM;
@@ -131,12 +197,12 @@ __global__ __launch_bounds__(256, 1) void conv2_kernel(ConvArgs a, int64_t ntile
       const int s = tid + k * 256;
       if (s < C::XF4) {
         const int row = s / (C::KCW / 4), c = (s - row * (C::KCW / 4)) * 4;
-        *reinterpret_cast<float4*>(Xs + row * C::LDX + c) = pf[k];
+        *reinterpret_cast<float4*>(Xs + row * C::LDX + c) = x_mask(a, m0, s, C::KCW, pf[k]);
       }
     }
     __syncthreads();
     // epilogue operands of THIS tile first (older than the prefetch in the vmcnt order)
-    float4 auxv[NB][PB];
+    float4 auxv[NB][PB] = {};
     if (a.act == 2) {
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb)
@@ -144,8 +210,8 @@ __global__ __launch_bounds__(256, 1) void conv2_kernel(ConvArgs a, int64_t ntile
         for (int pb = 0; pb < PB; ++pb) {
           const int64_t r = m0 + (wave * PB + pb) * 16 + l16;
           const int n0 = nb * 16 + 4 * lg4;
-          const bool ok = r < a.R && n0 < a.N;
-          auxv[nb][pb] = *reinterpret_cast<const float4*>(a.aux + (ok ? r : 0) * a.N + (ok ? n0 : 0));
+          const int ldn = ld4(a.N);
+          auxv[nb][pb] = *reinterpret_cast<const float4*>(a.aux + (r < a.R ? r : a.R - 1) * ldn + min(n0, ldn - 4));
         }
     }
     const int64_t next = tile + gridDim.x;
@@ -153,7 +219,7 @@ __global__ __launch_bounds__(256, 1) void conv2_kernel(ConvArgs a, int64_t ntile
 #pragma unroll
       for (int k = 0; k < C::PF; ++k) {
         const int s = tid + k * 256;
-        if (s < C::XF4) pf[k] = x_slot(a, next * C::BM, s, C::KCW, vec);
+        pf[k] = x_raw(a, next * C::BM, s < C::XF4 ? s : 0, C::KCW);
       }
     }
     // ---- MFMA: acc[nb][pb] = Y^T block (16 n x 16 rows)
@@ -186,114 +252,50 @@ __global__ __launch_bounds__(256, 1) void conv2_kernel(ConvArgs a, int64_t ntile
           }
       }
     }
-    // ---- epilogue: lane (lg4, l16) holds channels nb*16 + 4*lg4 + v of row m0 + (wave*PB+pb)*16 + l16
-#pragma unroll
-    for (int pb = 0; pb < PB; ++pb) {
-      const int64_t r = m0 + (wave * PB + pb) * 16 + l16;
-      int64_t b;
-      int t;
-      const bool valid = row_bt(r, a.R, a.T, b, t);
-#pragma unroll
-      for (int nb = 0; nb < NB; ++nb) {
-        f32x4 y;
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          float yy = acc[nb][pb][v] * sc + bias_r[nb][v];
-          if (a.act == 1) yy = fmaxf(yy, 0.f);
-          else if (a.act == 2) yy = (v == 0 ? auxv[nb][pb].x : v == 1 ? auxv[nb][pb].y : v == 2 ? auxv[nb][pb].z
-                                                                                                 : auxv[nb][pb].w) > 0.f
-                                        ? yy
-                                        : 0.f;
-          y[v] = valid ? yy : 0.f;
-        }
-        acc[nb][pb] = y;
-        const int n0 = nb * 16 + 4 * lg4;
-        if (a.out && r < a.R) {
-          if ((a.N & 3) == 0) {
-            if (n0 < a.N) *reinterpret_cast<f32x4*>(a.out + r * a.N + n0) = y;
-          } else {
-#pragma unroll
-            for (int v = 0; v < 4; ++v)
-              if (n0 + v < a.N) a.out[r * a.N + n0 + v] = y[v];
-          }
-        }
-        if (a.out_cf && valid) {
-#pragma unroll
-          for (int v = 0; v < 4; ++v)
-            if (n0 + v < a.N) a.out_cf[(b * a.N + n0 + v) * a.T + t] = y[v];
-        }
-      }
-      if (tail) {
-        // z^T (16 c2 x 16 rows) = tW (16 x N) @ Y^T: B operand = the fragments above
-        f32x4 z = tb0;
-#pragma unroll
-        for (int nb = 0; nb < NB; ++nb)
-#pragma unroll
-          for (int v = 0; v < 4; ++v) z = mfma16x16x4(tw[nb][v], acc[nb][pb][v], z);
-        // lane holds c2 = 4*lg4 + v of row r
-        const int c0 = 4 * lg4;
-#pragma unroll
-        for (int v = 0; v < 4; ++v) z[v] = valid ? z[v] : 0.f;
-        if (a.t_out && r < a.R) {
-#pragma unroll
-          for (int v = 0; v < 4; ++v)
-            if (c0 + v < a.C2) a.t_out[r * a.C2 + c0 + v] = z[v];
-        }
-        if (a.t_cf0 && valid) {
-#pragma unroll
-          for (int v = 0; v < 4; ++v) {
-            const int c2 = c0 + v;
-            if (c2 < a.t_split) a.t_cf0[(b * a.t_split + c2) * a.T + t] = z[v];
-            else if (c2 < a.C2) a.t_cf1[(b * (a.C2 - a.t_split) + c2 - a.t_split) * a.T + t] = z[v];
-          }
-        }
-        if (a.q_out || a.q_cf) {
-          float m = -__builtin_inff();
-#pragma unroll
-          for (int v = 0; v < 4; ++v)
-            if (c0 + v < a.C2) m = fmaxf(m, z[v]);
-          m = fmaxf(m, __shfl_xor(m, 16));
-          m = fmaxf(m, __shfl_xor(m, 32));
-          float e[4], s = 0.f;
-#pragma unroll
-          for (int v = 0; v < 4; ++v) {
-            e[v] = (c0 + v < a.C2) ? __expf(z[v] - m) : 0.f;
-            s += e[v];
-          }
-          s += __shfl_xor(s, 16);
-          s += __shfl_xor(s, 32);
-#pragma unroll
-          for (int v = 0; v < 4; ++v) {
-            const int c2 = c0 + v;
-            if (c2 < a.C2) {
-              const float qv = valid ? e[v] / s : 0.f;
-              if (a.q_out && r < a.R) a.q_out[r * a.C2 + c2] = qv;
-              if (a.q_cf && valid) a.q_cf[(b * a.C2 + c2) * a.T + t] = qv;
-            }
-          }
-        }
-      }
-    }
+    if (a.act == 2)
+      conv2_epilogue<NB, PB, 2>(a, m0, wave, lg4, l16, acc, auxv, bias_r, tw, tb0, sc, tail);
+    else if (a.act == 1)
+      conv2_epilogue<NB, PB, 1>(a, m0, wave, lg4, l16, acc, auxv, bias_r, tw, tb0, sc, tail);
+    else
+      conv2_epilogue<NB, PB, 0>(a, m0, wave, lg4, l16, acc, auxv, bias_r, tw, tb0, sc, tail);
     tile = next;
   }
 }
 
 bool conv2_supported(const ConvArgs& a) {
-  return a.N <= 64 && a.Kc <= 64 && (a.tW == nullptr || a.C2 <= 16);
+  return !a.src_cf && a.N <= 64 && a.Kc <= 64 && (a.tW == nullptr || a.C2 <= 16);
 }
 
-template <int NB, int KCP, int KS>
-static int launch_c2(const ConvArgs& a, hipStream_t s) {
-  constexpr int PB = 2;
+template <int NB, int KCP, int KS, int PB>
+static int launch_c2p(const ConvArgs& a, hipStream_t s) {
   using C = C2Cfg<NB, KCP, KS, PB>;
   const int64_t ntiles = cdiv(a.R, C::BM);
   int per_cu = (int)((160 * 1024) / C::LDS);
   if (per_cu < 1) return VQHMM_EUNSUPPORTED;
-  if (per_cu > 2) per_cu = 2;
+  if (per_cu > 4) per_cu = 4;
   const int64_t grid = ntiles < 256LL * per_cu ? ntiles : 256LL * per_cu;
   conv2_kernel<NB, KCP, KS, PB><<<(unsigned)grid, 256, C::LDS, s>>>(a, ntiles);
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
+}
+
+// rows per tile = 64*PB; PB = 1 halves the X tile so two workgroups fit per CU
+// (tuning override: VQHMM_CONV2_PB=1|2, read once)
+static int conv2_pb() {
+  static int pb = [] {
+    const char* e = getenv("VQHMM_CONV2_PB");
+    return (e && e[0] == '1') ? 1 : (e && e[0] == '2') ? 2 : 0;
+  }();
+  return pb;
+}
+
+template <int NB, int KCP, int KS>
+static int launch_c2(const ConvArgs& a, hipStream_t s) {
+  const int pb = conv2_pb();
+  const bool big = NB * KCP >= 8;  // default: PB=1 for the 64x64 layers (2 WG/CU), PB=2 otherwise
+  (void)big;
+  if (pb != 2) return launch_c2p<NB, KCP, KS, 1>(a, s);
+  return launch_c2p<NB, KCP, KS, 2>(a, s);
 }
 
 template <int NB, int KS>

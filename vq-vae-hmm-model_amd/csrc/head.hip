@@ -126,7 +126,7 @@ __global__ __launch_bounds__(256) void elbo_head_kernel(HeadArgs a) {
       wS[tid + 1] = (valid && t >= 1 && t < L) ? 1 : 0;
       float uv[UM];
 #pragma unroll
-      for (int c = 0; c < UM; ++c) uv[c] = (valid && c < a.U) ? a.u[b * (int64_t)a.U * a.T + c * a.u_sc + t * a.u_st] : 0.f;
+      for (int c = 0; c < UM; ++c) uv[c] = (valid && c < a.U) ? a.u[r * ld4(a.U) + c] : 0.f;
 #pragma unroll
       for (int c = 0; c < UM; ++c) uS[tid * UM + c] = uv[c];
       float la[KM * KM];
@@ -134,23 +134,23 @@ __global__ __launch_bounds__(256) void elbo_head_kernel(HeadArgs a) {
 #pragma unroll
       for (int ij = 0; ij < KM * KM; ++ij) laS[tid * KM * KM + ij] = la[ij];
 #pragma unroll
-      for (int k = 0; k < KM; ++k) qS[(tid + 1) * KM + k] = (valid && k < K) ? a.q[r * K + k] : 0.f;
+      for (int k = 0; k < KM; ++k) qS[(tid + 1) * KM + k] = (valid && k < K) ? a.q[r * ld4(K) + k] : 0.f;
       if (tid == 0) {
         const int64_t rp = r0 - 1;
         int64_t bp;
         int tpv;
         const bool vp = row_bt(rp, a.R, a.T, bp, tpv);
 #pragma unroll
-        for (int k = 0; k < KM; ++k) qS[k] = (vp && k < K) ? a.q[rp * K + k] : 0.f;
+        for (int k = 0; k < KM; ++k) qS[k] = (vp && k < K) ? a.q[rp * ld4(K) + k] : 0.f;
       }
       if (tid < HP && r < a.R) {
         // recon NLL (:118-120)
         for (int c = 0; c < D; ++c) {
           float dmu = 0.f, dlv = 0.f;
           if (m) {
-            const float mu = a.par[r * 2 * D + c];
-            const float lv = a.par[r * 2 * D + D + c];
-            const float xv = a.x[(b * D + c) * a.T + t];
+            const float mu = a.par[r * ld4(2 * D) + c];
+            const float lv = a.par[r * ld4(2 * D) + D + c];
+            const float xv = a.x[r * ld4(D) + c];
             const float ev = __expf(lv);
             const float var = fmaxf(ev, 1e-8f);
             const float df = mu - xv;
@@ -160,16 +160,18 @@ __global__ __launch_bounds__(256) void elbo_head_kernel(HeadArgs a) {
             dlv = (ev >= 1e-8f) ? 0.5f * (1.f - r2) * inv_n : 0.f;
           }
           if (a.need_grad) {
-            a.dpar[r * 2 * D + c] = dmu;
-            a.dpar[r * 2 * D + D + c] = dlv;
+            a.dpar[r * ld4(2 * D) + c] = dmu;
+            a.dpar[r * ld4(2 * D) + D + c] = dlv;
           }
         }
+        if (a.need_grad)
+          for (int c = 2 * D; c < ld4(2 * D); ++c) a.dpar[r * ld4(2 * D) + c] = 0.f;
         // entropy (:134-135): sum_k q log_softmax
         float lg[KM], qv[KM];
         float mx = -__builtin_inff();
 #pragma unroll
         for (int k = 0; k < KM; ++k) {
-          lg[k] = (valid && k < K) ? a.logits[r * K + k] : 0.f;
+          lg[k] = (valid && k < K) ? a.logits[r * ld4(K) + k] : 0.f;
           qv[k] = qS[(tid + 1) * KM + k];
           if (k < K) mx = fmaxf(mx, lg[k]);
         }
@@ -186,7 +188,7 @@ __global__ __launch_bounds__(256) void elbo_head_kernel(HeadArgs a) {
         if (a.need_grad) {
 #pragma unroll
           for (int k = 0; k < KM; ++k)
-            if (k < K) a.dlx[r * K + k] = m ? cent * qv[k] * ((lg[k] - lse) - f) : 0.f;
+            if (k < ld4(K)) a.dlx[r * ld4(K) + k] = (m && k < K) ? cent * qv[k] * ((lg[k] - lse) - f) : 0.f;
         }
         // init term (:123), unmasked, t == 0
         if (valid && t == 0) {
@@ -248,8 +250,9 @@ __global__ __launch_bounds__(256) void elbo_head_kernel(HeadArgs a) {
             if (jj < K) nx = fmaf(qn[jj], lan[j * K + jj], nx);
           float v = cpri * (w * dq[j] + wn * nx);
           if (valid && t == 0) v = fmaf(cpri, lpS[j], v);
-          a.dqx[r * K + j] = valid ? v : 0.f;
+          a.dqx[r * ld4(K) + j] = valid ? v : 0.f;
         }
+        for (int j = K; j < ld4(K); ++j) a.dqx[r * ld4(K) + j] = 0.f;
       }
     }
     if (!a.need_grad) continue;
@@ -370,7 +373,7 @@ __global__ __launch_bounds__(256) void elbo_head_kernel(HeadArgs a) {
 
 int head_grid(int64_t R) {
   const int64_t ntiles = cdiv(R, HP);
-  return (int)(ntiles < 256 ? ntiles : 256);
+  return (int)(ntiles < 512 ? ntiles : 512);
 }
 
 int launch_head(const HeadArgs& a0, int grid, hipStream_t s) {

@@ -29,22 +29,57 @@ template <int K, int HB>
 struct HeadLds {
   static constexpr int TH = HB * 16;
   static constexpr int LDW2 = TH + 4;   // W2S row stride: 4*LDW2 = 16 (mod 32) -> conflict-free
-  static constexpr int LDH = TH + 16;   // hS / dhS row stride (= 16 mod 32)
   float W2S[16 * LDW2];
+  float W1S[TH * 8];      // W1' = [W1 | b1 | 0]  (TH x 8)
   float uS[MP * 8];
   float lgS[MP * 16];
   float dlgS[MP * 16];
   float qS[(MP + 2) * 4];
   int wS[MP + 2];
-  float hS[4][16 * LDH];
-  float dhS[4][16 * LDH];
+  float hT[4][16 * 16];   // per-wave 16-row x 16-h transposes (row stride 16 = conflict-free column reads)
+  float dT[4][16 * 16];
   float lpS[4];
   unsigned long long cnt;
 };
 }  // namespace
 
-template <int K, int HB>
-__global__ __launch_bounds__(256, 1) void elbo_head_mfma_kernel(HeadArgs a) {
+// Per-row global inputs of one tile, loaded one tile ahead into registers.
+template <int K, int DM>
+struct RowIn {
+  float u[8];
+  float q[4];
+  float par[2 * DM];
+  float x[DM];
+  float lg[4];
+  int64_t L;
+};
+
+template <int K, int DM>
+__device__ __forceinline__ void load_row(const HeadArgs& a, int64_t r, RowIn<K, DM>& in) {
+  // raw loads from clamped addresses of the PCL inputs; validity is re-derived
+  // from r where the values are consumed (no select next to a load, so the
+  // prefetch stays in flight)
+  const int64_t rc = r < 0 ? 0 : (r >= a.R ? a.R - 1 : r);
+  const int64_t b = rc / ((int64_t)a.T + 2);
+  in.L = a.lengths[b];
+  const int ldu = ld4(a.U), ldx = ld4(a.D), ldp = ld4(2 * a.D);
+#pragma unroll
+  for (int c = 0; c < 8; ++c) in.u[c] = a.u[rc * ldu + min(c, ldu - 1)];
+  const float4 qv = *reinterpret_cast<const float4*>(a.q + rc * 4);
+  const float4 lv = *reinterpret_cast<const float4*>(a.logits + rc * 4);
+  in.q[0] = qv.x; in.q[1] = qv.y; in.q[2] = qv.z; in.q[3] = qv.w;
+  in.lg[0] = lv.x; in.lg[1] = lv.y; in.lg[2] = lv.z; in.lg[3] = lv.w;
+#pragma unroll
+  for (int c = 0; c < DM; ++c) {
+    const int cc = min(c, a.D - 1);
+    in.par[c] = a.par[rc * ldp + cc];
+    in.par[DM + c] = a.par[rc * ldp + a.D + cc];
+    in.x[c] = a.x[rc * ldx + min(c, ldx - 1)];
+  }
+}
+
+template <int K, int HB, int DM>
+__global__ __launch_bounds__(256, 2) void elbo_head_mfma_kernel(HeadArgs a) {
   constexpr int KK = K * K;
   constexpr int TH = HB * 16;
   using S = HeadLds<K, HB>;
@@ -70,21 +105,12 @@ __global__ __launch_bounds__(256, 1) void elbo_head_mfma_kernel(HeadArgs a) {
     for (int k = 0; k < K; ++k) sh.lpS[k] = a.log_prior[k] - l;
     sh.cnt = 0;
   }
-  // A fragments of W1' (hid^T = W1' u'^T): lane (i = h, k = c')   [2 k-steps of 4]
-  float w1f[HB][2];
-#pragma unroll
-  for (int hb = 0; hb < HB; ++hb)
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int h = hb * 16 + l16, c = ks * 4 + lg4;
-      w1f[hb][ks] = c < U ? a.W1[h * U + c] : (c == U ? a.b1[h] : 0.f);
-    }
-  // A fragments of W2 for lg^T: lane (i = ij, k = h = hb*16 + 4*lg4 + v)
-  float w2f[HB][4];
-#pragma unroll
-  for (int hb = 0; hb < HB; ++hb)
-#pragma unroll
-    for (int v = 0; v < 4; ++v) w2f[hb][v] = l16 < KK ? a.W2[l16 * TH + hb * 16 + 4 * lg4 + v] : 0.f;
+  for (int i = tid; i < TH * 8; i += 256) {
+    const int h = i >> 3, c = i & 7;
+    sh.W1S[i] = c < U ? a.W1[h * U + c] : (c == U ? a.b1[h] : 0.f);
+  }
+  // A fragments come from LDS: W1'[h = hb*16 + l16][c' = 4*ks + lg4] and, for lg^T,
+  // W2[ij = l16][h = hb*16 + 4*lg4 + v] (one float4 per hidden block)
   f32x4 b2f;
 #pragma unroll
   for (int v = 0; v < 4; ++v) b2f[v] = (4 * lg4 + v) < KK ? a.b2[4 * lg4 + v] : 0.f;
@@ -97,8 +123,6 @@ __global__ __launch_bounds__(256, 1) void elbo_head_mfma_kernel(HeadArgs a) {
     }
     atomicAdd(&sh.cnt, c);
   }
-  // per-wave constant ones block of hS (h in [TH, TH+16): column TH = 1)
-  for (int i = lane; i < 16 * 16; i += 64) sh.hS[wave][(i >> 4) * S::LDH + TH + (i & 15)] = (i & 15) == 0 ? 1.f : 0.f;
   __syncthreads();
   const float inv_n = 1.0f / fmaxf((float)(sh.cnt * (unsigned long long)D), 1.0f);
 
@@ -112,33 +136,30 @@ __global__ __launch_bounds__(256, 1) void elbo_head_mfma_kernel(HeadArgs a) {
 #pragma unroll
   for (int i = 0; i < HB; ++i) gW1[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  RowIn<K, DM> cur, nxt;
+  load_row<K, DM>(a, (int64_t)blockIdx.x * MOWN + tid, cur);
+  nxt = cur;
   for (int64_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
     const int64_t r0 = tile * MOWN;
     __syncthreads();
-    // ---------------- L: per-row loads (thread = row r0 + tid)
+    // ---------------- L: stage this tile's rows (prefetched in registers)
     {
       const int64_t r = r0 + tid;
       int64_t b;
       int t;
       const bool valid = row_bt(r, a.R, a.T, b, t);
-      const int64_t L = valid ? a.lengths[b] : 0;
-      sh.wS[tid + 1] = (valid && t >= 1 && t < L) ? 1 : 0;
+      sh.wS[tid + 1] = (valid && t >= 1 && t < cur.L) ? 1 : 0;
 #pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        float v = 0.f;
-        if (c < U) v = valid ? a.u[b * (int64_t)U * a.T + c * a.u_sc + t * a.u_st] : 0.f;
-        if (c == U) v = 1.f;
-        sh.uS[tid * 8 + c] = v;
-      }
+      for (int c = 0; c < 8; ++c) sh.uS[tid * 8 + c] = (valid && c < U) ? cur.u[c] : (c == U ? 1.f : 0.f);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) sh.qS[(tid + 1) * 4 + k] = (valid && k < K) ? a.q[r * K + k] : 0.f;
+      for (int k = 0; k < 4; ++k) sh.qS[(tid + 1) * 4 + k] = (valid && k < K) ? cur.q[k] : 0.f;
       if (tid == 0) {
         const int64_t rp = r0 - 1;
         int64_t bp;
         int tp;
         const bool vp = row_bt(rp, a.R, a.T, bp, tp);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) sh.qS[k] = (vp && k < K) ? a.q[rp * K + k] : 0.f;
+        for (int k = 0; k < 4; ++k) sh.qS[k] = (vp && k < K) ? a.q[rp * 4 + k] : 0.f;
         sh.wS[0] = (vp && tp >= 1 && tp < a.lengths[bp]) ? 1 : 0;
       }
     }
@@ -152,12 +173,13 @@ __global__ __launch_bounds__(256, 1) void elbo_head_mfma_kernel(HeadArgs a) {
 #pragma unroll
       for (int hb = 0; hb < HB; ++hb) {
         f32x4 h = f32x4{0.f, 0.f, 0.f, 0.f};
-        h = mfma16x16x4(w1f[hb][0], ub0, h);
-        h = mfma16x16x4(w1f[hb][1], ub1, h);
+        h = mfma16x16x4(sh.W1S[(hb * 16 + l16) * 8 + lg4], ub0, h);
+        h = mfma16x16x4(sh.W1S[(hb * 16 + l16) * 8 + 4 + lg4], ub1, h);
 #pragma unroll
         for (int v = 0; v < 4; ++v) h[v] = fmaxf(h[v], 0.f);
+        const f32x4 w2v = *reinterpret_cast<const f32x4*>(&sh.W2S[l16 * S::LDW2 + hb * 16 + 4 * lg4]);
 #pragma unroll
-        for (int v = 0; v < 4; ++v) lg = mfma16x16x4(w2f[hb][v], h[v], lg);
+        for (int v = 0; v < 4; ++v) lg = mfma16x16x4(w2v[v], h[v], lg);
       }
       *reinterpret_cast<f32x4*>(&sh.lgS[(p0 + l16) * 16 + 4 * lg4]) = lg;
     }
@@ -183,14 +205,15 @@ __global__ __launch_bounds__(256, 1) void elbo_head_mfma_kernel(HeadArgs a) {
         for (int j = 0; j < K; ++j) la[i * K + j] -= ls;
       }
       if (p < MOWN && r < a.R) {
-        const int64_t L = valid ? a.lengths[b] : 0;
-        const bool m = valid && t < L;
-        for (int c = 0; c < D; ++c) {
+        const bool m = valid && t < cur.L;
+#pragma unroll
+        for (int c = 0; c < DM; ++c) {
+          if (c >= D) break;
           float dmu = 0.f, dlv = 0.f;
           if (m) {
-            const float mu = a.par[r * 2 * D + c];
-            const float lv = a.par[r * 2 * D + D + c];
-            const float xv = a.x[(b * D + c) * a.T + t];
+            const float mu = cur.par[c];
+            const float lv = cur.par[DM + c];
+            const float xv = cur.x[c];
             const float ev = __expf(lv);
             const float var = fmaxf(ev, 1e-8f);
             const float df = mu - xv;
@@ -200,16 +223,18 @@ __global__ __launch_bounds__(256, 1) void elbo_head_mfma_kernel(HeadArgs a) {
             dlv = (ev >= 1e-8f) ? 0.5f * (1.f - r2) * inv_n : 0.f;
           }
           if (a.need_grad) {
-            a.dpar[r * 2 * D + c] = dmu;
-            a.dpar[r * 2 * D + D + c] = dlv;
+            a.dpar[r * ld4(2 * D) + c] = dmu;
+            a.dpar[r * ld4(2 * D) + D + c] = dlv;
           }
         }
+        if (a.need_grad)
+          for (int c = 2 * D; c < ld4(2 * D); ++c) a.dpar[r * ld4(2 * D) + c] = 0.f;
         float lgv[K], qv[K];
         float mx = -__builtin_inff();
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-          lgv[k] = valid ? a.logits[r * K + k] : 0.f;
-          qv[k] = sh.qS[(p + 1) * 4 + k];
+          lgv[k] = valid ? cur.lg[k] : 0.f;
+          qv[k] = valid ? cur.q[k] : 0.f;
           mx = fmaxf(mx, lgv[k]);
         }
         float se = 0.f;
@@ -221,8 +246,10 @@ __global__ __launch_bounds__(256, 1) void elbo_head_mfma_kernel(HeadArgs a) {
         for (int k = 0; k < K; ++k) f = fmaf(qv[k], lgv[k] - lse, f);
         if (m) s_ent -= f;
         if (a.need_grad) {
+          f32x4 d4 = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int k = 0; k < K; ++k) a.dlx[r * K + k] = m ? cent * qv[k] * ((lgv[k] - lse) - f) : 0.f;
+          for (int k = 0; k < K; ++k) d4[k] = m ? cent * qv[k] * ((lgv[k] - lse) - f) : 0.f;
+          *reinterpret_cast<f32x4*>(a.dlx + r * 4) = d4;
         }
         if (valid && t == 0) {
 #pragma unroll
@@ -273,6 +300,7 @@ __global__ __launch_bounds__(256, 1) void elbo_head_mfma_kernel(HeadArgs a) {
           int64_t b;
           int t;
           const bool valid = row_bt(r, a.R, a.T, b, t);
+          f32x4 d4 = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int j = 0; j < K; ++j) {
             float nx = 0.f;
@@ -280,55 +308,70 @@ __global__ __launch_bounds__(256, 1) void elbo_head_mfma_kernel(HeadArgs a) {
             for (int jj = 0; jj < K; ++jj) nx = fmaf(qn[jj], lan[j * K + jj], nx);
             float v = cpri * (w * dq[j] + wn * nx);
             if (valid && t == 0) v = fmaf(cpri, sh.lpS[j], v);
-            a.dqx[r * K + j] = valid ? v : 0.f;
+            d4[j] = valid ? v : 0.f;
           }
+          *reinterpret_cast<f32x4*>(a.dqx + r * 4) = d4;
         }
       } else {
 #pragma unroll
         for (int ij = 0; ij < 16; ++ij) dl[ij] = 0.f;
       }
     }
-    if (!a.need_grad) continue;
-    __syncthreads();
-    // ---------------- C: MLP backward (MFMA)
-    float* hS = sh.hS[wave];
-    float* dhS = sh.dhS[wave];
-    for (int pbi = 0; pbi < 4; ++pbi) {
-      const int p0 = (wave * 4 + pbi) * 16;
-      const float ub0 = sh.uS[(p0 + l16) * 8 + lg4];
-      const float ub1 = sh.uS[(p0 + l16) * 8 + 4 + lg4];
-      const f32x4 dlb = *reinterpret_cast<const f32x4*>(&sh.dlgS[(p0 + l16) * 16 + 4 * lg4]);
+    {
+      const int64_t nt = tile + gridDim.x;
+      if (nt < a.ntiles) load_row<K, DM>(a, nt * MOWN + tid, nxt);
+    }
+    if (a.need_grad) {
+      __syncthreads();
+      // ---------------- C: MLP backward (MFMA)
+      float* hT = sh.hT[wave];
+      float* dT = sh.dT[wave];
+      for (int pbi = 0; pbi < 4; ++pbi) {
+        const int p0 = (wave * 4 + pbi) * 16;
+        const float ub0 = sh.uS[(p0 + l16) * 8 + lg4];
+        const float ub1 = sh.uS[(p0 + l16) * 8 + 4 + lg4];
+        const f32x4 dlb = *reinterpret_cast<const f32x4*>(&sh.dlgS[(p0 + l16) * 16 + 4 * lg4]);
+        float dla[4], ua[4];
 #pragma unroll
-      for (int hb = 0; hb < HB; ++hb) {
-        f32x4 h = f32x4{0.f, 0.f, 0.f, 0.f};
-        h = mfma16x16x4(w1f[hb][0], ub0, h);
-        h = mfma16x16x4(w1f[hb][1], ub1, h);
-        // dhid^T block: A[i = h][k = ij = 4*lg4 + s] = W2[ij][h], B[k][j = p] = dlg[p][ij]
-        f32x4 dh = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-          dh = mfma16x16x4(sh.W2S[(4 * lg4 + s) * S::LDW2 + hb * 16 + l16], dlb[s], dh);
-        f32x4 hr, dm;
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          hr[v] = fmaxf(h[v], 0.f);
-          dm[v] = h[v] > 0.f ? dh[v] : 0.f;
+        for (int s4 = 0; s4 < 4; ++s4) {
+          const int pr = p0 + 4 * s4 + lg4;
+          dla[s4] = sh.dlgS[pr * 16 + l16];
+          const float uv = sh.uS[pr * 8 + (l16 & 7)];
+          ua[s4] = l16 < 8 ? uv : 0.f;
         }
-        *reinterpret_cast<f32x4*>(&hS[l16 * S::LDH + hb * 16 + 4 * lg4]) = hr;
-        *reinterpret_cast<f32x4*>(&dhS[l16 * S::LDH + hb * 16 + 4 * lg4]) = dm;
-      }
-      // contractions over the 16 rows of the block (k = p = 4*s + lg4)
+        // db2: contraction of dlg^T with a ones column
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int pr = 4 * s + lg4;
-        const float dla = sh.dlgS[(p0 + pr) * 16 + l16];
-        const float ua = l16 < 8 ? sh.uS[(p0 + pr) * 8 + (l16 & 7)] : 0.f;
+        for (int s4 = 0; s4 < 4; ++s4) gW2[HB] = mfma16x16x4(dla[s4], l16 == 0 ? 1.f : 0.f, gW2[HB]);
 #pragma unroll
-        for (int hb = 0; hb <= HB; ++hb) gW2[hb] = mfma16x16x4(dla, hS[pr * S::LDH + hb * 16 + l16], gW2[hb]);
+        for (int hb = 0; hb < HB; ++hb) {
+          f32x4 h = f32x4{0.f, 0.f, 0.f, 0.f};
+          h = mfma16x16x4(sh.W1S[(hb * 16 + l16) * 8 + lg4], ub0, h);
+          h = mfma16x16x4(sh.W1S[(hb * 16 + l16) * 8 + 4 + lg4], ub1, h);
+          // dhid^T block: A[i = h][k = ij = 4*lg4 + s] = W2[ij][h], B[k][j = p] = dlg[p][ij]
+          f32x4 dh = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int hb = 0; hb < HB; ++hb) gW1[hb] = mfma16x16x4(dhS[pr * S::LDH + hb * 16 + l16], ua, gW1[hb]);
+          for (int s4 = 0; s4 < 4; ++s4)
+            dh = mfma16x16x4(sh.W2S[(4 * lg4 + s4) * S::LDW2 + hb * 16 + l16], dlb[s4], dh);
+          f32x4 hr, dm;
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            hr[v] = fmaxf(h[v], 0.f);
+            dm[v] = h[v] > 0.f ? dh[v] : 0.f;
+          }
+          // transpose through LDS: [p][h_local]
+          *reinterpret_cast<f32x4*>(&hT[l16 * 16 + 4 * lg4]) = hr;
+          *reinterpret_cast<f32x4*>(&dT[l16 * 16 + 4 * lg4]) = dm;
+          // contractions over the 16 rows (k = p = 4*s + lg4)
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) {
+            const int pr = 4 * s4 + lg4;
+            gW2[hb] = mfma16x16x4(dla[s4], hT[pr * 16 + l16], gW2[hb]);
+            gW1[hb] = mfma16x16x4(dT[pr * 16 + l16], ua[s4], gW1[hb]);
+          }
+        }
       }
     }
+    cur = nxt;
   }
 
   // ---------------- epilogue: loss partials, q0 sums, weight-gradient partials
@@ -414,14 +457,17 @@ __global__ __launch_bounds__(256, 1) void elbo_head_mfma_kernel(HeadArgs a) {
 }
 
 bool head_mfma_supported(const HeadArgs& a) {
-  return a.K >= 1 && a.K <= 4 && a.U <= 7 && (a.TH == 64 || a.TH == 128);
+  return a.K >= 1 && a.K <= 4 && a.U <= 7 && (a.TH == 64 || a.TH == 128) && a.D <= 16;
 }
 
 int launch_head_mfma(const HeadArgs& a, int grid, hipStream_t s) {
 #define VQHMM_HM(KV, HBV)                                                                    \
   {                                                                                          \
     const size_t lds = sizeof(HeadLds<KV, HBV>);                                             \
-    elbo_head_mfma_kernel<KV, HBV><<<grid, 256, lds, s>>>(a);                                \
+    if (a.D <= 8)                                                                            \
+      elbo_head_mfma_kernel<KV, HBV, 8><<<grid, 256, lds, s>>>(a);                           \
+    else                                                                                     \
+      elbo_head_mfma_kernel<KV, HBV, 16><<<grid, 256, lds, s>>>(a);                          \
   }
   const int HB = a.TH / 16;
   switch (a.K * 10 + HB) {

@@ -5,9 +5,10 @@
 
 namespace vqhmm {
 
+// All PCL tensors below have row stride ld4(channels) with zero pad channels.
 struct ConvArgs {
   const float* src;  // input activations
-  int src_cf;        // 1: CF (B, Kc, T); 0: PCL (R, Kc)
+  int src_cf;        // 1: CF (B, Kc, T) (generic kernel only); 0: PCL (R, ld4(Kc))
   int Kc;            // input channels (GEMM K per tap)
   int64_t R;
   int T;
@@ -18,14 +19,14 @@ struct ConvArgs {
   const float* scale;// device scalar multiplying the accumulator, or null
   int N;             // output channels
   int act;           // 0 none, 1 relu, 2 multiply by (aux > 0)
-  const float* aux;  // PCL (R, N) for act == 2
-  float* out;        // PCL (R, N) or null
+  const float* aux;  // PCL (R, ld4(N)) for act == 2
+  float* out;        // PCL (R, ld4(N)) or null
   float* out_cf;     // CF (B, N, T) or null
   // fused 1x1 tail on the activated output (requires N <= BN)
   const float* tW;   // (C2, N)
   const float* tb;   // (C2)
   int C2;
-  float* t_out;      // PCL (R, C2)
+  float* t_out;      // PCL (R, ld4(C2))
   float* t_cf0;      // CF, channels [0, t_split)
   float* t_cf1;      // CF, channels [t_split, C2)
   int t_split;
@@ -34,8 +35,8 @@ struct ConvArgs {
 };
 
 struct WgradArgs {
-  const float* dy;   // PCL (R, N) output gradient (pad rows zero)
-  const float* x;    // layer input: PCL (R, C) or CF (B, C, T)
+  const float* dy;   // PCL (R, ld4(N)) output gradient (pad rows zero)
+  const float* x;    // layer input: PCL (R, ld4(C)) or CF (B, C, T) (generic kernel only)
   int x_cf;
   int64_t R;
   int T;
@@ -50,13 +51,12 @@ struct HeadArgs {
   int T;
   int64_t R;
   int D, K, U, TH;
-  const float* x;        // CF (B, D, T)
-  const float* u;        // (B, U, T) with strides below
-  int64_t u_sc, u_st;    // u[b, c, t] = u[b*U*T + c*u_sc + t*u_st]
+  const float* x;        // PCL (R, ld4(D))  (x converted once per step)
+  const float* u;        // PCL (R, ld4(U))
   const int64_t* lengths;
-  const float* par;      // PCL (R, 2D): mu | logvar
-  const float* logits;   // PCL (R, K)
-  const float* q;        // PCL (R, K)
+  const float* par;      // PCL (R, ld4(2D)): mu | logvar
+  const float* logits;   // PCL (R, ld4(K))
+  const float* q;        // PCL (R, ld4(K))
   const float* W1;       // (TH, U)
   const float* b1;       // (TH)
   const float* W2;       // (K*K, TH)
@@ -64,9 +64,9 @@ struct HeadArgs {
   const float* log_prior;// (K)
   float beta;
   int need_grad;
-  float* dpar;           // PCL (R, 2D)
-  float* dqx;            // PCL (R, K)  dL/dq from the prior term
-  float* dlx;            // PCL (R, K)  dL/dlogits from the entropy term
+  float* dpar;           // PCL (R, ld4(2D))
+  float* dqx;            // PCL (R, ld4(K))  dL/dq from the prior term
+  float* dlx;            // PCL (R, ld4(K))  dL/dlogits from the entropy term
   double* part;          // [gridDim.x][4]: recon_sum, init_sum, trans_sum, ent_sum
   float* slab_W1;        // [grid][TH*U]
   float* slab_b1;        // [grid][TH]
@@ -117,6 +117,9 @@ int launch_logits_bwd(const float* q, const float* dq_dec, const float* dqx, con
                       int64_t R, int K, float* dlog, hipStream_t s);
 int launch_log_prior_grad(const float* q0sum, const float* log_prior, int K, float c, const float* scale, float* out,
                           hipStream_t s);
+// CF / (B,T,C) tensor -> PCL (R, ld4(C)) with zero pad rows / channels:
+// dst[b*(T+2)+1+t][c] = src[b*C*T + c*sc + t*st]
+int launch_to_pcl(const float* src, int C, int64_t B, int T, int64_t sc, int64_t st, float* dst, hipStream_t s);
 int launch_log_softmax_vec(const float* x, int K, float* out, hipStream_t s);
 size_t viterbi_ws_bytes(int64_t B, int64_t T, int64_t K);
 int launch_viterbi(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths, int64_t B,

@@ -174,16 +174,17 @@ __global__ void logits_bwd_kernel(const float* q, const float* dq_dec, const flo
                                   const float* scale, int64_t R, int K, float* dlog) {
   const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (r >= R) return;
+  const int L = ld4(K);  // pad channels: q = dq = dlx = 0 there, so dlog stays 0
   const float sc = scale ? *scale : 1.f;
   float s = 0.f;
-  for (int k = 0; k < K; ++k) {
-    const float dq = dq_dec[r * K + k] + sc * dqx[r * K + k];
-    s = fmaf(q[r * K + k], dq, s);
+  for (int k = 0; k < L; ++k) {
+    const float dq = dq_dec[r * L + k] + sc * dqx[r * L + k];
+    s = fmaf(q[r * L + k], dq, s);
   }
-  for (int k = 0; k < K; ++k) {
-    const float qk = q[r * K + k];
-    const float dq = dq_dec[r * K + k] + sc * dqx[r * K + k];
-    dlog[r * K + k] = qk * (dq - s) + sc * dlx[r * K + k];
+  for (int k = 0; k < L; ++k) {
+    const float qk = q[r * L + k];
+    const float dq = dq_dec[r * L + k] + sc * dqx[r * L + k];
+    dlog[r * L + k] = qk * (dq - s) + sc * dlx[r * L + k];
   }
 }
 
@@ -267,6 +268,33 @@ __global__ void log_softmax_vec_kernel(const float* x, int K, float* out) {
 }
 int launch_log_softmax_vec(const float* x, int K, float* out, hipStream_t s) {
   log_softmax_vec_kernel<<<1, 64, 0, s>>>(x, K, out);
+  VQHMM_LAUNCH_CHECK();
+  return VQHMM_OK;
+}
+}  // namespace vqhmm
+
+namespace vqhmm {
+__global__ __launch_bounds__(256) void to_pcl_kernel(const float* __restrict__ src, int C, int64_t B, int T,
+                                                     int64_t sc, int64_t st, float* __restrict__ dst) {
+  const int L4 = ld4(C) / 4;
+  const int64_t R = B * (int64_t)(T + 2);
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // float4 slot
+  if (i >= R * L4) return;
+  const int64_t r = i / L4;
+  const int c0 = (int)(i - r * L4) * 4;
+  int64_t b;
+  int t;
+  const bool valid = row_bt(r, R, T, b, t);
+  float e[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    e[k] = (valid && c0 + k < C) ? src[b * (int64_t)C * T + (c0 + k) * sc + (int64_t)t * st] : 0.f;
+  reinterpret_cast<float4*>(dst)[i] = make_float4(e[0], e[1], e[2], e[3]);
+}
+int launch_to_pcl(const float* src, int C, int64_t B, int T, int64_t sc, int64_t st, float* dst, hipStream_t s) {
+  const int64_t n = B * (int64_t)(T + 2) * (ld4(C) / 4);
+  if (n == 0) return VQHMM_OK;
+  to_pcl_kernel<<<(unsigned)cdiv(n, 256), 256, 0, s>>>(src, C, B, T, sc, st, dst);
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
 }

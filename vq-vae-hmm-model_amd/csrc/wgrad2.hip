@@ -37,69 +37,42 @@ __global__ __launch_bounds__(256) void wgrad2_kernel(WgradArgs a, int WN, int WC
   const int64_t chunk = blockIdx.x;
   const int64_t rbeg = chunk * a.rows_per_chunk;
   const int64_t rend = min(a.R, rbeg + a.rows_per_chunk);
-  const int64_t Tp = (int64_t)a.T + 2;
-  const bool vdy = (a.N % 4) == 0;
-  const bool vx = !a.x_cf && (a.C % 4) == 0;
 
+  // Raw float4 loads from clamped addresses (row strides ld4(N), ld4(C); pad
+  // channels are zero in memory).  No select next to a load, so the prefetch
+  // stays in flight across the MFMAs; rows outside the chunk / channels past
+  // the row are zeroed when the registers are written to LDS.
+  const int ldn = ld4(a.N), ldc = ld4(a.C);
   auto load_dy = [&](int64_t r0, float4* p) {
 #pragma unroll
     for (int k = 0; k < PD; ++k) {
       const int s = tid + k * 256;
       const int row = s / (NPAD / 4), c = (s - row * (NPAD / 4)) * 4;
-      const int64_t r = r0 + row;
-      const bool rin = s < DY4 && r < rend;
-      const int64_t rc = rin ? r : rbeg;
-      if (vdy) {
-        const bool ok = rin && c < a.N;
-        const float4 v = *reinterpret_cast<const float4*>(a.dy + rc * a.N + (ok ? c : 0));
-        p[k] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
-      } else {
-        float e[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const bool ok = rin && c + q < a.N;
-          const float v = a.dy[rc * a.N + (ok ? c + q : 0)];
-          e[q] = ok ? v : 0.f;
-        }
-        p[k] = make_float4(e[0], e[1], e[2], e[3]);
-      }
+      int64_t r = r0 + row;
+      r = r < rend ? r : rend - 1;
+      p[k] = *reinterpret_cast<const float4*>(a.dy + r * ldn + min(c, ldn - 4));
     }
+  };
+  auto mask_dy = [&](int64_t r0, int k, float4 v) {
+    const int s = tid + k * 256;
+    const int row = s / (NPAD / 4), c = (s - row * (NPAD / 4)) * 4;
+    return (r0 + row < rend && c < ldn) ? v : make_float4(0.f, 0.f, 0.f, 0.f);
   };
   auto load_x = [&](int64_t r0, float4* p) {
 #pragma unroll
     for (int k = 0; k < PX; ++k) {
       const int s = tid + k * 256;
       const int row = s / (CPAD / 4), c = (s - row * (CPAD / 4)) * 4;
-      const int64_t r = r0 - 1 + row;
-      const bool rin = s < X4 && r >= 0 && r < a.R;
-      const int64_t rc = rin ? r : 0;
-      if (a.x_cf) {
-        const int64_t b = rc / Tp;
-        const int t = (int)(rc - b * Tp) - 1;
-        const bool tin = rin && t >= 0 && t < a.T;
-        float e[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const bool ok = tin && c + q < a.C;
-          const float v = a.x[(b * a.C + (ok ? c + q : 0)) * a.T + (tin ? t : 0)];
-          e[q] = ok ? v : 0.f;
-        }
-        p[k] = make_float4(e[0], e[1], e[2], e[3]);
-      } else if (vx) {
-        const bool ok = rin && c < a.C;
-        const float4 v = *reinterpret_cast<const float4*>(a.x + rc * a.C + (ok ? c : 0));
-        p[k] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
-      } else {
-        float e[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const bool ok = rin && c + q < a.C;
-          const float v = a.x[rc * a.C + (ok ? c + q : 0)];
-          e[q] = ok ? v : 0.f;
-        }
-        p[k] = make_float4(e[0], e[1], e[2], e[3]);
-      }
+      int64_t r = r0 - 1 + row;
+      r = r < 0 ? 0 : (r >= a.R ? a.R - 1 : r);
+      p[k] = *reinterpret_cast<const float4*>(a.x + r * ldc + min(c, ldc - 4));
     }
+  };
+  auto mask_x = [&](int64_t r0, int k, float4 v) {
+    const int s = tid + k * 256;
+    const int row = s / (CPAD / 4), c = (s - row * (CPAD / 4)) * 4;
+    const int64_t r = r0 - 1 + row;
+    return (r >= 0 && r < a.R && c < ldc) ? v : make_float4(0.f, 0.f, 0.f, 0.f);
   };
 
   f32x4 acc[KS][NBW][CBW];
@@ -122,7 +95,7 @@ __global__ __launch_bounds__(256) void wgrad2_kernel(WgradArgs a, int WN, int WC
       const int s = tid + k * 256;
       if (s < DY4) {
         const int row = s / (NPAD / 4), c = (s - row * (NPAD / 4)) * 4;
-        *reinterpret_cast<float4*>(dys + row * LDA + c) = pdy[k];
+        *reinterpret_cast<float4*>(dys + row * LDA + c) = mask_dy(r0, k, pdy[k]);
       }
     }
 #pragma unroll
@@ -130,7 +103,7 @@ __global__ __launch_bounds__(256) void wgrad2_kernel(WgradArgs a, int WN, int WC
       const int s = tid + k * 256;
       if (s < X4) {
         const int row = s / (CPAD / 4), c = (s - row * (CPAD / 4)) * 4;
-        *reinterpret_cast<float4*>(xs + row * LDB + c) = px[k];
+        *reinterpret_cast<float4*>(xs + row * LDB + c) = mask_x(r0, k, px[k]);
       }
     }
     __syncthreads();
@@ -219,7 +192,7 @@ __global__ __launch_bounds__(256) void wgrad2_kernel(WgradArgs a, int WN, int WC
   }
 }
 
-bool wgrad2_supported(const WgradArgs& a) { return a.N <= 64 && a.C <= 64; }
+bool wgrad2_supported(const WgradArgs& a) { return !a.x_cf && a.N <= 64 && a.C <= 64; }
 
 int64_t wgrad2_rows(int64_t R, int N, int C, int ks) {
   // big outputs: one chunk per CU (small slabs); small outputs: 2 per CU
