@@ -63,8 +63,11 @@ int vqhmm_param_layout(const vqhmm_dims_t* dims, int64_t offsets[VQHMM_NPARAMS +
  * Nearest-codeword quantization (semantics pseudocode.txt:11
  * `quantize`, hard regimes backtesting.py:154-155 — no reference code).
  * z (B, Dv, T) CF, codebook (K, Dv) -> idx (B, T) int32, dmin (B, T) fp32
- * (nullable).  dist_k = fmaf chain over d ascending of (z_d - c_kd)^2 from
- * +0.0f; ties -> lowest k.  Bit-exact vs oracle/c/hmm_oracle.c. */
+ * (nullable).  Expansion form ||z||^2 + ||c_k||^2 - 2 z.c_k, evaluated as
+ * s_k = fmaf chain over d ascending of z_d * (-2 c_kd) starting from
+ * ||c_k||^2 (itself the fmaf chain of c_kd^2); idx = first k with the
+ * smallest s_k; dmin = s_idx + ((q0 + q1) + (q2 + q3)), q_r the fmaf chain of
+ * z_d^2 over d = r (mod 4).  Bit-exact vs oracle/c/hmm_oracle.c. */
 int vqhmm_vq_argmin_f32(const float* z, int64_t B, int64_t Dv, int64_t T,
                         const float* codebook, int64_t K,
                         int32_t* idx, float* dmin, void* stream);

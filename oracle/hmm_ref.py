@@ -10,10 +10,15 @@ Semantic sources (no reference code exists for these):
   Viterbi          same tables, max-plus instead of log-sum-exp.
 
 Exact contracts (the HIP kernels follow them operation for operation):
-  vq_argmin  dist[n,k] = fmaf chain over d = 0..Dv-1 of (z[n,d]-c[k,d])^2
-             starting from +0.0f; idx = first k with the smallest dist.
-             (fmaf is emulated exactly here via the C oracle; the pure-numpy
-             `vq_argmin_np` uses float64 and is only used for KATs.)
+  vq_argmin  expansion form ||z||^2 + ||c_k||^2 - 2 z.c_k, evaluated as
+             cn[k]   = fmaf chain over d = 0..Dv-1 of c[k,d]^2 from +0.0f,
+             s[n,k]  = fmaf chain over d = 0..Dv-1 of z[n,d]*(-2 c[k,d])
+                       starting from cn[k]  (what a f32 MFMA computes),
+             idx     = first k with the smallest s (ties -> lowest k),
+             dmin    = s[n,idx] + ((q0 + q1) + (q2 + q3)), q_r = fmaf chain
+                       of z^2 over the d = r (mod 4).
+             (fmaf is exact in the C oracle, oracle/c/hmm_oracle.c; the
+             pure-numpy `vq_argmin_np` uses float64 and is only used for KATs.)
   viterbi    d0[j] = log_pi[j] + e[0,j];
              d_t[j] = (max_i (d_{t-1}[i] + log_A[t,i,j])) + e[t,j]   (fp32,
              i ascending, strict '>' so ties keep the lowest i);

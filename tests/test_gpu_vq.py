@@ -18,8 +18,10 @@ def run(z, cb):
     return idx.cpu().numpy(), d.cpu().numpy()
 
 
-@pytest.mark.parametrize("B,Dv,T,K", [(3, 5, 200, 3), (2, 64, 100, 32), (4, 16, 77, 8), (1, 1, 1, 1),
-                                      (2, 33, 129, 5), (3, 64, 50, 70), (5, 7, 3, 17)])
+# T % 4 == 0 -> row-load MFMA kernel; otherwise the 32-position MFMA kernel; K > 32 -> VALU kernel
+@pytest.mark.parametrize("B,Dv,T,K", [(3, 5, 200, 3), (2, 64, 100, 32), (2, 64, 96, 17), (3, 30, 64, 32),
+                                      (1, 3, 4, 2), (4, 16, 77, 8), (1, 1, 1, 1), (2, 33, 129, 5),
+                                      (3, 64, 50, 70), (5, 7, 3, 17)])
 def test_vq_bit_exact(B, Dv, T, K):
     rng = np.random.default_rng(B * 1000 + Dv * 10 + K)
     z = rng.standard_normal((B, Dv, T)).astype(np.float32)
@@ -37,7 +39,10 @@ def test_vq_ties_and_duplicates():
     z = np.repeat(cb[[1, 3, 5]].T[None], 2, axis=0).astype(np.float32)  # z exactly on codewords
     idx, d = run(z, cb)
     assert np.all(idx[:, 0] == 1) and np.all(idx[:, 1] == 1) and np.all(idx[:, 2] == 5)
-    assert np.all(d == 0)
+    ridx, rd = c_oracle.vq_argmin(z, cb)
+    assert np.array_equal(d.view(np.uint32), rd.view(np.uint32))
+    # expansion form: the distance of an exact hit is zero up to rounding of ||c||^2
+    assert np.abs(d).max() <= 1e-5 * (cb ** 2).sum(1).max()
 
 
 def test_vq_one_hot_equals_argmax():

@@ -48,6 +48,17 @@ def bench_vq(a):
                       "GBps": byts / t / 1e9, "frac_hbm": byts / t / HBM_PEAK}))
 
 
+def bench_stream(a):
+    """Bandwidth references on the VQ input size: torch read-reduce and copy of z."""
+    z = torch.randn(a.B, a.Dv, a.T, device="cuda")
+    out = torch.empty_like(z)
+    nb = z.numel() * 4
+    t_sum = time_fn(lambda: z.sum())
+    t_cp = time_fn(lambda: out.copy_(z))
+    print(json.dumps({"kernel": "torch_stream", "bytes": nb, "sum_us": t_sum * 1e6, "sum_GBps": nb / t_sum / 1e9,
+                      "copy_us": t_cp * 1e6, "copy_GBps": 2 * nb / t_cp / 1e9}))
+
+
 def hmm_tables(B, T, K, seed=7):
     g = torch.Generator(device="cuda").manual_seed(seed)
     log_pi = torch.log_softmax(torch.randn(K, device="cuda", generator=g), -1)
@@ -105,4 +116,4 @@ if __name__ == "__main__":
     ap.add_argument("--T", type=int, default=200)
     ap.add_argument("--K", type=int, default=32)
     a = ap.parse_args()
-    {"vq": bench_vq, "viterbi": bench_viterbi, "fwdbwd": bench_fwdbwd}[a.what](a)
+    {"vq": bench_vq, "stream": bench_stream, "viterbi": bench_viterbi, "fwdbwd": bench_fwdbwd}[a.what](a)

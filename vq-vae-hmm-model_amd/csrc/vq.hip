@@ -2,24 +2,233 @@
 //
 // Semantics (no reference code exists): pseudocode.txt:11
 // `quantize(z_e, codebook)` and the hard-regime argmax of backtesting.py:154-155.
-// Exact contract (oracle/hmm_ref.py, oracle/c/hmm_oracle.c): per k the distance is
-// the fmaf chain over d = 0..Dv-1 of (z_d - c_kd)^2 from +0.0f, and the first k
-// with the smallest distance wins.  The kernel evaluates exactly that chain.
+// Exact contract (oracle/hmm_ref.py, oracle/c/hmm_oracle.c), the expansion form
+// ||z||^2 + ||c_k||^2 - 2 z.c_k of SURVEY.md §8d:
+//   cn_k = fmaf chain over d of c_kd^2 from +0,
+//   s_k  = fmaf chain over d = 0..Dv-1 of z_d * (-2 c_kd) starting from cn_k,
+//   idx  = first k with the smallest s_k,  dmin = s_idx + ((q0 + q1) + (q2 + q3))
+// where q_r is the fmaf chain of z_d^2 over d = r (mod 4).  A f32 MFMA is
+// bit-for-bit a k-ordered fmaf chain, so the matrix cores evaluate s_k exactly.
 //
-// Design (cfg3: 4*N*Dv bytes in, 4*N out; 2 VALU ops per (n,k,d) -> VALU and
-// HBM roofs are within 30% of each other, so both the load path and the
-// VALU stream are kept dense):
-//  * one wave = 128 consecutive positions, lane l owns positions n0+l and
-//    n0+64+l; every z load is a coalesced 256-B wave access of the CF tensor;
-//  * a block of KB codewords is staged in LDS once per workgroup and read
-//    with wave-uniform float4 broadcasts: one ds_read_b128 feeds 16 VALU ops
-//    (4 dims x 2 positions x {v_sub, v_fma});
-//  * per lane 2*KB independent fma chains give ILP; z for a 16-dim chunk
-//    stays in VGPRs and is reused across all KB codewords.
+// Main kernel (K <= 32, Dv <= 64 — cfg2 and cfg3):
+//  * one v_mfma_f32_32x32x2_f32 per pair of dims: A = the codebook pre-scaled by
+//    -2 (32 codes x 2 dims, resident in VGPRs for the whole launch), B = the z
+//    tile (2 dims x 32 positions), C starts at cn_k;
+//  * every lane loads one dword per dim pair: each wave load is two 128-B
+//    segments of the channels-first z; the next tile is prefetched into
+//    registers while the MFMAs of the current one run;
+//  * the argmin is 15 in-lane compares + one lane^32 exchange (lowest code on
+//    ties); the VALU only does the argmin and the ||z||^2 chains.
+// Fallback (K > 32 or Dv > 64): VALU kernel over LDS codebook blocks, same chain.
+#include <stdlib.h>
+
 #include "kernels.h"
 
 namespace vqhmm {
 
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <int S>  // MFMA steps of 2 dims each, 2*S >= Dv
+__global__ __launch_bounds__(256) void vq_mfma_kernel(const float* __restrict__ z, int64_t B, int Dv, int T,
+                                                      const float* __restrict__ cb, int K, int32_t* __restrict__ idx,
+                                                      float* __restrict__ dmin, int64_t tiles) {
+  const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31;
+  const int64_t N = B * (int64_t)T;
+  const int64_t wave0 = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+
+  auto load = [&](int64_t tile, float* zr) {
+    int64_t p = tile * 32 + j;
+    p = p < N ? p : N - 1;  // clamped address; the result of a clamped lane is not stored
+    const int64_t b = p / T;
+    const float* base = z + b * (int64_t)Dv * T + (p - b * T);
+#pragma unroll
+    for (int s = 0; s < S; ++s) zr[s] = base[(int64_t)min(2 * s + h, Dv - 1) * T];  // padded dims: a = 0
+  };
+  float zc[S];
+  if (wave0 < tiles) load(wave0, zc);  // first tile in flight during the codebook prologue
+
+  // A fragments: code j, dim 2s+h, pre-scaled by -2 (exact).  Loads first from
+  // clamped addresses (all in flight together), masks after.
+  const int jc = min(j, K - 1);
+  float a[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) a[s] = cb[(int64_t)jc * Dv + min(2 * s + h, Dv - 1)];
+#pragma unroll
+  for (int s = 0; s < S; ++s) a[s] = (j < K && 2 * s + h < Dv) ? -2.0f * a[s] : 0.0f;
+  // cn_j = chain over d ascending: even dims live in lane h=0, odd in h=1
+  float cn = 0.0f;
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const float o = __shfl_xor(a[s], 32);
+    const float ce = -0.5f * (h ? o : a[s]), co = -0.5f * (h ? a[s] : o);
+    if (2 * s < Dv) cn = __builtin_fmaf(ce, ce, cn);
+    if (2 * s + 1 < Dv) cn = __builtin_fmaf(co, co, cn);
+  }
+  if (j >= K) cn = __builtin_inff();
+  // C/D rows of this lane: code i(v) = (v & 3) + 8 (v >> 2) + 4 h, ascending in v
+  float init[16];
+#pragma unroll
+  for (int v = 0; v < 16; ++v) init[v] = __shfl(cn, (v & 3) + 8 * (v >> 2) + 4 * h);
+
+  for (int64_t tile = wave0; tile < tiles; tile += nwaves) {
+    float zn[S];
+    const bool more = tile + nwaves < tiles;
+    if (more) load(tile + nwaves, zn);
+    f32x16 acc;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[v] = init[v];
+#pragma unroll
+    for (int s = 0; s < S; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], zc[s], acc, 0, 0, 0);
+    // ||z||^2 partial chains: lane h holds d = 2s+h, i.e. d mod 4 = h (s even) or
+    // 2+h (s odd); zn = (q0 + q1) + (q2 + q3)
+    float qa = 0.0f, qb = 0.0f;  // d mod 4 = h, 2 + h
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const float zv = (2 * s + h < Dv) ? zc[s] : 0.0f;
+      if (2 * s < Dv) {
+        if (s & 1) qb = __builtin_fmaf(zv, zv, qb);
+        else qa = __builtin_fmaf(zv, zv, qa);
+      }
+    }
+    const float pqa = __shfl_xor(qa, 32), pqb = __shfl_xor(qb, 32);
+    const float zp = (qa + pqa) + (qb + pqb);
+    float best = __builtin_inff();
+    int arg = 4 * h;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      if (acc[v] < best) { best = acc[v]; arg = (v & 3) + 8 * (v >> 2) + 4 * h; }
+    }
+    const float pb = __shfl_xor(best, 32);
+    const int pa = __shfl_xor(arg, 32);
+    if (pb < best || (pb == best && pa < arg)) { best = pb; arg = pa; }
+    const int64_t p = tile * 32 + j;
+    if (h == 0 && p < N) {
+      idx[p] = arg;
+      if (dmin) dmin[p] = best + zp;
+    }
+    if (more) {
+#pragma unroll
+      for (int s = 0; s < S; ++s) zc[s] = zn[s];
+    }
+  }
+}
+
+// Row-load variant (T % 4 == 0): a 64-position tile per wave, lane (g, j) =
+// (lane >> 4, lane & 15) loads float4 z[d = 4 dg + g][t .. t+3] of positions
+// 4j .. 4j+3 (each wave load = four 256-B row runs).  v_mfma_f32_16x16x4_f32 m
+// (m = 0..3) takes component m as B[k = g][col j] = z[4 dg + g][position 4j + m];
+// A = -2 c[16 cb + j][4 dg + g].  CB x 4 independent accumulators per tile.
+template <int DG, int CB>  // Dv <= 4 DG, K <= 16 CB
+__global__ __launch_bounds__(256) void vq_rows_kernel(const float* __restrict__ z, int64_t B, int Dv, int T,
+                                                      const float* __restrict__ cb, int K, int32_t* __restrict__ idx,
+                                                      float* __restrict__ dmin, int64_t tiles) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
+  const int64_t N = B * (int64_t)T;
+  const int64_t wave0 = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+
+  // byte offsets are 32-bit (launcher guarantees 4*B*Dv*T < 2^32): a uniform base
+  // plus one VGPR offset per load; per-lane row offsets are tile-invariant
+  const char* zb = reinterpret_cast<const char*>(z);
+  uint32_t rowoff[DG];
+#pragma unroll
+  for (int dg = 0; dg < DG; ++dg) rowoff[dg] = (uint32_t)min(4 * dg + g, Dv - 1) * (uint32_t)T * 4u;
+  auto tile_off = [&](int64_t tile) -> uint32_t {
+    int64_t n = tile * 64 + 4 * j;
+    n = n < N ? n : N - 4;  // clamped address; clamped lanes store nothing
+    const int64_t b = n / T;
+    return (uint32_t)((b * (int64_t)Dv * T + (n - b * T)) * 4);
+  };
+  f32x4 zc[DG];
+  if (wave0 < tiles) {
+    const uint32_t o = tile_off(wave0);
+#pragma unroll
+    for (int dg = 0; dg < DG; ++dg) zc[dg] = *reinterpret_cast<const f32x4*>(zb + (o + rowoff[dg]));
+  }
+
+  float a[CB][DG];
+#pragma unroll
+  for (int c = 0; c < CB; ++c)
+#pragma unroll
+    for (int dg = 0; dg < DG; ++dg)
+      a[c][dg] = cb[(int64_t)min(16 * c + j, K - 1) * Dv + min(4 * dg + g, Dv - 1)];
+#pragma unroll
+  for (int c = 0; c < CB; ++c)
+#pragma unroll
+    for (int dg = 0; dg < DG; ++dg) a[c][dg] = (16 * c + j < K && 4 * dg + g < Dv) ? -2.0f * a[c][dg] : 0.0f;
+  // ||c||^2 of code 16 c + j in d order: dims 4 dg + r live in lane j + 16 r
+  float init[CB][4];
+#pragma unroll
+  for (int c = 0; c < CB; ++c) {
+    float cn = 0.0f;
+#pragma unroll
+    for (int dg = 0; dg < DG; ++dg)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = -0.5f * __shfl(a[c][dg], j + 16 * r);
+        if (4 * dg + r < Dv) cn = __builtin_fmaf(v, v, cn);
+      }
+    if (16 * c + j >= K) cn = __builtin_inff();
+#pragma unroll
+    for (int v = 0; v < 4; ++v) init[c][v] = __shfl(cn, 4 * g + v);  // rows of this lane: codes 16c + 4g + v
+  }
+
+  for (int64_t tile = wave0; tile < tiles; tile += nwaves) {
+    // next tile's row pointer; its loads are issued dim-group by dim-group as
+    // soon as the current tile's group has gone through the MFMAs
+    const bool more = tile + nwaves < tiles;
+    const uint32_t no = tile_off(more ? tile + nwaves : tile);
+    f32x4 acc[CB][4];
+#pragma unroll
+    for (int c = 0; c < CB; ++c)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) acc[c][m] = f32x4{init[c][0], init[c][1], init[c][2], init[c][3]};
+    // ||z||^2 partial chain of this lane's residue d = g (mod 4), per position m
+    float q[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int dg = 0; dg < DG; ++dg) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int c = 0; c < CB; ++c) acc[c][m] = mfma16x16x4(a[c][dg], zc[dg][m], acc[c][m]);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const float zv = (4 * dg + g < Dv) ? zc[dg][m] : 0.0f;
+        if (4 * dg < Dv) q[m] = __builtin_fmaf(zv, zv, q[m]);
+      }
+      if (more) zc[dg] = *reinterpret_cast<const f32x4*>(zb + (no + rowoff[dg]));
+    }
+    float fb = 0.f, fz = 0.f;
+    int fa = 0;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      float best = __builtin_inff();
+      int arg = 4 * g;
+#pragma unroll
+      for (int c = 0; c < CB; ++c)
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          if (acc[c][m][v] < best) { best = acc[c][m][v]; arg = 16 * c + 4 * g + v; }
+#pragma unroll
+      for (int o = 16; o <= 32; o <<= 1) {
+        const float pb = __shfl_xor(best, o);
+        const int pa = __shfl_xor(arg, o);
+        if (pb < best || (pb == best && pa < arg)) { best = pb; arg = pa; }
+      }
+      const float s2 = q[m] + __shfl_xor(q[m], 16);  // q0+q1 (g < 2) or q2+q3 (g >= 2)
+      const float zz = s2 + __shfl_xor(s2, 32);
+      if (g == m) { fb = best; fa = arg; fz = zz; }
+    }
+    const int64_t n = tile * 64 + 4 * j + g;
+    if (n < N) {
+      idx[n] = fa;
+      if (dmin) dmin[n] = fb + fz;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- VALU fallback
 constexpr int VQ_DCH = 16;
 
 template <int KB>
@@ -27,7 +236,8 @@ __global__ __launch_bounds__(256) void vq_argmin_kernel(const float* __restrict_
                                                         const float* __restrict__ cb, int K, int ldc,
                                                         int32_t* __restrict__ idx, float* __restrict__ dmin) {
   extern __shared__ float4 cbs4[];
-  float* cbs = reinterpret_cast<float*>(cbs4);  // [KB][ldc], ldc = Dv rounded up to 16
+  float* cbs = reinterpret_cast<float*>(cbs4);  // [KB][ldc] = -2 c, ldc = Dv rounded up to 16
+  __shared__ float cns[KB];
   const int64_t N = B * (int64_t)T;
   const int lane = threadIdx.x & 63;
   const int64_t n0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 128;
@@ -39,53 +249,43 @@ __global__ __launch_bounds__(256) void vq_argmin_kernel(const float* __restrict_
 
   float best_a = __builtin_inff(), best_b = __builtin_inff();
   int arg_a = 0, arg_b = 0;
+  float qa[4] = {0.f, 0.f, 0.f, 0.f}, qb[4] = {0.f, 0.f, 0.f, 0.f};
   for (int kb = 0; kb < K; kb += KB) {
     const int kn = min(KB, K - kb);
     __syncthreads();
     for (int i = threadIdx.x; i < KB * ldc; i += 256) {
       const int k = i / ldc, d = i - k * ldc;
-      cbs[i] = (k < kn && d < Dv) ? cb[(int64_t)(kb + k) * Dv + d] : 0.0f;
+      cbs[i] = (k < kn && d < Dv) ? -2.0f * cb[(int64_t)(kb + k) * Dv + d] : 0.0f;
+    }
+    if (threadIdx.x < KB) {
+      float c2 = 0.f;
+      if ((int)threadIdx.x < kn)
+        for (int d = 0; d < Dv; ++d) {
+          const float c = cb[(int64_t)(kb + threadIdx.x) * Dv + d];
+          c2 = __builtin_fmaf(c, c, c2);
+        }
+      cns[threadIdx.x] = c2;
     }
     __syncthreads();
     float acc_a[KB], acc_b[KB];
 #pragma unroll
-    for (int k = 0; k < KB; ++k) acc_a[k] = acc_b[k] = 0.0f;
+    for (int k = 0; k < KB; ++k) acc_a[k] = acc_b[k] = cns[k];
     for (int dc = 0; dc < Dv; dc += VQ_DCH) {
       const int dn = min(VQ_DCH, Dv - dc);
-      float zca[VQ_DCH], zcb[VQ_DCH];
-      if (dn == VQ_DCH) {
+      for (int d = 0; d < dn; ++d) {
+        const float zva = va ? za[(int64_t)(dc + d) * T] : 0.0f;
+        const float zvb = vb ? zb[(int64_t)(dc + d) * T] : 0.0f;
+        if (kb == 0) {
+          const int r = (dc + d) & 3;
 #pragma unroll
-        for (int d = 0; d < VQ_DCH; ++d) {
-          zca[d] = va ? za[(int64_t)(dc + d) * T] : 0.0f;
-          zcb[d] = vb ? zb[(int64_t)(dc + d) * T] : 0.0f;
+          for (int rr = 0; rr < 4; ++rr)
+            if (rr == r) { qa[rr] = __builtin_fmaf(zva, zva, qa[rr]); qb[rr] = __builtin_fmaf(zvb, zvb, qb[rr]); }
         }
 #pragma unroll
         for (int k = 0; k < KB; ++k) {
-          const float4* c4 = reinterpret_cast<const float4*>(cbs + k * ldc + dc);
-#pragma unroll
-          for (int q = 0; q < VQ_DCH / 4; ++q) {
-            const float4 c = c4[q];
-            const float cc[4] = {c.x, c.y, c.z, c.w};
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float da = zca[4 * q + e] - cc[e];
-              const float db = zcb[4 * q + e] - cc[e];
-              acc_a[k] = __builtin_fmaf(da, da, acc_a[k]);
-              acc_b[k] = __builtin_fmaf(db, db, acc_b[k]);
-            }
-          }
-        }
-      } else {  // ragged last chunk: still strictly d-ascending per chain
-        for (int d = 0; d < dn; ++d) {
-          const float zva = va ? za[(int64_t)(dc + d) * T] : 0.0f;
-          const float zvb = vb ? zb[(int64_t)(dc + d) * T] : 0.0f;
-#pragma unroll
-          for (int k = 0; k < KB; ++k) {
-            const float c = cbs[k * ldc + dc + d];
-            const float da = zva - c, db = zvb - c;
-            acc_a[k] = __builtin_fmaf(da, da, acc_a[k]);
-            acc_b[k] = __builtin_fmaf(db, db, acc_b[k]);
-          }
+          const float c = cbs[k * ldc + dc + d];
+          acc_a[k] = __builtin_fmaf(zva, c, acc_a[k]);
+          acc_b[k] = __builtin_fmaf(zvb, c, acc_b[k]);
         }
       }
     }
@@ -97,8 +297,43 @@ __global__ __launch_bounds__(256) void vq_argmin_kernel(const float* __restrict_
       }
     }
   }
-  if (va) { idx[na] = arg_a; if (dmin) dmin[na] = best_a; }
-  if (vb) { idx[nb] = arg_b; if (dmin) dmin[nb] = best_b; }
+  if (va) { idx[na] = arg_a; if (dmin) dmin[na] = best_a + ((qa[0] + qa[1]) + (qa[2] + qa[3])); }
+  if (vb) { idx[nb] = arg_b; if (dmin) dmin[nb] = best_b + ((qb[0] + qb[1]) + (qb[2] + qb[3])); }
+}
+
+static int env_int(const char* name, int dflt, int lo, int hi) {
+  const char* e = getenv(name);
+  const int v = e ? atoi(e) : dflt;
+  return v >= lo && v <= hi ? v : dflt;
+}
+
+static int64_t persistent_waves(int64_t tiles) {
+  static const int wpc = env_int("VQHMM_VQ_WPC", 8, 1, 32);  // tuning knob: resident waves per CU
+  return std::min<int64_t>(tiles, 256 * (int64_t)wpc);
+}
+
+template <int S>
+static void launch_mfma(const float* z, int64_t B, int Dv, int T, const float* cb, int K, int32_t* idx, float* dmin,
+                        hipStream_t s) {
+  const int64_t tiles = cdiv(B * (int64_t)T, 32);
+  vq_mfma_kernel<S><<<(unsigned)cdiv(persistent_waves(tiles), 4), 256, 0, s>>>(z, B, Dv, T, cb, K, idx, dmin, tiles);
+}
+
+template <int DG, int CB>
+static void launch_rows(const float* z, int64_t B, int Dv, int T, const float* cb, int K, int32_t* idx, float* dmin,
+                        hipStream_t s) {
+  const int64_t tiles = cdiv(B * (int64_t)T, 64);
+  vq_rows_kernel<DG, CB>
+      <<<(unsigned)cdiv(persistent_waves(tiles), 4), 256, 0, s>>>(z, B, Dv, T, cb, K, idx, dmin, tiles);
+}
+
+template <int CB>
+static void dispatch_rows(const float* z, int64_t B, int Dv, int T, const float* cb, int K, int32_t* idx,
+                          float* dmin, hipStream_t s) {
+  if (Dv <= 8) launch_rows<2, CB>(z, B, Dv, T, cb, K, idx, dmin, s);
+  else if (Dv <= 16) launch_rows<4, CB>(z, B, Dv, T, cb, K, idx, dmin, s);
+  else if (Dv <= 32) launch_rows<8, CB>(z, B, Dv, T, cb, K, idx, dmin, s);
+  else launch_rows<16, CB>(z, B, Dv, T, cb, K, idx, dmin, s);
 }
 
 int launch_vq_argmin(const float* z, int64_t B, int64_t Dv, int64_t T, const float* cb, int64_t K,
@@ -106,6 +341,24 @@ int launch_vq_argmin(const float* z, int64_t B, int64_t Dv, int64_t T, const flo
   const int64_t N = B * T;
   if (N == 0) return VQHMM_OK;
   if (K <= 0 || Dv <= 0 || Dv > 2048 || T <= 0 || T > INT32_MAX) return VQHMM_EINVAL;
+  static const int impl = env_int("VQHMM_VQ_IMPL", 0, 0, 2);  // 0 auto, 1 tile-32, 2 rows
+  const bool rows_ok = T % 4 == 0 && (reinterpret_cast<uintptr_t>(z) & 15) == 0 && N * Dv < (int64_t(1) << 30);
+  if (K <= 32 && Dv <= 64 && rows_ok && impl != 1) {
+    if (K <= 16) dispatch_rows<1>(z, B, (int)Dv, (int)T, cb, (int)K, idx, dmin, s);
+    else dispatch_rows<2>(z, B, (int)Dv, (int)T, cb, (int)K, idx, dmin, s);
+    VQHMM_LAUNCH_CHECK();
+    return VQHMM_OK;
+  }
+  if (K <= 32 && Dv <= 64) {
+    const int S = (int)cdiv(Dv, 2);
+    if (S <= 2) launch_mfma<2>(z, B, (int)Dv, (int)T, cb, (int)K, idx, dmin, s);
+    else if (S <= 4) launch_mfma<4>(z, B, (int)Dv, (int)T, cb, (int)K, idx, dmin, s);
+    else if (S <= 8) launch_mfma<8>(z, B, (int)Dv, (int)T, cb, (int)K, idx, dmin, s);
+    else if (S <= 16) launch_mfma<16>(z, B, (int)Dv, (int)T, cb, (int)K, idx, dmin, s);
+    else launch_mfma<32>(z, B, (int)Dv, (int)T, cb, (int)K, idx, dmin, s);
+    VQHMM_LAUNCH_CHECK();
+    return VQHMM_OK;
+  }
   const int ldc = (int)cdiv(Dv, VQ_DCH) * VQ_DCH;
   const dim3 grid((unsigned)cdiv(N, 512));
   int kb = K <= 4 ? 4 : K <= 8 ? 8 : K <= 16 ? 16 : 32;
