@@ -11,7 +11,7 @@ for p in (ROOT, PKG_DIR):
     if p not in sys.path:
         sys.path.insert(0, p)
 
-GOLDEN_CASES = ("cfg1_seeded", "cfg1_trained", "cfg2_slice_seeded", "cfg2_slice_trained",
+GOLDEN_CASES = ("cfg1_seeded", "cfg1_trained", "cfg2_slice_seeded", "cfg2_slice_trained", "k32_wide",
                 "k8_d16", "smoke_tiny")
 
 

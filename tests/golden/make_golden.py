@@ -156,6 +156,8 @@ def main():
               weights=os.path.join(REF, "models/vae_hmm.pt"))
     make_case("k8_d16", (16, 64, 8, 32, 4, 128), 8, 64, [64, 64, 20, 40, 63, 1, 64, 33], seed=77)
     make_case("smoke_tiny", (5, 8, 3, 4, 2, 8), 2, 16, [16, 9], seed=5)
+    # large codebook (K=32, K^2 = 1024 transition logits) with channel counts past 64
+    make_case("k32_wide", (64, 80, 32, 72, 4, 16), 4, 24, [24, 24, 13, 7], seed=32, train_lines=False)
     make_collate_case()
 
 

@@ -56,9 +56,13 @@ struct ElboPlan {
   double* part;
   float *sW1, *sb1, *sW2, *sb2, *sq0;
   float *loss, *pieces;
+  // staged head (shapes the fused heads do not cover): Prior MLP as 1x1 convs
+  bool staged;
+  float *hid, *lgA, *dhid, *nx, *dqc, *trw, *logpi;
   // backward
   float *dg2, *dg1, *dqd, *dlog, *dh2, *dh1, *dWc, *q0sum;
-  WLayer wl[6];  // 0 to_params, 1 dec2, 2 dec1', 3 to_logits, 4 enc2, 5 enc1
+  int nwl;
+  WLayer wl[8];  // 0 to_params, 1 dec2, 2 dec1', 3 to_logits, 4 enc2, 5 enc1, [6 Prior W1, 7 Prior W2]
   size_t bytes;
 };
 
@@ -84,11 +88,27 @@ ElboPlan plan_elbo(const vqhmm_dims_t* d, int64_t B, int64_t T, void* ws) {
   p.dqx = c.take<float>(R * ld4(K));
   p.dlx = c.take<float>(R * ld4(K));
   p.part = c.take<double>((size_t)p.hgrid * 4);
-  p.sW1 = c.take<float>((size_t)p.hgrid * p.TH * p.U);
-  p.sb1 = c.take<float>((size_t)p.hgrid * p.TH);
-  p.sW2 = c.take<float>((size_t)p.hgrid * K * K * p.TH);
-  p.sb2 = c.take<float>((size_t)p.hgrid * K * K);
-  p.sq0 = c.take<float>((size_t)p.hgrid * K);
+  {
+    HeadArgs hc{};
+    hc.K = K; hc.U = p.U; hc.TH = p.TH; hc.D = D;
+    p.staged = !fused_head_supported(hc);
+  }
+  if (!p.staged) {
+    p.sW1 = c.take<float>((size_t)p.hgrid * p.TH * p.U);
+    p.sb1 = c.take<float>((size_t)p.hgrid * p.TH);
+    p.sW2 = c.take<float>((size_t)p.hgrid * K * K * p.TH);
+    p.sb2 = c.take<float>((size_t)p.hgrid * K * K);
+    p.sq0 = c.take<float>((size_t)p.hgrid * K);
+  } else {
+    p.sq0 = c.take<float>(K);  // one chunk: q summed over the t = 0 rows
+    p.hid = c.take<float>(R * ld4(p.TH));
+    p.lgA = c.take<float>(R * ld4(K * K));
+    p.dhid = c.take<float>(R * ld4(p.TH));
+    p.nx = c.take<float>(R * ld4(K));
+    p.dqc = c.take<float>(R * ld4(K));
+    p.trw = c.take<float>(R);
+    p.logpi = c.take<float>(K);
+  }
   p.loss = c.take<float>(1);
   p.pieces = c.take<float>(4);
   p.dg2 = c.take<float>(R * ld4(H));
@@ -99,8 +119,10 @@ ElboPlan plan_elbo(const vqhmm_dims_t* d, int64_t B, int64_t T, void* ws) {
   p.dh1 = c.take<float>(R * ld4(H));
   p.dWc = c.take<float>((size_t)H * K * 3);
   p.q0sum = c.take<float>(K);
-  const int shapes[6][3] = {{2 * D, H, 1}, {H, H, 3}, {H, K, 3}, {K, H2, 1}, {H2, H, 3}, {H, D, 3}};
-  for (int i = 0; i < 6; ++i) {
+  const int shapes[8][3] = {{2 * D, H, 1}, {H, H, 3}, {H, K, 3}, {K, H2, 1}, {H2, H, 3}, {H, D, 3},
+                            {p.TH, p.U, 1}, {K * K, p.TH, 1}};
+  p.nwl = p.staged ? 8 : 6;
+  for (int i = 0; i < p.nwl; ++i) {
     WLayer& w = p.wl[i];
     w.N = shapes[i][0]; w.C = shapes[i][1]; w.ks = shapes[i][2];
     const int64_t tiles = cdiv(w.N, 64) * cdiv(w.C, 64);
@@ -261,6 +283,41 @@ ConvArgs conv_of(const ElboPlan& p, const float* const* wp, int st) {
   return a;
 }
 
+// Staged head: Prior MLP as 1x1 convs over PCL rows, L1/L2 row kernels, then the
+// MLP backward as a dgrad conv + two wgrads (head_staged.hip).
+int run_staged_head(const ElboPlan& p, const StepCtx& c, const float* const* w, hipStream_t s) {
+  int rc;
+  ConvArgs a = conv_base(p);
+  a.src = p.up; a.Kc = p.U; a.ks = 1; a.W = w[TN0_W]; a.bias = w[TN0_B]; a.N = p.TH; a.act = 1; a.out = p.hid;
+  if ((rc = launch_conv(a, s))) return rc;
+  a = conv_base(p);
+  a.src = p.hid; a.Kc = p.TH; a.ks = 1; a.W = w[TN2_W]; a.bias = w[TN2_B]; a.N = p.K * p.K; a.act = 0;
+  a.out = p.lgA;
+  if ((rc = launch_conv(a, s))) return rc;
+  StagedHeadArgs h{};
+  h.B = p.B; h.T = p.T; h.R = p.R; h.D = p.D; h.K = p.K;
+  h.x = p.xp; h.par = p.par; h.logits = p.logits; h.q = p.q; h.lengths = c.lengths;
+  h.log_prior = w[LOG_PRIOR]; h.log_pi = p.logpi; h.lgA = p.lgA; h.nx = p.nx; h.dqc = p.dqc; h.trw = p.trw;
+  h.cpri = -c.beta / (float)p.B; h.cent = c.beta / (float)p.B; h.need_grad = c.need_grad;
+  h.dpar = p.dpar; h.dlx = p.dlx; h.dqx = p.dqx; h.part = p.part; h.q0 = p.sq0;
+  if ((rc = launch_staged_head(h, p.hgrid, s))) return rc;
+  if (!c.need_grad) return VQHMM_OK;
+  a = conv_base(p);
+  a.src = p.lgA; a.Kc = p.K * p.K; a.ks = 1; a.W = w[TN2_W]; a.w_dgrad = 1; a.N = p.TH; a.act = 2; a.aux = p.hid;
+  a.out = p.dhid;
+  if ((rc = launch_conv(a, s))) return rc;
+  const float* dys[2] = {p.dhid, p.lgA};
+  const float* xs[2] = {p.up, p.hid};
+  for (int i = 0; i < 2; ++i) {
+    const WLayer& L = p.wl[6 + i];
+    WgradArgs wa{};
+    wa.dy = dys[i]; wa.x = xs[i]; wa.x_cf = 0; wa.R = p.R; wa.T = p.T;
+    wa.N = L.N; wa.C = L.C; wa.ks = L.ks; wa.rows_per_chunk = L.rows; wa.slab = L.slab; wa.bias_slab = L.bslab;
+    if ((rc = launch_wgrad(wa, s))) return rc;
+  }
+  return VQHMM_OK;
+}
+
 int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
   const float* const* w = c.w;
   switch (st) {
@@ -279,6 +336,7 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       return launch_conv(a, s);
     }
     case S_HEAD: {
+      if (p.staged) return run_staged_head(p, c, w, s);
       HeadArgs h{};
       h.B = p.B; h.T = p.T; h.R = p.R; h.D = p.D; h.K = p.K; h.U = p.U; h.TH = p.TH;
       h.x = p.xp; h.u = p.up;
@@ -328,11 +386,19 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       seg(wl[4].bslab, wl[4].nchunks, wl[4].N, g + off[ENC2_B], nullptr);
       seg(wl[5].slab, wl[5].nchunks, (int64_t)wl[5].N * wl[5].C * 3, g + off[ENC1_W], nullptr);
       seg(wl[5].bslab, wl[5].nchunks, wl[5].N, g + off[ENC1_B], nullptr);
-      seg(p.sW1, p.hgrid, (int64_t)p.TH * p.U, g + off[TN0_W], gs);
-      seg(p.sb1, p.hgrid, p.TH, g + off[TN0_B], gs);
-      seg(p.sW2, p.hgrid, (int64_t)p.K * p.K * p.TH, g + off[TN2_W], gs);
-      seg(p.sb2, p.hgrid, (int64_t)p.K * p.K, g + off[TN2_B], gs);
-      seg(p.sq0, p.hgrid, p.K, p.q0sum, nullptr);
+      if (p.staged) {
+        seg(wl[6].slab, wl[6].nchunks, (int64_t)p.TH * p.U, g + off[TN0_W], gs);
+        seg(wl[6].bslab, wl[6].nchunks, p.TH, g + off[TN0_B], gs);
+        seg(wl[7].slab, wl[7].nchunks, (int64_t)p.K * p.K * p.TH, g + off[TN2_W], gs);
+        seg(wl[7].bslab, wl[7].nchunks, (int64_t)p.K * p.K, g + off[TN2_B], gs);
+        seg(p.sq0, 1, p.K, p.q0sum, nullptr);
+      } else {
+        seg(p.sW1, p.hgrid, (int64_t)p.TH * p.U, g + off[TN0_W], gs);
+        seg(p.sb1, p.hgrid, p.TH, g + off[TN0_B], gs);
+        seg(p.sW2, p.hgrid, (int64_t)p.K * p.K * p.TH, g + off[TN2_W], gs);
+        seg(p.sb2, p.hgrid, (int64_t)p.K * p.K, g + off[TN2_B], gs);
+        seg(p.sq0, p.hgrid, p.K, p.q0sum, nullptr);
+      }
       return launch_reduce_slabs(segs, n, s);
     }
     case S_COMPOSE_BWD: {
@@ -370,8 +436,12 @@ void stage_work(const ElboPlan& p, int st, double* flops, double* bytes, int* mf
     *mfma = 1;
   } else if (st == S_HEAD) {
     const double KK = (double)p.K * p.K;
-    *flops = N * (2.0 * p.TH * p.U + 2.0 * p.TH * KK + 6.0 * p.TH * KK + 4.0 * p.TH * p.U + 20.0 * p.D + 12.0 * KK);
+    // Prior MLP fwd (2 TH U + 2 TH K^2) + bwd (dh 2 TH K^2, dW2 2 TH K^2, dW1 2 TH U) + elementwise
+    *flops = N * (4.0 * p.TH * p.U + 6.0 * p.TH * KK + 20.0 * p.D + 12.0 * KK);
     *bytes = 4.0 * R * (2 * p.D + p.D + p.U + 2 * p.K + 2 * p.D + 2 * p.K);
+    HeadArgs h{};
+    h.K = p.K; h.U = p.U; h.TH = p.TH; h.D = p.D;
+    *mfma = head_mfma_supported(h) ? 1 : 0;
   } else if (st == S_TOPCL) {
     *bytes = 4.0 * (N * (p.D + p.U) + R * (ld4(p.D) + ld4(p.U)));
   } else if (st == S_LOGIT_BWD) {

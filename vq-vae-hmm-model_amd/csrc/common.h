@@ -46,6 +46,31 @@ __device__ __forceinline__ bool row_bt(int64_t r, int64_t R, int T, int64_t& b, 
   return t >= 0 && t < T;
 }
 
+// Lane exchange x[lane ^ 16] / x[lane ^ 32] on the VALU (gfx950 v_permlane16/32_swap:
+// vdst's odd 16-lane rows (upper half) trade places with src's even rows (lower
+// half); with vdst = src = x the partner's value lands in r[0] for lanes with
+// the bit set and in r[1] otherwise).  No LDS round trip, unlike ds_bpermute.
+template <typename V>
+__device__ __forceinline__ V xor16(V x) {
+  const unsigned u = __builtin_bit_cast(unsigned, x);
+  const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  return __builtin_bit_cast(V, (threadIdx.x & 16) ? r[0] : r[1]);
+}
+template <typename V>
+__device__ __forceinline__ V xor32(V x) {
+  const unsigned u = __builtin_bit_cast(unsigned, x);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return __builtin_bit_cast(V, (threadIdx.x & 32) ? r[0] : r[1]);
+}
+
+// Workgroup barrier that orders LDS only: global loads in flight stay in flight
+// (__syncthreads() would drain vmcnt first).
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);

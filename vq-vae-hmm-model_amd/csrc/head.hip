@@ -11,6 +11,8 @@
 //
 // Tile = 255 rows of the PCL layout per 256-thread block (thread 255 builds the
 // halo row r0+255, whose log_A the transition t -> t+1 of the last row needs).
+#include <algorithm>
+
 #include "kernels.h"
 
 namespace vqhmm {
@@ -376,6 +378,10 @@ int head_grid(int64_t R) {
   return (int)(ntiles < 512 ? ntiles : 512);
 }
 
+bool fused_head_supported(const HeadArgs& a) {
+  return head_mfma_supported(a) || (a.K <= 8 && a.U <= 8 && a.TH <= 256 && a.D <= 16);
+}
+
 int launch_head(const HeadArgs& a0, int grid, hipStream_t s) {
   HeadArgs a = a0;
   a.ntiles = cdiv(a.R, HP);
@@ -412,15 +418,56 @@ __global__ __launch_bounds__(256) void prior_fwd_kernel(PriorArgs p) {
     if (ij < KK) p.log_A[n * KK + ij] = la[ij];
 }
 
+// Any K <= 64, TH <= 1024: one wave per position; hidden layer and the K*K
+// logits staged in LDS, then lane i log_softmaxes row i of log_A.
+__global__ __launch_bounds__(256) void prior_fwd_wave_kernel(PriorArgs p) {
+  __shared__ float hS[4][1024];
+  __shared__ float zS[4][64 * 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int K = p.K, KK = K * K;
+  for (int64_t n = (int64_t)blockIdx.x * 4 + wave; n < p.B * p.T; n += (int64_t)gridDim.x * 4) {
+    const int64_t b = n / p.T;
+    const int t = (int)(n - b * p.T);
+    const float* u = p.u + b * (int64_t)p.U * p.T + (int64_t)t * p.u_st;
+    for (int h = lane; h < p.TH; h += 64) {
+      float v = p.b1[h];
+      for (int c = 0; c < p.U; ++c) v = fmaf(p.W1[(int64_t)h * p.U + c], u[(int64_t)c * p.u_sc], v);
+      hS[wave][h] = fmaxf(v, 0.f);
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (int ij = lane; ij < KK; ij += 64) {
+      float z = p.b2[ij];
+      const float* w2 = p.W2 + (int64_t)ij * p.TH;
+      for (int h = 0; h < p.TH; ++h) z = fmaf(w2[h], hS[wave][h], z);
+      zS[wave][ij] = z;
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (lane < K) {
+      const float* zr = &zS[wave][lane * K];
+      float m = -__builtin_inff();
+      for (int j = 0; j < K; ++j) m = fmaxf(m, zr[j]);
+      float s = 0.f;
+      for (int j = 0; j < K; ++j) s += __expf(zr[j] - m);
+      const float ls = m + __logf(s);
+      for (int j = 0; j < K; ++j) p.log_A[n * KK + lane * K + j] = zr[j] - ls;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 int launch_prior_fwd(const PriorArgs& p, hipStream_t s) {
   const int64_t N = p.B * p.T;
   if (N == 0) return VQHMM_OK;
-  if (p.K > 8 || p.U > 8) return VQHMM_EUNSUPPORTED;
-  const dim3 grid((unsigned)cdiv(N, 256));
-  if (p.K <= 4)
-    prior_fwd_kernel<4, 8><<<grid, 256, 0, s>>>(p);
-  else
-    prior_fwd_kernel<8, 8><<<grid, 256, 0, s>>>(p);
+  if (p.K <= 8 && p.U <= 8) {
+    const dim3 grid((unsigned)cdiv(N, 256));
+    if (p.K <= 4)
+      prior_fwd_kernel<4, 8><<<grid, 256, 0, s>>>(p);
+    else
+      prior_fwd_kernel<8, 8><<<grid, 256, 0, s>>>(p);
+  } else {
+    if (p.K > 64 || p.TH > 1024) return VQHMM_EUNSUPPORTED;
+    prior_fwd_wave_kernel<<<(unsigned)std::min<int64_t>(cdiv(N, 4), 4096), 256, 0, s>>>(p);
+  }
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
 }

@@ -17,6 +17,8 @@
 //            contractions over rows.
 // Weight-gradient accumulators stay in registers across all tiles of the
 // workgroup; the 4 waves are summed in fixed order at the end (deterministic).
+#include <type_traits>
+
 #include "kernels.h"
 
 namespace vqhmm {
@@ -36,8 +38,8 @@ struct HeadLds {
   float dlgS[MP * 16];
   float qS[(MP + 2) * 4];
   int wS[MP + 2];
-  float hT[4][16 * 16];   // per-wave 16-row x 16-h transposes (row stride 16 = conflict-free column reads)
-  float dT[4][16 * 16];
+  float hT[4][2][16 * 16];  // per-wave, per-block-of-the-pair 16-row x 16-h transposes
+  float dT[4][2][16 * 16];  //   (row stride 16 = conflict-free column reads)
   float lpS[4];
   unsigned long long cnt;
 };
@@ -136,18 +138,141 @@ __global__ __launch_bounds__(256, 2) void elbo_head_mfma_kernel(HeadArgs a) {
 #pragma unroll
   for (int i = 0; i < HB; ++i) gW1[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // This workgroup's rows: an equal share [rb, re) of all R rows, walked in
+  // tiles of up to MOWN owned rows + 1 halo row (equal shares keep every CU
+  // busy to the end; 16-row blocks past a short last tile are skipped).
+  const int64_t rb = a.R * (int64_t)blockIdx.x / gridDim.x;
+  const int64_t re = a.R * ((int64_t)blockIdx.x + 1) / gridDim.x;
+
+  // ---- phase A on NP (1 or 2) row blocks of this wave at once: lg^T -> lgS
+  auto phase_a = [&](auto np_tag, int blk0, int blk1) {
+    constexpr int NP = decltype(np_tag)::value;
+    const int p0[2] = {blk0 * 16, blk1 * 16};
+    float ub0[NP], ub1[NP];
+    f32x4 lg[NP];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      ub0[i] = sh.uS[(p0[i] + l16) * 8 + lg4];
+      ub1[i] = sh.uS[(p0[i] + l16) * 8 + 4 + lg4];
+      lg[i] = b2f;
+    }
+#pragma unroll
+    for (int hb = 0; hb < HB; ++hb) {
+      const float w1a = sh.W1S[(hb * 16 + l16) * 8 + lg4], w1b = sh.W1S[(hb * 16 + l16) * 8 + 4 + lg4];
+      const f32x4 w2v = *reinterpret_cast<const f32x4*>(&sh.W2S[l16 * S::LDW2 + hb * 16 + 4 * lg4]);
+      f32x4 h[NP];
+#pragma unroll
+      for (int i = 0; i < NP; ++i) h[i] = mfma16x16x4(w1a, ub0[i], f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+      for (int i = 0; i < NP; ++i) h[i] = mfma16x16x4(w1b, ub1[i], h[i]);
+#pragma unroll
+      for (int i = 0; i < NP; ++i)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) h[i][v] = fmaxf(h[i][v], 0.f);
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+#pragma unroll
+        for (int i = 0; i < NP; ++i) lg[i] = mfma16x16x4(w2v[v], h[i][v], lg[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < NP; ++i) *reinterpret_cast<f32x4*>(&sh.lgS[(p0[i] + l16) * 16 + 4 * lg4]) = lg[i];
+  };
+
+  // ---- phase C (MLP backward) on NP row blocks of this wave at once
+  auto phase_c = [&](auto np_tag, int blk0, int blk1) {
+    constexpr int NP = decltype(np_tag)::value;
+    const int p0[2] = {blk0 * 16, blk1 * 16};
+    float ub0[NP], ub1[NP], dla[NP][4], ua[NP][4];
+    f32x4 dlb[NP];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      ub0[i] = sh.uS[(p0[i] + l16) * 8 + lg4];
+      ub1[i] = sh.uS[(p0[i] + l16) * 8 + 4 + lg4];
+      dlb[i] = *reinterpret_cast<const f32x4*>(&sh.dlgS[(p0[i] + l16) * 16 + 4 * lg4]);
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const int pr = p0[i] + 4 * s4 + lg4;
+        dla[i][s4] = sh.dlgS[pr * 16 + l16];
+        const float uv = sh.uS[pr * 8 + (l16 & 7)];
+        ua[i][s4] = l16 < 8 ? uv : 0.f;
+      }
+    }
+    // db2: contraction of dlg^T with a ones column
+#pragma unroll
+    for (int i = 0; i < NP; ++i)
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) gW2[HB] = mfma16x16x4(dla[i][s4], l16 == 0 ? 1.f : 0.f, gW2[HB]);
+#pragma unroll
+    for (int hb = 0; hb < HB; ++hb) {
+      const float w1a = sh.W1S[(hb * 16 + l16) * 8 + lg4], w1b = sh.W1S[(hb * 16 + l16) * 8 + 4 + lg4];
+      float w2c[4];
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) w2c[s4] = sh.W2S[(4 * lg4 + s4) * S::LDW2 + hb * 16 + l16];
+      f32x4 h[NP], dh[NP];
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        h[i] = mfma16x16x4(w1a, ub0[i], f32x4{0.f, 0.f, 0.f, 0.f});
+        dh[i] = mfma16x16x4(w2c[0], dlb[i][0], f32x4{0.f, 0.f, 0.f, 0.f});
+      }
+#pragma unroll
+      for (int i = 0; i < NP; ++i) h[i] = mfma16x16x4(w1b, ub1[i], h[i]);
+      // dhid^T block: A[i = h][k = ij = 4*lg4 + s] = W2[ij][h], B[k][j = p] = dlg[p][ij]
+#pragma unroll
+      for (int s4 = 1; s4 < 4; ++s4)
+#pragma unroll
+        for (int i = 0; i < NP; ++i) dh[i] = mfma16x16x4(w2c[s4], dlb[i][s4], dh[i]);
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        f32x4 hr, dm;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          hr[v] = fmaxf(h[i][v], 0.f);
+          dm[v] = h[i][v] > 0.f ? dh[i][v] : 0.f;
+        }
+        // transpose through LDS: [p][h_local]
+        *reinterpret_cast<f32x4*>(&sh.hT[wave][i][l16 * 16 + 4 * lg4]) = hr;
+        *reinterpret_cast<f32x4*>(&sh.dT[wave][i][l16 * 16 + 4 * lg4]) = dm;
+      }
+      // contractions over the rows (k = p = 4*s + lg4) of both blocks
+#pragma unroll
+      for (int i = 0; i < NP; ++i)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          const int pr = 4 * s4 + lg4;
+          gW2[hb] = mfma16x16x4(dla[i][s4], sh.hT[wave][i][pr * 16 + l16], gW2[hb]);
+          gW1[hb] = mfma16x16x4(sh.dT[wave][i][pr * 16 + l16], ua[i][s4], gW1[hb]);
+        }
+    }
+  };
+  using One = std::integral_constant<int, 1>;
+  using Two = std::integral_constant<int, 2>;
+  // blocks of this wave in a tile: wave, wave + 4, wave + 8, wave + 12 (interleaved so a
+  // short tile still spreads over the 4 waves), processed in pairs
+  auto for_blocks = [&](int nblk, auto&& fn) {
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      const int b0 = wave + 8 * pr, b1 = b0 + 4;
+      if (b1 < nblk) fn(Two{}, b0, b1);
+      else if (b0 < nblk) fn(One{}, b0, b0);
+    }
+  };
+  auto for_blocks1 = [&](int nblk, auto&& fn) {
+    for (int b0 = wave; b0 < nblk; b0 += 4) fn(One{}, b0, b0);
+  };
+
   RowIn<K, DM> cur, nxt;
-  load_row<K, DM>(a, (int64_t)blockIdx.x * MOWN + tid, cur);
+  load_row<K, DM>(a, rb + tid, cur);
   nxt = cur;
-  for (int64_t tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
-    const int64_t r0 = tile * MOWN;
+  for (int64_t r0 = rb; r0 < re; r0 += MOWN) {
+    const int nown = (int)min<int64_t>(MOWN, re - r0);  // owned rows; row nown is the halo
+    const int nblk = (nown + 16) / 16;                   // 16-row blocks holding rows 0..nown
     __syncthreads();
     // ---------------- L: stage this tile's rows (prefetched in registers)
     {
       const int64_t r = r0 + tid;
       int64_t b;
       int t;
-      const bool valid = row_bt(r, a.R, a.T, b, t);
+      const bool valid = tid <= nown && row_bt(r, a.R, a.T, b, t);
       sh.wS[tid + 1] = (valid && t >= 1 && t < cur.L) ? 1 : 0;
 #pragma unroll
       for (int c = 0; c < 8; ++c) sh.uS[tid * 8 + c] = (valid && c < U) ? cur.u[c] : (c == U ? 1.f : 0.f);
@@ -165,24 +290,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_mfma_kernel(HeadArgs a) {
     }
     __syncthreads();
     // ---------------- A: MLP forward (MFMA), lg^T -> lgS[p][ij]
-    for (int pbi = 0; pbi < 4; ++pbi) {
-      const int p0 = (wave * 4 + pbi) * 16;
-      const float ub0 = sh.uS[(p0 + l16) * 8 + lg4];
-      const float ub1 = sh.uS[(p0 + l16) * 8 + 4 + lg4];
-      f32x4 lg = b2f;
-#pragma unroll
-      for (int hb = 0; hb < HB; ++hb) {
-        f32x4 h = f32x4{0.f, 0.f, 0.f, 0.f};
-        h = mfma16x16x4(sh.W1S[(hb * 16 + l16) * 8 + lg4], ub0, h);
-        h = mfma16x16x4(sh.W1S[(hb * 16 + l16) * 8 + 4 + lg4], ub1, h);
-#pragma unroll
-        for (int v = 0; v < 4; ++v) h[v] = fmaxf(h[v], 0.f);
-        const f32x4 w2v = *reinterpret_cast<const f32x4*>(&sh.W2S[l16 * S::LDW2 + hb * 16 + 4 * lg4]);
-#pragma unroll
-        for (int v = 0; v < 4; ++v) lg = mfma16x16x4(w2v[v], h[v], lg);
-      }
-      *reinterpret_cast<f32x4*>(&sh.lgS[(p0 + l16) * 16 + 4 * lg4]) = lg;
-    }
+    for_blocks(nblk, phase_a);
     __syncthreads();
     // ---------------- B1: log_softmax rows -> log_A (in place); recon, entropy, init
     {
@@ -204,7 +312,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_mfma_kernel(HeadArgs a) {
 #pragma unroll
         for (int j = 0; j < K; ++j) la[i * K + j] -= ls;
       }
-      if (p < MOWN && r < a.R) {
+      if (p < nown) {
         const bool m = valid && t < cur.L;
 #pragma unroll
         for (int c = 0; c < DM; ++c) {
@@ -266,7 +374,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_mfma_kernel(HeadArgs a) {
       const int p = tid;
       const int64_t r = r0 + p;
       float* dl = &sh.dlgS[p * 16];
-      if (p < MOWN && r < a.R) {
+      if (p < nown) {
         const float* qp = &sh.qS[p * 4];
         const float* qc = &sh.qS[(p + 1) * 4];
         const float* qn = &sh.qS[(p + 2) * 4];
@@ -317,59 +425,11 @@ __global__ __launch_bounds__(256, 2) void elbo_head_mfma_kernel(HeadArgs a) {
         for (int ij = 0; ij < 16; ++ij) dl[ij] = 0.f;
       }
     }
-    {
-      const int64_t nt = tile + gridDim.x;
-      if (nt < a.ntiles) load_row<K, DM>(a, nt * MOWN + tid, nxt);
-    }
+    if (r0 + MOWN < re) load_row<K, DM>(a, r0 + MOWN + tid, nxt);
     if (a.need_grad) {
       __syncthreads();
       // ---------------- C: MLP backward (MFMA)
-      float* hT = sh.hT[wave];
-      float* dT = sh.dT[wave];
-      for (int pbi = 0; pbi < 4; ++pbi) {
-        const int p0 = (wave * 4 + pbi) * 16;
-        const float ub0 = sh.uS[(p0 + l16) * 8 + lg4];
-        const float ub1 = sh.uS[(p0 + l16) * 8 + 4 + lg4];
-        const f32x4 dlb = *reinterpret_cast<const f32x4*>(&sh.dlgS[(p0 + l16) * 16 + 4 * lg4]);
-        float dla[4], ua[4];
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) {
-          const int pr = p0 + 4 * s4 + lg4;
-          dla[s4] = sh.dlgS[pr * 16 + l16];
-          const float uv = sh.uS[pr * 8 + (l16 & 7)];
-          ua[s4] = l16 < 8 ? uv : 0.f;
-        }
-        // db2: contraction of dlg^T with a ones column
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) gW2[HB] = mfma16x16x4(dla[s4], l16 == 0 ? 1.f : 0.f, gW2[HB]);
-#pragma unroll
-        for (int hb = 0; hb < HB; ++hb) {
-          f32x4 h = f32x4{0.f, 0.f, 0.f, 0.f};
-          h = mfma16x16x4(sh.W1S[(hb * 16 + l16) * 8 + lg4], ub0, h);
-          h = mfma16x16x4(sh.W1S[(hb * 16 + l16) * 8 + 4 + lg4], ub1, h);
-          // dhid^T block: A[i = h][k = ij = 4*lg4 + s] = W2[ij][h], B[k][j = p] = dlg[p][ij]
-          f32x4 dh = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int s4 = 0; s4 < 4; ++s4)
-            dh = mfma16x16x4(sh.W2S[(4 * lg4 + s4) * S::LDW2 + hb * 16 + l16], dlb[s4], dh);
-          f32x4 hr, dm;
-#pragma unroll
-          for (int v = 0; v < 4; ++v) {
-            hr[v] = fmaxf(h[v], 0.f);
-            dm[v] = h[v] > 0.f ? dh[v] : 0.f;
-          }
-          // transpose through LDS: [p][h_local]
-          *reinterpret_cast<f32x4*>(&hT[l16 * 16 + 4 * lg4]) = hr;
-          *reinterpret_cast<f32x4*>(&dT[l16 * 16 + 4 * lg4]) = dm;
-          // contractions over the 16 rows (k = p = 4*s + lg4)
-#pragma unroll
-          for (int s4 = 0; s4 < 4; ++s4) {
-            const int pr = 4 * s4 + lg4;
-            gW2[hb] = mfma16x16x4(dla[s4], hT[pr * 16 + l16], gW2[hb]);
-            gW1[hb] = mfma16x16x4(dT[pr * 16 + l16], ua[s4], gW1[hb]);
-          }
-        }
-      }
+      for_blocks1(nblk, phase_c);
     }
     cur = nxt;
   }

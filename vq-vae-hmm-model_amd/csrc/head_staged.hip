@@ -1,0 +1,220 @@
+// ELBO head for shapes the fused heads do not cover (large K: K^2 transition
+// logits per position; wide U / TH / D).  Same math as head_mfma.hip
+// (VQ_VAE_HMM_fixed.py:59-71 Prior, :106-137 loss), split into stages because
+// log_A (B,T,K,K) no longer fits in registers:
+//   1. hid  = relu(W1 u + b1)        1x1 conv over PCL rows (conv kernels)
+//   2. lgA  = W2 hid + b2            1x1 conv, K^2 channels
+//   3. L1   (this file) one wave per row, lane i = row i of log_A_t:
+//           log_softmax, transition term w_t sum q_{t-1,i} q_{t,j} log_A_t[i][j],
+//           nx_t[i] = sum_j log_A_t[i][j] q_{t,j}   (the t -> t+1 term of dq_{t-1}),
+//           dqc_t[j] = sum_i q_{t-1,i} log_A_t[i][j] (the t-1 -> t term of dq_t),
+//           d lgA (log_softmax backward) written in place over lgA
+//   4. L2   (this file) one thread per row: recon NLL, entropy, init, dq, loss
+//           partials (fixed-order block sums, deterministic)
+//   5. dhid = (W2^T dlgA) * relu'(hid); dW2, db2, dW1, db1 by the wgrad kernels.
+#include <algorithm>
+
+#include "kernels.h"
+
+namespace vqhmm {
+
+template <int KM>
+__global__ __launch_bounds__(256) void head_l1_kernel(StagedHeadArgs a) {
+  __shared__ float qcS[4][KM];
+  __shared__ float qpS[4][KM];
+  __shared__ float laS[4][KM][KM + 1];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int K = a.K, KK = K * K, LDA = ld4(KK), LQ = ld4(K);
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + wave; r < a.R; r += nw) {
+    int64_t b;
+    int t;
+    const bool valid = row_bt(r, a.R, a.T, b, t);
+    float* row = a.lgA + r * LDA;
+    if (!valid) {  // pad rows: zero gradient rows (the wgrad / dgrad sums run over all rows)
+      for (int e = lane; e < LDA; e += 64) row[e] = 0.f;
+      if (lane < LQ) { a.nx[r * LQ + lane] = 0.f; a.dqc[r * LQ + lane] = 0.f; }
+      if (lane == 0) a.trw[r] = 0.f;
+      continue;
+    }
+    const int64_t L = a.lengths[b];
+    const float w = (t >= 1 && t < L) ? 1.f : 0.f;
+    if (lane < KM) {
+      qcS[wave][lane] = lane < K ? a.q[r * LQ + lane] : 0.f;
+      qpS[wave][lane] = lane < K ? a.q[(r - 1) * LQ + lane] : 0.f;  // row r-1 is a zero pad row at t = 0
+    }
+    __builtin_amdgcn_wave_barrier();
+    float la[KM];
+    float tri = 0.f, nxi = 0.f, qp = 0.f, sq = 0.f;
+    if (lane < K) {
+      const float* src = row + lane * K;
+      float m = -__builtin_inff();
+#pragma unroll
+      for (int j = 0; j < KM; ++j) {
+        la[j] = j < K ? src[j] : -__builtin_inff();
+        m = fmaxf(m, la[j]);
+      }
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < KM; ++j) s += j < K ? __expf(la[j] - m) : 0.f;
+      const float ls = m + __logf(s);
+      qp = qpS[wave][lane];
+#pragma unroll
+      for (int j = 0; j < KM; ++j) {
+        if (j < K) {
+          la[j] -= ls;
+          const float qc = qcS[wave][j];
+          nxi = fmaf(la[j], qc, nxi);
+          sq += qc;
+          laS[wave][lane][j] = la[j];
+        }
+      }
+      tri = qp * nxi;
+    }
+    __builtin_amdgcn_wave_barrier();
+    const float tr = wave_sum(tri);
+    if (lane < K) a.nx[r * LQ + lane] = nxi;
+    else if (lane < LQ) a.nx[r * LQ + lane] = 0.f;
+    if (lane == 0) a.trw[r] = w * tr;
+    // dqc_j = sum_i q_{t-1,i} log_A[i][j]  (lane j, column of the LDS copy)
+    if (lane < LQ) {
+      float d = 0.f;
+      if (lane < K)
+        for (int i = 0; i < K; ++i) d = fmaf(qpS[wave][i], laS[wave][i][lane], d);
+      a.dqc[r * LQ + lane] = w * d;
+    }
+    // log_softmax backward of d tr / d log_A = cpri w q_{t-1,i} q_{t,j}
+    if (lane < K) {
+      const float ci = a.cpri * w * qp;
+      const float rs = ci * sq;
+      float* dst = row + lane * K;
+#pragma unroll
+      for (int j = 0; j < KM; ++j)
+        if (j < K) dst[j] = ci * qcS[wave][j] - __expf(la[j]) * rs;
+    }
+    if (lane < LDA - KK) row[KK + lane] = 0.f;
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+__global__ __launch_bounds__(256) void head_l2_kernel(StagedHeadArgs a) {
+  __shared__ double red[4][256];
+  __shared__ unsigned long long cnt;
+  const int tid = threadIdx.x;
+  const int K = a.K, D = a.D, LQ = ld4(K), LP = ld4(2 * D), LX = ld4(D);
+  if (tid == 0) cnt = 0;
+  __syncthreads();
+  {  // valid positions (the recon normaliser mask.sum() * C, VQ_VAE_HMM_fixed.py:120)
+    unsigned long long c = 0;
+    for (int64_t b = tid; b < a.B; b += 256) {
+      const int64_t L = a.lengths[b];
+      c += (unsigned long long)(L <= 0 ? 0 : (L < a.T ? L : a.T));
+    }
+    atomicAdd(&cnt, c);
+  }
+  __syncthreads();
+  const float inv_n = 1.0f / fmaxf((float)(cnt * (unsigned long long)D), 1.0f);
+  float s_rec = 0.f, s_init = 0.f, s_tr = 0.f, s_ent = 0.f;
+  for (int64_t r = (int64_t)blockIdx.x * 256 + tid; r < a.R; r += (int64_t)gridDim.x * 256) {
+    int64_t b;
+    int t;
+    const bool valid = row_bt(r, a.R, a.T, b, t);
+    const int64_t L = valid ? a.lengths[b] : 0;
+    const bool m = valid && t < L;
+    if (a.need_grad) {
+      for (int c = 0; c < LP; ++c) a.dpar[r * LP + c] = 0.f;
+    }
+    for (int c = 0; c < D; ++c) {
+      if (!m) break;
+      const float mu = a.par[r * LP + c], lv = a.par[r * LP + D + c], xv = a.x[r * LX + c];
+      const float ev = __expf(lv);
+      const float var = fmaxf(ev, 1e-8f);
+      const float df = mu - xv;
+      const float r2 = df * df / var;
+      s_rec += 0.5f * (__logf(6.2831855f * var) + r2);
+      if (a.need_grad) {
+        a.dpar[r * LP + c] = df / var * inv_n;
+        a.dpar[r * LP + D + c] = (ev >= 1e-8f) ? 0.5f * (1.f - r2) * inv_n : 0.f;
+      }
+    }
+    // entropy of q = softmax(logits) and its logits gradient
+    float mx = -__builtin_inff();
+    for (int k = 0; k < K; ++k) mx = fmaxf(mx, a.logits[r * LQ + k]);
+    float se = 0.f;
+    for (int k = 0; k < K; ++k) se += __expf(a.logits[r * LQ + k] - mx);
+    const float lse = mx + __logf(se);
+    float f = 0.f;
+    for (int k = 0; k < K; ++k) f = fmaf(a.q[r * LQ + k], a.logits[r * LQ + k] - lse, f);
+    if (m) s_ent -= f;
+    if (valid) s_tr += a.trw[r];
+    const float wn = (valid && t + 1 < L) ? 1.f : 0.f;  // weight of the t -> t+1 transition
+    for (int k = 0; k < LQ; ++k) {
+      float dl = 0.f, dq = 0.f;
+      if (valid && k < K) {
+        const float qk = a.q[r * LQ + k];
+        if (m) dl = a.cent * qk * ((a.logits[r * LQ + k] - lse) - f);
+        dq = a.cpri * (a.dqc[r * LQ + k] + wn * a.nx[(r + 1) * LQ + k]);  // dqc already carries w_t
+        if (t == 0) {
+          dq = fmaf(a.cpri, a.log_pi[k], dq);
+          s_init = fmaf(qk, a.log_pi[k], s_init);
+        }
+      }
+      if (a.need_grad) {
+        a.dlx[r * LQ + k] = dl;
+        a.dqx[r * LQ + k] = dq;
+      }
+    }
+  }
+  red[0][tid] = s_rec;
+  red[1][tid] = s_init;
+  red[2][tid] = s_tr;
+  red[3][tid] = s_ent;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if (tid < st)
+      for (int i = 0; i < 4; ++i) red[i][tid] += red[i][tid + st];
+    __syncthreads();
+  }
+  if (tid < 4) a.part[blockIdx.x * 4 + tid] = red[tid][0];
+}
+
+// q summed over the t = 0 rows (init term gradient of log_prior), one chunk
+__global__ void head_q0_kernel(const float* q, int64_t B, int T, int K, float* q0) {
+  const int k = threadIdx.x;
+  if (k >= K) return;
+  float s = 0.f;
+  for (int64_t b = 0; b < B; ++b) s += q[(b * (T + 2) + 1) * ld4(K) + k];
+  q0[k] = s;
+}
+
+__global__ void log_softmax_small_kernel(const float* v, int K, float* out) {
+  if (threadIdx.x != 0) return;
+  float m = -__builtin_inff();
+  for (int k = 0; k < K; ++k) m = fmaxf(m, v[k]);
+  float s = 0.f;
+  for (int k = 0; k < K; ++k) s += __expf(v[k] - m);
+  const float l = m + __logf(s);
+  for (int k = 0; k < K; ++k) out[k] = v[k] - l;
+}
+
+bool staged_head_supported(int K) { return K >= 1 && K <= 64; }
+
+int launch_staged_head(const StagedHeadArgs& a, int l2grid, hipStream_t s) {
+  if (!staged_head_supported(a.K)) return VQHMM_EUNSUPPORTED;
+  log_softmax_small_kernel<<<1, 64, 0, s>>>(a.log_prior, a.K, a.log_pi);
+  VQHMM_LAUNCH_CHECK();
+  const unsigned g1 = (unsigned)std::min<int64_t>(cdiv(a.R, 4), 2048);
+  if (a.K <= 16) head_l1_kernel<16><<<g1, 256, 0, s>>>(a);
+  else if (a.K <= 32) head_l1_kernel<32><<<g1, 256, 0, s>>>(a);
+  else head_l1_kernel<64><<<g1, 256, 0, s>>>(a);
+  VQHMM_LAUNCH_CHECK();
+  head_l2_kernel<<<l2grid, 256, 0, s>>>(a);
+  VQHMM_LAUNCH_CHECK();
+  if (a.need_grad) {
+    head_q0_kernel<<<1, 64, 0, s>>>(a.q, a.B, a.T, a.K, a.q0);
+    VQHMM_LAUNCH_CHECK();
+  }
+  return VQHMM_OK;
+}
+
+}  // namespace vqhmm

@@ -102,6 +102,28 @@ int64_t wgrad_chunks(int64_t R, int64_t tiles);
 bool wgrad2_supported(const WgradArgs& a);
 int64_t wgrad2_rows(int64_t R, int N, int C, int ks);
 int launch_wgrad2(const WgradArgs& a, hipStream_t s);
+// Staged ELBO head (head_staged.hip): shapes the fused heads do not cover.
+struct StagedHeadArgs {
+  int64_t B;
+  int T;
+  int64_t R;
+  int D, K;
+  const float *x, *par, *logits, *q;  // PCL
+  const int64_t* lengths;
+  const float* log_prior;
+  float* log_pi;                      // (K) scratch
+  float* lgA;                         // PCL (R, ld4(K*K)): transition logits in, d logits out
+  float *nx, *dqc, *trw;              // PCL (R, ld4(K)) x2, (R)
+  float cpri, cent;                   // -beta / B, beta / B
+  int need_grad;
+  float *dpar, *dlx, *dqx;
+  double* part;                       // [l2grid][4]
+  float* q0;                          // (K)
+};
+bool staged_head_supported(int K);
+bool fused_head_supported(const HeadArgs& a);
+int launch_staged_head(const StagedHeadArgs& a, int l2grid, hipStream_t s);
+
 int head_grid(int64_t R);
 bool head_mfma_supported(const HeadArgs& a);
 int launch_head_mfma(const HeadArgs& a, int grid, hipStream_t s);

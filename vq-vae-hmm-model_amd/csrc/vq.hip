@@ -22,6 +22,8 @@
 // Fallback (K > 32 or Dv > 64): VALU kernel over LDS codebook blocks, same chain.
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "kernels.h"
 
 namespace vqhmm {
@@ -114,90 +116,104 @@ __global__ __launch_bounds__(256) void vq_mfma_kernel(const float* __restrict__ 
   }
 }
 
-// Row-load variant (T % 4 == 0): a 64-position tile per wave, lane (g, j) =
-// (lane >> 4, lane & 15) loads float4 z[d = 4 dg + g][t .. t+3] of positions
-// 4j .. 4j+3 (each wave load = four 256-B row runs).  v_mfma_f32_16x16x4_f32 m
-// (m = 0..3) takes component m as B[k = g][col j] = z[4 dg + g][position 4j + m];
-// A = -2 c[16 cb + j][4 dg + g].  CB x 4 independent accumulators per tile.
-template <int DG, int CB>  // Dv <= 4 DG, K <= 16 CB
+// Row-load variant (T % 4 == 0, Dv % 4 == 0): a 64-position tile per wave, lane
+// (g, j) = (lane >> 4, lane & 15) loads float4 z[d = 4 dg + g][t .. t+3] of
+// positions 4j .. 4j+3 (each wave load = four 256-B row runs).
+// v_mfma_f32_16x16x4_f32 m (m = 0..3) takes component m as B[k = g][col j] =
+// z[4 dg + g][position 4j + m]; A = -2 c[16 cb + j][4 dg + g] (from LDS).
+// CB x 4 independent accumulators per tile.  Loads are buffer loads: one VGPR
+// byte offset per tile + the dim-group offset 16 T dg as an SGPR.  Each wave
+// walks a contiguous range of tiles (lines shared by neighbouring tiles stay
+// in one XCD's L2), and reloads dim group dg of the next tile right after the
+// current tile's MFMAs have consumed it.
+template <int DG, int CB>  // Dv == 4 DG, K <= 16 CB
 __global__ __launch_bounds__(256) void vq_rows_kernel(const float* __restrict__ z, int64_t B, int Dv, int T,
                                                       const float* __restrict__ cb, int K, int32_t* __restrict__ idx,
-                                                      float* __restrict__ dmin, int64_t tiles) {
-  const int lane = threadIdx.x & 63, g = lane >> 4, j = lane & 15;
+                                                      float* __restrict__ dmin, int64_t tiles, int64_t per_wave) {
+  __shared__ float cbS[16 * CB][4 * DG + 1];  // codebook, +1 pad: conflict-free per-code rows
+  __shared__ float aS[CB][DG][64];
+  __shared__ float cnS[16 * CB];
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, j = lane & 15;
   const int64_t N = B * (int64_t)T;
-  const int64_t wave0 = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t nwaves = (int64_t)gridDim.x * 4;
 
-  // byte offsets are 32-bit (launcher guarantees 4*B*Dv*T < 2^32): a uniform base
-  // plus one VGPR offset per load; per-lane row offsets are tile-invariant
-  const char* zb = reinterpret_cast<const char*>(z);
-  uint32_t rowoff[DG];
-#pragma unroll
-  for (int dg = 0; dg < DG; ++dg) rowoff[dg] = (uint32_t)min(4 * dg + g, Dv - 1) * (uint32_t)T * 4u;
+  const uint32_t nbytes = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(N * Dv * 4));
+  const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc((void*)z, (short)0, (int)nbytes, 0x00020000);
+  const int gstep = __builtin_amdgcn_readfirstlane(16 * T);  // bytes between dim groups
+  const uint32_t goff = (uint32_t)g * (uint32_t)T * 4u;
   auto tile_off = [&](int64_t tile) -> uint32_t {
     int64_t n = tile * 64 + 4 * j;
     n = n < N ? n : N - 4;  // clamped address; clamped lanes store nothing
     const int64_t b = n / T;
-    return (uint32_t)((b * (int64_t)Dv * T + (n - b * T)) * 4);
+    return (uint32_t)((b * (int64_t)Dv * T + (n - b * T)) * 4) + goff;
   };
-  f32x4 zc[DG];
-  if (wave0 < tiles) {
-    const uint32_t o = tile_off(wave0);
-#pragma unroll
-    for (int dg = 0; dg < DG; ++dg) zc[dg] = *reinterpret_cast<const f32x4*>(zb + (o + rowoff[dg]));
-  }
+  auto ld = [&](uint32_t o, int dg) -> f32x4 {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rz, (int)o, dg * gstep, 0));
+  };
 
-  float a[CB][DG];
+  constexpr int NC = 16 * CB * 4 * DG, NCP = (NC + 255) / 256;
+  float cbv[NCP];
 #pragma unroll
-  for (int c = 0; c < CB; ++c)
+  for (int k = 0; k < NCP; ++k) cbv[k] = cb[min(tid + 256 * k, K * Dv - 1)];
+
+  const int64_t gw = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t t0 = gw * per_wave, t1 = min(t0 + per_wave, tiles);
+  f32x4 zc[DG];
+  {
+    const uint32_t o = tile_off(t0 < t1 ? t0 : 0);  // unconditional: keeps vmcnt counting exact
 #pragma unroll
-    for (int dg = 0; dg < DG; ++dg)
-      a[c][dg] = cb[(int64_t)min(16 * c + j, K - 1) * Dv + min(4 * dg + g, Dv - 1)];
+    for (int dg = 0; dg < DG; ++dg) zc[dg] = ld(o, dg);  // in flight during the prologue
+  }
+  // prologue: the codebook crosses HBM once per workgroup (coalesced; loaded
+  // before the first tile so vmcnt can retire it first), then the A fragments
+  // and the ||c||^2 chains are built from LDS
 #pragma unroll
-  for (int c = 0; c < CB; ++c)
-#pragma unroll
-    for (int dg = 0; dg < DG; ++dg) a[c][dg] = (16 * c + j < K && 4 * dg + g < Dv) ? -2.0f * a[c][dg] : 0.0f;
-  // ||c||^2 of code 16 c + j in d order: dims 4 dg + r live in lane j + 16 r
-  float init[CB][4];
-#pragma unroll
-  for (int c = 0; c < CB; ++c) {
+  for (int k = 0; k < NCP; ++k) {
+    const int i = tid + 256 * k;
+    if (i < NC) cbS[i / (4 * DG)][i % (4 * DG)] = (i / (4 * DG)) < K ? cbv[k] : 0.0f;
+  }
+  lds_barrier();
+  for (int i = tid; i < CB * DG * 64; i += 256) {
+    const int c = i / (DG * 64), dg = (i / 64) % DG, l = i & 63;
+    aS[c][dg][l] = -2.0f * cbS[16 * c + (l & 15)][4 * dg + (l >> 4)];
+  }
+  if (tid < 16 * CB) {
     float cn = 0.0f;
 #pragma unroll
-    for (int dg = 0; dg < DG; ++dg)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float v = -0.5f * __shfl(a[c][dg], j + 16 * r);
-        if (4 * dg + r < Dv) cn = __builtin_fmaf(v, v, cn);
-      }
-    if (16 * c + j >= K) cn = __builtin_inff();
-#pragma unroll
-    for (int v = 0; v < 4; ++v) init[c][v] = __shfl(cn, 4 * g + v);  // rows of this lane: codes 16c + 4g + v
+    for (int d = 0; d < 4 * DG; ++d) cn = __builtin_fmaf(cbS[tid][d], cbS[tid][d], cn);
+    cnS[tid] = tid < K ? cn : __builtin_inff();
   }
 
-  for (int64_t tile = wave0; tile < tiles; tile += nwaves) {
-    // next tile's row pointer; its loads are issued dim-group by dim-group as
-    // soon as the current tile's group has gone through the MFMAs
-    const bool more = tile + nwaves < tiles;
-    const uint32_t no = tile_off(more ? tile + nwaves : tile);
+  lds_barrier();
+  float init[CB][4];
+#pragma unroll
+  for (int c = 0; c < CB; ++c)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) init[c][v] = cnS[16 * c + 4 * g + v];
+
+  // one tile; RELOAD: fetch dim group dg of tile + 1 into zc[dg] right after it
+  // has been consumed (the last tile of the range is peeled off with RELOAD =
+  // false, so the steady-state reload is unconditional and lands in place)
+  auto run_tile = [&](int64_t tile, auto reload) {
+    constexpr bool RELOAD = decltype(reload)::value;
+    const uint32_t no = tile_off(tile + 1);
     f32x4 acc[CB][4];
 #pragma unroll
     for (int c = 0; c < CB; ++c)
 #pragma unroll
       for (int m = 0; m < 4; ++m) acc[c][m] = f32x4{init[c][0], init[c][1], init[c][2], init[c][3]};
-    // ||z||^2 partial chain of this lane's residue d = g (mod 4), per position m
-    float q[4] = {0.f, 0.f, 0.f, 0.f};
+    float q[4] = {0.f, 0.f, 0.f, 0.f};  // ||z||^2 chain of residue d = g (mod 4), per position m
 #pragma unroll
     for (int dg = 0; dg < DG; ++dg) {
+      float av[CB];
+#pragma unroll
+      for (int c = 0; c < CB; ++c) av[c] = aS[c][dg][lane];
 #pragma unroll
       for (int m = 0; m < 4; ++m)
 #pragma unroll
-        for (int c = 0; c < CB; ++c) acc[c][m] = mfma16x16x4(a[c][dg], zc[dg][m], acc[c][m]);
+        for (int c = 0; c < CB; ++c) acc[c][m] = mfma16x16x4(av[c], zc[dg][m], acc[c][m]);
 #pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const float zv = (4 * dg + g < Dv) ? zc[dg][m] : 0.0f;
-        if (4 * dg < Dv) q[m] = __builtin_fmaf(zv, zv, q[m]);
-      }
-      if (more) zc[dg] = *reinterpret_cast<const f32x4*>(zb + (no + rowoff[dg]));
+      for (int m = 0; m < 4; ++m) q[m] = __builtin_fmaf(zc[dg][m], zc[dg][m], q[m]);
+      if constexpr (RELOAD) zc[dg] = ld(no, dg);
     }
     float fb = 0.f, fz = 0.f;
     int fa = 0;
@@ -210,14 +226,18 @@ __global__ __launch_bounds__(256) void vq_rows_kernel(const float* __restrict__ 
 #pragma unroll
         for (int v = 0; v < 4; ++v)
           if (acc[c][m][v] < best) { best = acc[c][m][v]; arg = 16 * c + 4 * g + v; }
-#pragma unroll
-      for (int o = 16; o <= 32; o <<= 1) {
-        const float pb = __shfl_xor(best, o);
-        const int pa = __shfl_xor(arg, o);
+      {
+        const float pb = xor16(best);
+        const int pa = xor16(arg);
         if (pb < best || (pb == best && pa < arg)) { best = pb; arg = pa; }
       }
-      const float s2 = q[m] + __shfl_xor(q[m], 16);  // q0+q1 (g < 2) or q2+q3 (g >= 2)
-      const float zz = s2 + __shfl_xor(s2, 32);
+      {
+        const float pb = xor32(best);
+        const int pa = xor32(arg);
+        if (pb < best || (pb == best && pa < arg)) { best = pb; arg = pa; }
+      }
+      const float s2 = q[m] + xor16(q[m]);  // q0+q1 (g < 2) or q2+q3 (g >= 2)
+      const float zz = s2 + xor32(s2);
       if (g == m) { fb = best; fa = arg; fz = zz; }
     }
     const int64_t n = tile * 64 + 4 * j + g;
@@ -225,6 +245,10 @@ __global__ __launch_bounds__(256) void vq_rows_kernel(const float* __restrict__ 
       idx[n] = fa;
       if (dmin) dmin[n] = fb + fz;
     }
+  };
+  if (t0 < t1) {
+    for (int64_t tile = t0; tile + 1 < t1; ++tile) run_tile(tile, std::true_type{});
+    run_tile(t1 - 1, std::false_type{});
   }
 }
 
@@ -323,17 +347,24 @@ template <int DG, int CB>
 static void launch_rows(const float* z, int64_t B, int Dv, int T, const float* cb, int K, int32_t* idx, float* dmin,
                         hipStream_t s) {
   const int64_t tiles = cdiv(B * (int64_t)T, 64);
-  vq_rows_kernel<DG, CB>
-      <<<(unsigned)cdiv(persistent_waves(tiles), 4), 256, 0, s>>>(z, B, Dv, T, cb, K, idx, dmin, tiles);
+  const int64_t waves = persistent_waves(tiles);
+  const int64_t per_wave = cdiv(tiles, waves);
+  vq_rows_kernel<DG, CB><<<(unsigned)cdiv(cdiv(tiles, per_wave), 4), 256, 0, s>>>(z, B, Dv, T, cb, K, idx, dmin,
+                                                                                   tiles, per_wave);
 }
 
+// Dv % 4 == 0 only (whole dim groups)
 template <int CB>
-static void dispatch_rows(const float* z, int64_t B, int Dv, int T, const float* cb, int K, int32_t* idx,
+static bool dispatch_rows(const float* z, int64_t B, int Dv, int T, const float* cb, int K, int32_t* idx,
                           float* dmin, hipStream_t s) {
-  if (Dv <= 8) launch_rows<2, CB>(z, B, Dv, T, cb, K, idx, dmin, s);
-  else if (Dv <= 16) launch_rows<4, CB>(z, B, Dv, T, cb, K, idx, dmin, s);
-  else if (Dv <= 32) launch_rows<8, CB>(z, B, Dv, T, cb, K, idx, dmin, s);
-  else launch_rows<16, CB>(z, B, Dv, T, cb, K, idx, dmin, s);
+  switch (Dv) {
+    case 4: launch_rows<1, CB>(z, B, Dv, T, cb, K, idx, dmin, s); return true;
+    case 8: launch_rows<2, CB>(z, B, Dv, T, cb, K, idx, dmin, s); return true;
+    case 16: launch_rows<4, CB>(z, B, Dv, T, cb, K, idx, dmin, s); return true;
+    case 32: launch_rows<8, CB>(z, B, Dv, T, cb, K, idx, dmin, s); return true;
+    case 64: launch_rows<16, CB>(z, B, Dv, T, cb, K, idx, dmin, s); return true;
+    default: return false;
+  }
 }
 
 int launch_vq_argmin(const float* z, int64_t B, int64_t Dv, int64_t T, const float* cb, int64_t K,
@@ -344,10 +375,12 @@ int launch_vq_argmin(const float* z, int64_t B, int64_t Dv, int64_t T, const flo
   static const int impl = env_int("VQHMM_VQ_IMPL", 0, 0, 2);  // 0 auto, 1 tile-32, 2 rows
   const bool rows_ok = T % 4 == 0 && (reinterpret_cast<uintptr_t>(z) & 15) == 0 && N * Dv < (int64_t(1) << 30);
   if (K <= 32 && Dv <= 64 && rows_ok && impl != 1) {
-    if (K <= 16) dispatch_rows<1>(z, B, (int)Dv, (int)T, cb, (int)K, idx, dmin, s);
-    else dispatch_rows<2>(z, B, (int)Dv, (int)T, cb, (int)K, idx, dmin, s);
-    VQHMM_LAUNCH_CHECK();
-    return VQHMM_OK;
+    const bool done = K <= 16 ? dispatch_rows<1>(z, B, (int)Dv, (int)T, cb, (int)K, idx, dmin, s)
+                              : dispatch_rows<2>(z, B, (int)Dv, (int)T, cb, (int)K, idx, dmin, s);
+    if (done) {
+      VQHMM_LAUNCH_CHECK();
+      return VQHMM_OK;
+    }
   }
   if (K <= 32 && Dv <= 64) {
     const int S = (int)cdiv(Dv, 2);
