@@ -125,9 +125,9 @@ def vq_cfg3(lib):
     byts = 4.0 * B * T * Dv + 4.0 * K * Dv + 4.0 * B * T
     gbps = byts / (us * 1e-6) / 1e9
     del z
-    return {"kernel": "vq_argmin_kernel", "bound": "hbm", "avg_us": round(us, 2), "achieved": round(gbps, 1),
+    return {"kernel": "vq_rows_kernel (vqhmm_vq_argmin_f32)", "bound": "hbm", "avg_us": round(us, 2), "achieved": round(gbps, 1),
             "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(gbps / HBM_PEAK_GBPS, 4),
-            "traffic": traffic_for("vq_argmin_kernel", "vq_cfg3"), "shape": "B2048 Dv64 T200 K32"}
+            "traffic": traffic_for("vq_argmin", "vq_cfg3"), "shape": "B2048 Dv64 T200 K32"}
 
 
 def cpu_baseline(cfg, seconds):

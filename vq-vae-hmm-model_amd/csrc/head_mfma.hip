@@ -10,11 +10,11 @@
 //            fragments are the B operand as they stand: rows h = 4*(l>>4)+v)
 //   phase B  VALU, thread per row: log_softmax -> log_A, recon NLL, entropy,
 //            init/transition terms, dq, d log_A -> d lg (log_softmax backward)
-//   phase C  dhid^T = W2^T @ dlg^T, masked by relu'(hid^T);
+//   phase C  hid, dhid = (dlg @ W2) * relu'(hid) in (rows x h) layout;
 //            gW2' (16 x TH+16) += dlg^T @ [hid | 1]   (the ones column gives db2)
 //            gW1' (TH x 16)   += dhid^T @ u'           (column U gives db1)
-//            hid and dhid cross LDS once (a 16-row transpose) for the two
-//            contractions over rows.
+//            with row 4*(lane>>4) + s as contraction step s, the hid / dhid
+//            accumulator registers are the operands directly (no transposes).
 // Weight-gradient accumulators stay in registers across all tiles of the
 // workgroup; the 4 waves are summed in fixed order at the end (deterministic).
 #include <type_traits>
@@ -38,8 +38,6 @@ struct HeadLds {
   float dlgS[MP * 16];
   float qS[(MP + 2) * 4];
   int wS[MP + 2];
-  float hT[4][2][16 * 16];  // per-wave, per-block-of-the-pair 16-row x 16-h transposes
-  float dT[4][2][16 * 16];  //   (row stride 16 = conflict-free column reads)
   float lpS[4];
   unsigned long long cnt;
 };
@@ -178,49 +176,51 @@ __global__ __launch_bounds__(256, 2) void elbo_head_mfma_kernel(HeadArgs a) {
     for (int i = 0; i < NP; ++i) *reinterpret_cast<f32x4*>(&sh.lgS[(p0[i] + l16) * 16 + 4 * lg4]) = lg[i];
   };
 
-  // ---- phase C (MLP backward) on NP row blocks of this wave at once
+  // ---- phase C (MLP backward) on NP row blocks of this wave at once.  hid and
+  // dhid are produced in (rows x h) layout, lane (lg4, l16) holding rows
+  // 4*lg4 + v of hidden unit hb*16 + l16; the contractions over rows then map
+  // row 4*lg4 + s to MFMA step s, so register v = s of those fragments IS the
+  // operand (no transposes).
   auto phase_c = [&](auto np_tag, int blk0, int blk1) {
     constexpr int NP = decltype(np_tag)::value;
     const int p0[2] = {blk0 * 16, blk1 * 16};
-    float ub0[NP], ub1[NP], dla[NP][4], ua[NP][4];
-    f32x4 dlb[NP];
+    float ua[NP][2], dla[NP][4], dlt[NP][4], ub[NP][4];
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
-      ub0[i] = sh.uS[(p0[i] + l16) * 8 + lg4];
-      ub1[i] = sh.uS[(p0[i] + l16) * 8 + 4 + lg4];
-      dlb[i] = *reinterpret_cast<const f32x4*>(&sh.dlgS[(p0[i] + l16) * 16 + 4 * lg4]);
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        const int pr = p0[i] + 4 * s4 + lg4;
-        dla[i][s4] = sh.dlgS[pr * 16 + l16];
-        const float uv = sh.uS[pr * 8 + (l16 & 7)];
-        ua[i][s4] = l16 < 8 ? uv : 0.f;
+      for (int s = 0; s < 2; ++s) ua[i][s] = sh.uS[(p0[i] + l16) * 8 + 4 * s + lg4];       // u'[row l16][c 4s+lg4]
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        dla[i][s] = sh.dlgS[(p0[i] + l16) * 16 + 4 * s + lg4];                              // dlg[row l16][ij 4s+lg4]
+        dlt[i][s] = sh.dlgS[(p0[i] + 4 * lg4 + s) * 16 + l16];                              // dlg[row 4lg4+s][ij l16]
+        const float uv = sh.uS[(p0[i] + 4 * lg4 + s) * 8 + (l16 & 7)];
+        ub[i][s] = l16 < 8 ? uv : 0.f;                                                      // u'[row 4lg4+s][c' l16]
       }
     }
     // db2: contraction of dlg^T with a ones column
 #pragma unroll
     for (int i = 0; i < NP; ++i)
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) gW2[HB] = mfma16x16x4(dla[i][s4], l16 == 0 ? 1.f : 0.f, gW2[HB]);
+      for (int s = 0; s < 4; ++s) gW2[HB] = mfma16x16x4(dlt[i][s], l16 == 0 ? 1.f : 0.f, gW2[HB]);
 #pragma unroll
     for (int hb = 0; hb < HB; ++hb) {
-      const float w1a = sh.W1S[(hb * 16 + l16) * 8 + lg4], w1b = sh.W1S[(hb * 16 + l16) * 8 + 4 + lg4];
-      float w2c[4];
+      float w1b[2], w2b[4];
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) w2c[s4] = sh.W2S[(4 * lg4 + s4) * S::LDW2 + hb * 16 + l16];
+      for (int s = 0; s < 2; ++s) w1b[s] = sh.W1S[(hb * 16 + l16) * 8 + 4 * s + lg4];        // W1'[h][c 4s+lg4]
+#pragma unroll
+      for (int s = 0; s < 4; ++s) w2b[s] = sh.W2S[(4 * s + lg4) * S::LDW2 + hb * 16 + l16];  // W2[ij 4s+lg4][h]
       f32x4 h[NP], dh[NP];
 #pragma unroll
       for (int i = 0; i < NP; ++i) {
-        h[i] = mfma16x16x4(w1a, ub0[i], f32x4{0.f, 0.f, 0.f, 0.f});
-        dh[i] = mfma16x16x4(w2c[0], dlb[i][0], f32x4{0.f, 0.f, 0.f, 0.f});
+        h[i] = mfma16x16x4(ua[i][0], w1b[0], f32x4{0.f, 0.f, 0.f, 0.f});
+        dh[i] = mfma16x16x4(dla[i][0], w2b[0], f32x4{0.f, 0.f, 0.f, 0.f});
       }
 #pragma unroll
-      for (int i = 0; i < NP; ++i) h[i] = mfma16x16x4(w1b, ub1[i], h[i]);
-      // dhid^T block: A[i = h][k = ij = 4*lg4 + s] = W2[ij][h], B[k][j = p] = dlg[p][ij]
+      for (int i = 0; i < NP; ++i) h[i] = mfma16x16x4(ua[i][1], w1b[1], h[i]);
 #pragma unroll
-      for (int s4 = 1; s4 < 4; ++s4)
+      for (int s = 1; s < 4; ++s)
 #pragma unroll
-        for (int i = 0; i < NP; ++i) dh[i] = mfma16x16x4(w2c[s4], dlb[i][s4], dh[i]);
+        for (int i = 0; i < NP; ++i) dh[i] = mfma16x16x4(dla[i][s], w2b[s], dh[i]);
 #pragma unroll
       for (int i = 0; i < NP; ++i) {
         f32x4 hr, dm;
@@ -229,19 +229,12 @@ __global__ __launch_bounds__(256, 2) void elbo_head_mfma_kernel(HeadArgs a) {
           hr[v] = fmaxf(h[i][v], 0.f);
           dm[v] = h[i][v] > 0.f ? dh[i][v] : 0.f;
         }
-        // transpose through LDS: [p][h_local]
-        *reinterpret_cast<f32x4*>(&sh.hT[wave][i][l16 * 16 + 4 * lg4]) = hr;
-        *reinterpret_cast<f32x4*>(&sh.dT[wave][i][l16 * 16 + 4 * lg4]) = dm;
-      }
-      // contractions over the rows (k = p = 4*s + lg4) of both blocks
 #pragma unroll
-      for (int i = 0; i < NP; ++i)
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) {
-          const int pr = 4 * s4 + lg4;
-          gW2[hb] = mfma16x16x4(dla[i][s4], sh.hT[wave][i][pr * 16 + l16], gW2[hb]);
-          gW1[hb] = mfma16x16x4(sh.dT[wave][i][pr * 16 + l16], ua[i][s4], gW1[hb]);
+        for (int s = 0; s < 4; ++s) {
+          gW2[hb] = mfma16x16x4(dlt[i][s], hr[s], gW2[hb]);   // (ij x h) += dlg^T . hid
+          gW1[hb] = mfma16x16x4(dm[s], ub[i][s], gW1[hb]);    // (h x c') += dhid^T . u'
         }
+      }
     }
   };
   using One = std::integral_constant<int, 1>;

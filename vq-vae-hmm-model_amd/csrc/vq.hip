@@ -126,14 +126,27 @@ __global__ __launch_bounds__(256) void vq_mfma_kernel(const float* __restrict__ 
 // walks a contiguous range of tiles (lines shared by neighbouring tiles stay
 // in one XCD's L2), and reloads dim group dg of the next tile right after the
 // current tile's MFMAs have consumed it.
-template <int DG, int CB>  // Dv == 4 DG, K <= 16 CB
-__global__ __launch_bounds__(256) void vq_rows_kernel(const float* __restrict__ z, int64_t B, int Dv, int T,
+template <int DG, int CB, bool PF>  // Dv == 4 DG, K <= 16 CB; PF: double-buffer the next tile in registers
+__global__ __launch_bounds__(256, PF ? 2 : 3) void vq_rows_kernel(const float* __restrict__ z, int64_t B, int Dv, int T,
                                                       const float* __restrict__ cb, int K, int32_t* __restrict__ idx,
-                                                      float* __restrict__ dmin, int64_t tiles, int64_t per_wave) {
-  __shared__ float cbS[16 * CB][4 * DG + 1];  // codebook, +1 pad: conflict-free per-code rows
+                                                      float* __restrict__ dmin, int64_t tiles, int64_t nwaves) {
+  constexpr int LDSC = 16 * CB + 4;  // score rows [position][code]
+  struct Prologue {
+    float cbS[16 * CB][4 * DG + 1];  // codebook, +1 pad: conflict-free per-code rows
+  };
+  struct Loop {
+    float scS[4][64 * LDSC];  // per-wave score transpose
+    float qS[4][64 * 4];      // per-wave ||z||^2 partials [position][residue]
+  };
+  __shared__ union {
+    Prologue pro;
+    Loop loop;
+  } u;
   __shared__ float aS[CB][DG][64];
   __shared__ float cnS[16 * CB];
+  auto& cbS = u.pro.cbS;
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, j = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t N = B * (int64_t)T;
 
   const uint32_t nbytes = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(N * Dv * 4));
@@ -156,7 +169,9 @@ __global__ __launch_bounds__(256) void vq_rows_kernel(const float* __restrict__ 
   for (int k = 0; k < NCP; ++k) cbv[k] = cb[min(tid + 256 * k, K * Dv - 1)];
 
   const int64_t gw = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int64_t t0 = gw * per_wave, t1 = min(t0 + per_wave, tiles);
+  // equal share of the tiles per wave (every resident wave gets floor or ceil of tiles / nwaves)
+  const int64_t t0 = gw < nwaves ? tiles * gw / nwaves : tiles;
+  const int64_t t1 = gw < nwaves ? tiles * (gw + 1) / nwaves : tiles;
   f32x4 zc[DG];
   {
     const uint32_t o = tile_off(t0 < t1 ? t0 : 0);  // unconditional: keeps vmcnt counting exact
@@ -215,40 +230,51 @@ __global__ __launch_bounds__(256) void vq_rows_kernel(const float* __restrict__ 
       for (int m = 0; m < 4; ++m) q[m] = __builtin_fmaf(zc[dg][m], zc[dg][m], q[m]);
       if constexpr (RELOAD) zc[dg] = ld(no, dg);
     }
-    float fb = 0.f, fz = 0.f;
-    int fa = 0;
+    // scores through LDS as [position][code] so each lane scans ONE position's
+    // codes in ascending order (strict <: lowest code wins ties); position
+    // p = 4j + m, code = 16c + 4g + v
+    float* sc = u.loop.scS[wave];
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
-      float best = __builtin_inff();
-      int arg = 4 * g;
 #pragma unroll
-      for (int c = 0; c < CB; ++c)
-#pragma unroll
-        for (int v = 0; v < 4; ++v)
-          if (acc[c][m][v] < best) { best = acc[c][m][v]; arg = 16 * c + 4 * g + v; }
-      {
-        const float pb = xor16(best);
-        const int pa = xor16(arg);
-        if (pb < best || (pb == best && pa < arg)) { best = pb; arg = pa; }
-      }
-      {
-        const float pb = xor32(best);
-        const int pa = xor32(arg);
-        if (pb < best || (pb == best && pa < arg)) { best = pb; arg = pa; }
-      }
-      const float s2 = q[m] + xor16(q[m]);  // q0+q1 (g < 2) or q2+q3 (g >= 2)
-      const float zz = s2 + xor32(s2);
-      if (g == m) { fb = best; fa = arg; fz = zz; }
+      for (int c = 0; c < CB; ++c) *reinterpret_cast<f32x4*>(sc + (4 * j + m) * LDSC + 16 * c + 4 * g) = acc[c][m];
+      u.loop.qS[wave][(4 * j + m) * 4 + g] = q[m];
     }
-    const int64_t n = tile * 64 + 4 * j + g;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    float best = __builtin_inff();
+    int arg = 0;
+#pragma unroll
+    for (int c4 = 0; c4 < 4 * CB; ++c4) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(sc + lane * LDSC + 4 * c4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (v[e] < best) { best = v[e]; arg = 4 * c4 + e; }
+    }
+    const f32x4 qq = *reinterpret_cast<const f32x4*>(&u.loop.qS[wave][lane * 4]);
+    const float zz = (qq[0] + qq[1]) + (qq[2] + qq[3]);
+    const int64_t n = tile * 64 + lane;
     if (n < N) {
-      idx[n] = fa;
-      if (dmin) dmin[n] = fb + fz;
+      idx[n] = arg;
+      if (dmin) dmin[n] = best + zz;
     }
+    __builtin_amdgcn_wave_barrier();  // the next tile's writes must not pass this tile's reads
   };
   if (t0 < t1) {
-    for (int64_t tile = t0; tile + 1 < t1; ++tile) run_tile(tile, std::true_type{});
-    run_tile(t1 - 1, std::false_type{});
+    if constexpr (PF) {
+      for (int64_t tile = t0; tile + 1 < t1; ++tile) run_tile(tile, std::true_type{});
+      run_tile(t1 - 1, std::false_type{});
+    } else {  // no in-wave prefetch: fewer registers, more resident waves hide the latency
+      for (int64_t tile = t0; tile < t1; ++tile) {
+        if (tile != t0) {
+          const uint32_t o = tile_off(tile);
+#pragma unroll
+          for (int dg = 0; dg < DG; ++dg) zc[dg] = ld(o, dg);
+        }
+        run_tile(tile, std::false_type{});
+      }
+    }
   }
 }
 
@@ -331,9 +357,9 @@ static int env_int(const char* name, int dflt, int lo, int hi) {
   return v >= lo && v <= hi ? v : dflt;
 }
 
-static int64_t persistent_waves(int64_t tiles) {
-  static const int wpc = env_int("VQHMM_VQ_WPC", 8, 1, 32);  // tuning knob: resident waves per CU
-  return std::min<int64_t>(tiles, 256 * (int64_t)wpc);
+static int64_t persistent_waves(int64_t tiles, int dflt = 8) {
+  static const int wpc = env_int("VQHMM_VQ_WPC", 0, 1, 32);  // tuning knob: resident waves per CU
+  return std::min<int64_t>(tiles, 256 * (int64_t)(wpc ? wpc : dflt));
 }
 
 template <int S>
@@ -346,11 +372,14 @@ static void launch_mfma(const float* z, int64_t B, int Dv, int T, const float* c
 template <int DG, int CB>
 static void launch_rows(const float* z, int64_t B, int Dv, int T, const float* cb, int K, int32_t* idx, float* dmin,
                         hipStream_t s) {
+  static const int pf = env_int("VQHMM_VQ_PF", 1, 0, 1);  // tuning knob: in-wave double buffer
   const int64_t tiles = cdiv(B * (int64_t)T, 64);
-  const int64_t waves = persistent_waves(tiles);
-  const int64_t per_wave = cdiv(tiles, waves);
-  vq_rows_kernel<DG, CB><<<(unsigned)cdiv(cdiv(tiles, per_wave), 4), 256, 0, s>>>(z, B, Dv, T, cb, K, idx, dmin,
-                                                                                   tiles, per_wave);
+  const int64_t waves = cdiv(persistent_waves(tiles, pf ? 8 : 12), 4) * 4;
+  const unsigned grid = (unsigned)(waves / 4);
+  if (pf)
+    vq_rows_kernel<DG, CB, true><<<grid, 256, 0, s>>>(z, B, Dv, T, cb, K, idx, dmin, tiles, waves);
+  else
+    vq_rows_kernel<DG, CB, false><<<grid, 256, 0, s>>>(z, B, Dv, T, cb, K, idx, dmin, tiles, waves);
 }
 
 // Dv % 4 == 0 only (whole dim groups)
