@@ -187,7 +187,7 @@ int vqhmm_viterbi_f32(const float* log_pi, const float* log_A, const float* em, 
 }
 
 size_t vqhmm_fwdbwd_workspace_size(int64_t B, int64_t T, int64_t K) {
-  return (B < 0 || T < 0 || K < 1) ? 0 : (size_t)B * T * K * sizeof(float);
+  return (B < 0 || T < 0 || K < 1) ? 0 : fwdbwd_ws_bytes(B, T, K);
 }
 
 int vqhmm_fwdbwd_f32(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths, int64_t B,

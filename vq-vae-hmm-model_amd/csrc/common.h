@@ -48,19 +48,30 @@ __device__ __forceinline__ bool row_bt(int64_t r, int64_t R, int T, int64_t& b, 
 
 // Lane exchange x[lane ^ 16] / x[lane ^ 32] on the VALU (gfx950 v_permlane16/32_swap:
 // vdst's odd 16-lane rows (upper half) trade places with src's even rows (lower
-// half); with vdst = src = x the partner's value lands in r[0] for lanes with
-// the bit set and in r[1] otherwise).  No LDS round trip, unlike ds_bpermute.
+// half); with vdst = src = x the partner's value lands in vdst for lanes with
+// the bit set and in src otherwise).  No LDS round trip, unlike ds_bpermute.
+// Inline asm: hipcc (ROCm 7.2) treats the two results of the permlane*_swap
+// builtins as equal and folds any use of both (a miscompile for this purpose).
+// The s_nop covers the VALU-write -> permlane-read hazard.
+__device__ __forceinline__ float2 pair16(float x) {
+  float a = x, b = x;
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+  return make_float2(a, b);  // {x, partner} in some order
+}
+__device__ __forceinline__ float2 pair32(float x) {
+  float a = x, b = x;
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+  return make_float2(a, b);
+}
 template <typename V>
 __device__ __forceinline__ V xor16(V x) {
-  const unsigned u = __builtin_bit_cast(unsigned, x);
-  const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
-  return __builtin_bit_cast(V, (threadIdx.x & 16) ? r[0] : r[1]);
+  const float2 r = pair16(__builtin_bit_cast(float, x));
+  return __builtin_bit_cast(V, (threadIdx.x & 16) ? r.x : r.y);
 }
 template <typename V>
 __device__ __forceinline__ V xor32(V x) {
-  const unsigned u = __builtin_bit_cast(unsigned, x);
-  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
-  return __builtin_bit_cast(V, (threadIdx.x & 32) ? r[0] : r[1]);
+  const float2 r = pair32(__builtin_bit_cast(float, x));
+  return __builtin_bit_cast(V, (threadIdx.x & 32) ? r.x : r.y);
 }
 
 // Workgroup barrier that orders LDS only: global loads in flight stay in flight

@@ -5,275 +5,699 @@
 // log_A (B,T,K,K)), transition indexing log_A[:, t] = t-1 -> t (:125-127).
 // Exact contracts: include/vqhmm.h and oracle/hmm_ref.py.
 //
-// Lane mapping (K <= 8, KP = next pow2 >= K): a group of KP*KP lanes owns one
-// sequence and holds the whole K x K transition block of a step, one (i, j)
-// entry per lane, so the step's loads are one coalesced access and the
-// reduction over the source state i is a butterfly across KP lanes.  The
-// (i, j) <-> lane map ALTERNATES between steps ("outer": i = g / KP, j = g % KP;
-// "inner": j = g / KP, i = g % KP): after reducing over i the result for state
-// j sits in every lane whose j-coordinate is j, which is exactly the lane that
-// needs it as its i-coordinate in the other map — no broadcast step.
+// Lane mapping (K <= 8, KP = next pow2 >= K): a group of G = KP*KP lanes owns
+// one sequence (SPW = 64 / G sequences per wave) and holds a step's whole K x K
+// transition block, one (i, j) entry per lane.  The (i, j) <-> lane map
+// ALTERNATES between steps ("outer" on even t: i = g / KP, j = g % KP; "inner"
+// on odd t: i = g % KP, j = g / KP): after reducing over i, the value for state
+// j sits in every lane whose j-coordinate is j, which is exactly where the next
+// step needs it as its i-coordinate — no broadcast.  The reductions are DPP
+// (quad_perm / row_half_mirror / row_ror) and gfx950 permlane16/32 swaps: no
+// LDS round trip on the serial chain.
+//
+// The recursion is serial in t, so a step must never wait for memory: the
+// tables stream through a per-wave LDS ring of R chunks of HC steps, filled by
+// LDS-DMA loads (global_load_lds, 16 B per lane when K % 4 == 0) issued R - 1
+// chunks ahead and retired with a counted `s_waitcnt vmcnt` (the loads never
+// drain inside the loop).  Every step then reads its A entry and emission from
+// LDS, off the dependency chain.
+//
+// Viterbi stores, per step, the 64-bit ballot of the lanes that attain the
+// max (one SGPR pair → two writelanes into a 64-step register buffer, one
+// 512-B store per 64 steps).  The backtrace runs on all 64 lanes: each lane
+// composes the backpointer maps of its slice of steps into one byte-permutation
+// (v_perm_b32), a 64-step serial resolve links the slices, then every lane
+// writes its slice of the path.
 // Sequences are independent: no inter-workgroup communication.
+#include <type_traits>
+
 #include "kernels.h"
 
 namespace vqhmm {
 
 constexpr float NEG_INF = -__builtin_inff();
+template <int K, bool W16>
+struct Geo {
+  // steps per staged chunk: a chunk's LDS-DMA instructions x ring depth must
+  // stay under vmcnt's 63 outstanding (more wraps the counter), so the
+  // many-sequences-per-wave small-K maps and 4-byte K = 8 staging use half chunks
+  static constexpr int HC = W16 ? 32 : (K <= 4 || K == 8) ? 16 : 32;
+  static constexpr int KP = K <= 2 ? 2 : K <= 4 ? 4 : 8;
+  static constexpr int G = KP * KP;     // lanes per sequence
+  static constexpr int SPW = 64 / G;    // sequences per wave
+  static constexpr int AS = HC * K * K;  // floats of log_A per sequence per chunk
+  static constexpr int ES = HC * K;      // floats of em per sequence per chunk
+  static constexpr int SLOT = SPW * (AS + ES);
+};
 
-// butterfly over the KP lanes of the reduction axis (outer axis: stride KP; inner: stride 1)
-template <int KP, bool OUTER>
-__device__ __forceinline__ float allmax(float v) {
-#pragma unroll
-  for (int o = OUTER ? KP : 1; o < (OUTER ? KP * KP : KP); o <<= 1) v = fmaxf(v, __shfl_xor(v, o));
+// glds instructions per chunk and ring depth: R chunks of NI instructions can
+// be outstanding at once (the wait leaves R - 1 in flight); vmcnt counts to 63
+template <int K, bool W16>
+struct Ring {
+  static constexpr int U = W16 ? 4 : 1;  // floats per lane per instruction
+  static constexpr int NI = Geo<K, W16>::SLOT / (64 * U);
+  static_assert(Geo<K, W16>::SLOT % (64 * U) == 0, "slot must be whole wave-instructions");
+  static constexpr int RD = 60 / NI;
+  static constexpr int R = RD > 4 ? 4 : RD;
+  static_assert(R >= 2, "chunk too large for a pipelined ring");
+  static constexpr int WAIT = NI * (R - 1);
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+  asm volatile("" ::: "memory");
+}
+
+// compile-time loop: f(std::integral_constant<int, I>) for I = 0 .. N-1
+template <int I, int N>
+struct SFor {
+  template <typename F>
+  __device__ __forceinline__ static void run(F& f) {
+    f(std::integral_constant<int, I>{});
+    SFor<I + 1, N>::run(f);
+  }
+};
+template <int N>
+struct SFor<N, N> {
+  template <typename F>
+  __device__ __forceinline__ static void run(F&) {}
+};
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  SFor<0, N>::run(f);
+}
+
+// ---------------------------------------------------------------- lane exchanges
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+constexpr int DPP_XOR1 = 0xB1;          // quad_perm [1,0,3,2]
+constexpr int DPP_XOR2 = 0x4E;          // quad_perm [2,3,0,1]
+constexpr int DPP_HALF_MIRROR = 0x141;  // l -> 7 - l within 8 lanes
+constexpr int DPP_ROR4 = 0x124;         // row_ror:4 (16-lane rows)
+constexpr int DPP_ROR8 = 0x128;         // row_ror:8
+
+// all-reduce over the KP lanes of one axis of a sequence's lane group:
+// INNER = lanes g % KP (stride 1), else lanes g / KP (stride KP)
+template <int KP, bool INNER, typename Op>
+__device__ __forceinline__ float allred(float v, Op op) {
+  if constexpr (KP == 2) {
+    v = op(v, dpp<INNER ? DPP_XOR1 : DPP_XOR2>(v));
+  } else if constexpr (KP == 4) {
+    if constexpr (INNER) {
+      v = op(v, dpp<DPP_XOR1>(v));
+      v = op(v, dpp<DPP_XOR2>(v));
+    } else {  // cosets {l, l+4, l+8, l+12} of a 16-lane row: two rotations
+      v = op(v, dpp<DPP_ROR4>(v));
+      v = op(v, dpp<DPP_ROR8>(v));
+    }
+  } else {
+    if constexpr (INNER) {
+      v = op(v, dpp<DPP_XOR1>(v));
+      v = op(v, dpp<DPP_XOR2>(v));
+      v = op(v, dpp<DPP_HALF_MIRROR>(v));
+    } else {
+      v = op(v, dpp<DPP_ROR8>(v));
+      const float2 r16 = pair16(v);
+      v = op(r16.x, r16.y);
+      const float2 r32 = pair32(v);
+      v = op(r32.x, r32.y);
+    }
+  }
   return v;
 }
-template <int KP, bool OUTER>
-__device__ __forceinline__ float allsum(float v) {
-#pragma unroll
-  for (int o = OUTER ? KP : 1; o < (OUTER ? KP * KP : KP); o <<= 1) v += __shfl_xor(v, o);
-  return v;
-}
-// arg-max with the lowest index winning ties (associative, so any butterfly order
-// yields the sequential "first maximum")
-template <int KP, bool OUTER>
+struct OpMax {
+  __device__ float operator()(float a, float b) const { return fmaxf(a, b); }
+};
+struct OpAdd {
+  __device__ float operator()(float a, float b) const { return a + b; }
+};
+
+// first arg-max over one axis (lowest index wins ties); one-time use, shuffles are fine
+template <int KP, bool INNER>
 __device__ __forceinline__ void allargmax(float& v, int& a) {
 #pragma unroll
-  for (int o = OUTER ? KP : 1; o < (OUTER ? KP * KP : KP); o <<= 1) {
+  for (int o = INNER ? 1 : KP; o < (INNER ? KP : KP * KP); o <<= 1) {
     const float ov = __shfl_xor(v, o);
     const int oa = __shfl_xor(a, o);
     if (ov > v || (ov == v && oa < a)) { v = ov; a = oa; }
   }
 }
-// log-sum-exp over the reduction axis; all -inf -> -inf
-template <int KP, bool OUTER>
-__device__ __forceinline__ float alllse(float v) {
-  const float m = allmax<KP, OUTER>(v);
-  if (m == NEG_INF) return NEG_INF;
-  const float s = allsum<KP, OUTER>(__expf(v - m));
-  return m + __logf(s);
+
+// ---------------------------------------------------------------- table staging
+// Chunk c of the wave's SPW sequences (b0 .. b0 + SPW - 1, clamped to B - 1)
+// into one ring slot: [SPW][HC][K][K] log_A then [SPW][HC][K] em.  Steps past
+// T read clamped (valid, unused) addresses.
+template <int K, bool W16>
+__device__ __forceinline__ void stage_chunk(const float* __restrict__ A, const float* __restrict__ E, int64_t b0,
+                                            int64_t B, int T, int c, float* slot, int lane) {
+  using Gm = Geo<K, W16>;
+  using Rg = Ring<K, W16>;
+  constexpr int U = Rg::U;
+#pragma unroll
+  for (int q = 0; q < Rg::NI; ++q) {
+    const int f = (q * 64 + lane) * U;
+    auto a_src = [&]() {
+      const int sq = f / Gm::AS, off = f - sq * Gm::AS;
+      const int64_t b = b0 + sq < B ? b0 + sq : B - 1;
+      int64_t o = (int64_t)c * Gm::AS + off;
+      const int64_t lim = (int64_t)T * K * K - U;
+      o = o < lim ? o : lim;
+      return A + b * (int64_t)T * K * K + o;
+    };
+    auto e_src = [&]() {
+      const int fe = f - Gm::SPW * Gm::AS;
+      const int sq = fe / Gm::ES, off = fe - sq * Gm::ES;
+      const int64_t b = b0 + sq < B ? b0 + sq : B - 1;
+      int64_t o = (int64_t)c * Gm::ES + off;
+      const int64_t lim = (int64_t)T * K - U;
+      o = o < lim ? o : lim;
+      return E + b * (int64_t)T * K + o;
+    };
+    const float* src;
+    if ((q + 1) * 64 * U <= Gm::SPW * Gm::AS) src = a_src();        // whole instruction in log_A
+    else if (q * 64 * U >= Gm::SPW * Gm::AS) src = e_src();         // whole instruction in em
+    else src = f < Gm::SPW * Gm::AS ? a_src() : e_src();
+    auto* dst = (__attribute__((address_space(3))) void*)(slot + q * 64 * U);
+    if constexpr (W16) __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
+    else __builtin_amdgcn_global_load_lds(src, dst, 4, 0, 0);
+  }
 }
 
-// ------------------------------------------------------------------ Viterbi
-// LDS: backpointers bp[seq_in_wave][t][j] (uint8) when they fit, else global ws.
-template <int KP, bool BP_LDS>
+// per-lane LDS offsets of the (i, j) entry / emission j for both step parities
+template <int K, bool W16>
+struct LaneMap {
+  int a_off[2], e_off[2];
+  bool a_ok[2], e_ok[2];
+  __device__ LaneMap(int grp, int g) {
+    using Gm = Geo<K, W16>;
+    constexpr int KP = Gm::KP;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {  // p = 0: even t (outer), 1: odd t (inner)
+      const int i = p == 0 ? g / KP : g % KP;
+      const int j = p == 0 ? g % KP : g / KP;
+      a_ok[p] = i < K && j < K;
+      e_ok[p] = j < K;
+      a_off[p] = grp * Gm::AS + (a_ok[p] ? i * K + j : 0);
+      e_off[p] = Gm::SPW * Gm::AS + grp * Gm::ES + (e_ok[p] ? j : 0);
+    }
+  }
+};
+
+// --------------------------------------------------------------------- Viterbi
+// bp map of one step for one sequence: byte j = lowest i with (v == max) at (i, j).
+template <int KP>
+__device__ __forceinline__ uint64_t transpose_bits(uint64_t x) {  // bit r*KP + c <-> c*KP + r
+  if constexpr (KP == 8) {
+    uint64_t t;
+    t = (x ^ (x >> 7)) & 0x00AA00AA00AA00AAull; x ^= t ^ (t << 7);
+    t = (x ^ (x >> 14)) & 0x0000CCCC0000CCCCull; x ^= t ^ (t << 14);
+    t = (x ^ (x >> 28)) & 0x00000000F0F0F0F0ull; x ^= t ^ (t << 28);
+  } else if constexpr (KP == 4) {
+    uint64_t t;
+    t = (x ^ (x >> 3)) & 0x0A0Aull; x ^= t ^ (t << 3);
+    t = (x ^ (x >> 6)) & 0x00CCull; x ^= t ^ (t << 6);
+  } else {
+    const uint64_t t = (x ^ (x >> 1)) & 0x2ull;
+    x ^= t ^ (t << 1);
+  }
+  return x;
+}
+
+template <int K>
+__device__ __forceinline__ uint2 bp_map(uint32_t mlo, uint32_t mhi, int q, bool odd) {
+  using Gm = Geo<K, false>;
+  constexpr int KP = Gm::KP, G = Gm::G;
+  uint64_t f = ((uint64_t)mhi << 32) | mlo;
+  if constexpr (G < 64) f = (f >> (q * G)) & ((1ull << G) - 1);
+  // odd t (inner map): bit g = j*KP + i, row j = the i's -> no transpose
+  if (!odd) f = transpose_bits<KP>(f);
+  uint32_t w[2] = {0u, 0u};
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const uint32_t row = (uint32_t)(f >> (j * KP)) & ((1u << KP) - 1);
+    const uint32_t bj = (uint32_t)__builtin_ctz(row | (1u << KP)) & (KP - 1);
+    w[j >> 2] |= bj << (8 * (j & 3));
+  }
+  return make_uint2(w[0], w[1]);
+}
+
+// lo[LANE] = bal[31:0], hi[LANE] = bal[63:32].  The s_nop covers the
+// "VALU writes SGPR -> v_writelane reads it" hazard (the ballot's v_cmp may
+// immediately precede; hipcc does not look inside inline asm).
+template <int LANE>
+__device__ __forceinline__ void writelane_pair(uint32_t& lo, uint32_t& hi, uint64_t bal) {
+  asm("s_nop 4\n\tv_writelane_b32 %0, %2, %4\n\tv_writelane_b32 %1, %3, %4"
+      : "+v"(lo), "+v"(hi)
+      : "s"((uint32_t)bal), "s"((uint32_t)(bal >> 32)), "i"(LANE));
+}
+
+__device__ __forceinline__ uint32_t perm_bytes(uint2 m, uint32_t sel) {
+  return __builtin_amdgcn_perm(m.y, m.x, sel);
+}
+
+template <int K, bool W16>
 __global__ __launch_bounds__(64) void viterbi_kernel(const float* __restrict__ log_pi, const float* __restrict__ log_A,
-                                                     const float* __restrict__ em, const int64_t* __restrict__ lengths,
-                                                     int64_t B, int T, int K, int32_t* __restrict__ path,
-                                                     float* __restrict__ score, uint8_t* __restrict__ bp_ws) {
-  constexpr int G = KP * KP, SPW = 64 / G;
-  extern __shared__ uint8_t bps[];
-  const int lane = threadIdx.x;
-  const int grp = lane / G, g = lane % G;
-  const int64_t b = (int64_t)blockIdx.x * SPW + grp;
+                                                     const float* __restrict__ em,
+                                                     const int64_t* __restrict__ lengths, int64_t B, int T,
+                                                     int32_t* __restrict__ path, float* __restrict__ score,
+                                                     uint2* __restrict__ masks) {
+  using Gm = Geo<K, W16>;
+  using Rg = Ring<K, W16>;
+  constexpr int KP = Gm::KP, G = Gm::G, SPW = Gm::SPW, R = Rg::R, HC = Gm::HC;
+  __shared__ float ring[R * Gm::SLOT];  // the only LDS object (keeps hipcc's LDS-DMA waits counted)
+
+  const int lane = threadIdx.x, grp = lane / G, g = lane % G;
+  const int64_t b0 = (int64_t)blockIdx.x * SPW;
+  const int64_t b = b0 + grp;
   const bool live = b < B;
   const int64_t Lr = live ? lengths[b] : 0;
   const int L = (int)(Lr <= 0 ? 0 : (Lr < T ? Lr : T));
-  uint8_t* bp = BP_LDS ? bps + (size_t)grp * T * KP : bp_ws + (size_t)(live ? b : 0) * T * KP;
-  const float* A = log_A + (size_t)(live ? b : 0) * T * K * K;
-  const float* E = em + (size_t)(live ? b : 0) * T * K;
-  // wave-uniform loop bound
+  const int i0 = g % KP;
+  const float lp = i0 < K ? log_pi[i0] : 0.f;
   int Lmax = L;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) Lmax = max(Lmax, __shfl_xor(Lmax, o));
+  Lmax = __builtin_amdgcn_readfirstlane(Lmax);
+  wait_vm<0>();  // ordinary loads retired before the LDS-DMA stream starts
+  const int Tr = (int)cdiv(T, 64) * 64;
+  uint2* wmask = masks + (size_t)blockIdx.x * Tr;
 
-  // step 0 holds delta_0 indexed by the "inner" map's i = g % KP
-  const int i0 = g % KP;
-  float d = (L > 0 && i0 < K) ? log_pi[i0] + E[i0] : NEG_INF;
-  for (int t = 1; t < Lmax; ++t) {
-    const bool outer = (t & 1) == 0;
-    const int i = outer ? g / KP : g % KP;
-    const int j = outer ? g % KP : g / KP;
-    const bool act = t < L;
-    float a = (act && i < K && j < K) ? A[(size_t)t * K * K + i * K + j] : NEG_INF;
-    float v = (i < K) ? d + a : NEG_INF;
-    int arg = i;
-    if (outer) allargmax<KP, true>(v, arg); else allargmax<KP, false>(v, arg);
-    const float ej = (act && j < K) ? E[(size_t)t * K + j] : 0.f;
-    if (act) {
-      d = v + ej;
-      if (i == 0 && j < K) bp[(size_t)t * KP + j] = (uint8_t)arg;
-    }
+  const LaneMap<K, W16> lm(grp, g);
+  const int nchunks = (int)cdiv(Lmax, HC);
+  float d = NEG_INF;
+  if (nchunks > 0) {
+#pragma unroll
+    for (int c = 0; c < R - 1; ++c)
+      stage_chunk<K, W16>(log_A, em, b0, B, T, min(c, nchunks - 1), ring + c * Gm::SLOT, lane);
   }
-  // final argmax over the state axis the lanes currently hold
-  const int tl = L - 1;  // last processed step; its map decides which axis holds the states
-  const bool held_inner = (tl <= 0) || ((tl & 1) == 0);  // even step (or t=0): state = g % KP
-  const int st = held_inner ? g % KP : g / KP;
-  float v = (st < K) ? d : NEG_INF;
-  int arg = st;
-  if (held_inner) allargmax<KP, false>(v, arg); else allargmax<KP, true>(v, arg);
-  if (BP_LDS) __syncthreads(); else __threadfence();
-  // backtrace: one lane per sequence walks the backpointers; lanes stride the path writes
-  int32_t* P = path + (size_t)(live ? b : 0) * T;
-  if (live) {
-    for (int t = L + g; t < T; t += G) P[t] = -1;
-    if (g == 0) {
-      if (L > 0) {
-        score[b] = v;
-        int s = arg;
-        P[L - 1] = s;
-        for (int t = L - 1; t > 0; --t) {
-          s = bp[(size_t)t * KP + s];
-          P[t - 1] = s;
-        }
-      } else {
-        score[b] = NEG_INF;
+  int Lmin = L;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) Lmin = min(Lmin, __shfl_xor(Lmin, o));
+  Lmin = __builtin_amdgcn_readfirstlane(Lmin);
+  uint32_t mlo = 0, mhi = 0;
+  // one chunk of steps: A / em values of the chunk are read from LDS up front
+  // (one wait), then the max-plus chain runs on registers only.  CHECK: some
+  // sequence of the wave ends inside this chunk.
+  auto run_chunk = [&](const float* sl, int t0, bool first, auto check) {
+    constexpr bool CHECK = decltype(check)::value;
+    float av[HC], ev[HC];
+#pragma unroll
+    for (int s = 0; s < HC; ++s) {
+      const int p = s & 1;  // parity of t (t0 even)
+      av[s] = lm.a_ok[p] ? sl[lm.a_off[p] + s * K * K] : NEG_INF;
+      ev[s] = lm.e_ok[p] ? sl[lm.e_off[p] + s * K] : 0.f;
+    }
+    static_for<HC>([&](auto si) {
+      constexpr int s = decltype(si)::value, p = s & 1;
+      if (s == 0 && first) {
+        // delta_0 on the inner axis: lane's i0 = g % KP = the even map's j
+        d = (L > 0 && i0 < K) ? lp + ev[0] : NEG_INF;
+        return;
       }
+      const float v = d + av[s];
+      const float m = p == 0 ? allred<KP, false>(v, OpMax{}) : allred<KP, true>(v, OpMax{});
+      const uint64_t bal = __builtin_amdgcn_ballot_w64(v == m);
+      writelane_pair<s>(mlo, mhi, bal);
+      if (!CHECK || t0 + s < L) d = m + ev[s];
+    });
+  };
+  for (int c = 0; c < nchunks; ++c) {
+    stage_chunk<K, W16>(log_A, em, b0, B, T, min(c + R - 1, nchunks - 1), ring + ((c + R - 1) % R) * Gm::SLOT,
+                        lane);
+    wait_vm<Rg::WAIT>();
+    const float* sl = ring + (c % R) * Gm::SLOT;
+    const int t0 = c * HC;
+    if (t0 + HC <= Lmin) run_chunk(sl, t0, c == 0, std::false_type{});
+    else run_chunk(sl, t0, c == 0, std::true_type{});
+    if (lane < HC) wmask[t0 + lane] = make_uint2(mlo, mhi);  // masks of steps t0 .. t0 + HC - 1
+  }
+
+  // final state: first arg-max over the state axis the lanes hold after step L-1
+  const int tl = L - 1;
+  const bool held_inner = (tl <= 0) || ((tl & 1) == 0);
+  const int st = held_inner ? g % KP : g / KP;
+  float best = (st < K) ? d : NEG_INF;
+  int arg = st;
+  if (held_inner) allargmax<KP, true>(best, arg); else allargmax<KP, false>(best, arg);
+
+  // ---- backtrace, one sequence at a time on all 64 lanes, in windows of WT steps
+  // staged from the mask stream into the (now idle) ring
+  __builtin_amdgcn_s_waitcnt(0);
+  __threadfence_block();
+  constexpr int WT = (R * Gm::SLOT * 4 / 8) / 64 * 64;
+  static_assert(WT >= 64, "ring too small for a mask window");
+  uint2* wl = reinterpret_cast<uint2*>(ring);
+  for (int q = 0; q < SPW; ++q) {
+    const int64_t bq = b0 + q;
+    if (bq >= B) break;
+    const int Lq = __builtin_amdgcn_readlane(L, q * G);
+    const int sq = __builtin_amdgcn_readlane(arg, q * G);
+    const float scq = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, best), q * G));
+    int32_t* P = path + bq * (int64_t)T;
+    for (int t = max(Lq, 0) + lane; t < T; t += 64) P[t] = -1;
+    if (lane == 0) score[bq] = Lq > 0 ? scq : NEG_INF;
+    if (Lq <= 0) continue;
+    if (lane == 0 && Lq == 1) P[0] = sq;
+    int state = sq;  // state at the top step of the current window (wave-uniform)
+    // mask steps 1 .. Lq-1; windows [w0, w0 + WT) from the top down
+    for (int w0 = ((Lq - 1) / WT) * WT; Lq > 1 && w0 >= 0; w0 -= WT) {
+      const int lo = max(w0, 1), hi = min(w0 + WT - 1, Lq - 1);
+      // stage masks [w0, w0 + WT) (whole 64-step blocks)
+      __syncthreads();
+      const int nblk = (hi - w0) / 64 + 1;
+      for (int k = 0; k < 2 * nblk; ++k)  // 64 dwords per instruction
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint32_t*>(wmask + w0) + k * 64 + lane,
+                                         (__attribute__((address_space(3))) void*)(reinterpret_cast<uint32_t*>(wl) +
+                                                                                   k * 64),
+                                         4, 0, 0);
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+      const int n = hi - lo + 1;
+      const int cl = (int)cdiv(n, 64);
+      const int clo = lo + lane * cl, chi = min(clo + cl - 1, hi);
+      // compose this lane's slice: F maps the state at step chi to the state at step clo - 1
+      uint32_t flo = 0x03020100u, fhi = 0x07060504u;
+      for (int t = chi; t >= clo; --t) {
+        const uint2 mm = wl[t - w0];
+        const uint2 mp = bp_map<K>(mm.x, mm.y, q, t & 1);
+        flo = perm_bytes(mp, flo);
+        fhi = perm_bytes(mp, fhi);
+      }
+      // serial resolve from the top slice down: end state of each slice
+      int ecur = state, mine = 0;
+      for (int cc = 63; cc >= 0; --cc) {
+        const int slo = lo + cc * cl;
+        if (slo > hi) continue;
+        mine = lane == cc ? ecur : mine;
+        const uint32_t xl = __builtin_amdgcn_readlane((int)flo, cc), xh = __builtin_amdgcn_readlane((int)fhi, cc);
+        ecur = (int)((ecur < 4 ? (xl >> (8 * ecur)) : (xh >> (8 * (ecur - 4)))) & 0xFFu);
+      }
+      // walk: P[t] for t in [clo, chi]; the lowest slice also writes P[lo - 1]
+      int s = mine;
+      for (int t = chi; t >= clo; --t) {
+        P[t] = s;
+        const uint2 mm = wl[t - w0];
+        const uint2 mp = bp_map<K>(mm.x, mm.y, q, t & 1);
+        s = (int)((s < 4 ? (mp.x >> (8 * s)) : (mp.y >> (8 * (s - 4)))) & 0xFFu);
+      }
+      if (clo == lo && clo <= chi) P[lo - 1] = s;
+      state = ecur;
     }
   }
 }
 
 size_t viterbi_ws_bytes(int64_t B, int64_t T, int64_t K) {
+  if (K < 1 || K > 8) return 0;
   const int KP = K <= 2 ? 2 : K <= 4 ? 4 : 8;
-  const size_t lds = (size_t)(64 / (KP * KP)) * T * KP;
-  return lds <= 64 * 1024 ? 0 : (size_t)B * T * KP;
+  const int64_t spw = 64 / (KP * KP);
+  return (size_t)cdiv(B, spw) * (size_t)cdiv(T, 64) * 64 * 8;
 }
+
+template <int K, bool W16>
+static void viterbi_go(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths, int64_t B,
+                       int64_t T, int32_t* path, float* score, void* ws, hipStream_t s) {
+  const dim3 grid((unsigned)cdiv(B, Geo<K, W16>::SPW));
+  viterbi_kernel<K, W16><<<grid, 64, 0, s>>>(log_pi, log_A, em, lengths, B, (int)T, path, score, (uint2*)ws);
+}
+
+static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 int launch_viterbi(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths, int64_t B,
                    int64_t T, int64_t K, int32_t* path, float* score, void* ws, size_t ws_bytes, hipStream_t s) {
   if (B == 0) return VQHMM_OK;
-  if (K < 1 || K > 8 || T < 1 || T > INT32_MAX) return VQHMM_EUNSUPPORTED;
-  const int KP = K <= 2 ? 2 : K <= 4 ? 4 : 8;
-  const int spw = 64 / (KP * KP);
-  const size_t lds = (size_t)spw * T * KP;
-  const bool in_lds = lds <= 64 * 1024;
-  if (!in_lds && ws_bytes < (size_t)B * T * KP) return VQHMM_EWORKSPACE;
-  const dim3 grid((unsigned)cdiv(B, spw));
-  uint8_t* bw = (uint8_t*)ws;
-#define VQHMM_VIT(KPV)                                                                                         \
-  if (in_lds)                                                                                                  \
-    viterbi_kernel<KPV, true><<<grid, 64, lds, s>>>(log_pi, log_A, em, lengths, B, (int)T, (int)K, path, score, \
-                                                    bw);                                                       \
-  else                                                                                                         \
-    viterbi_kernel<KPV, false><<<grid, 64, 0, s>>>(log_pi, log_A, em, lengths, B, (int)T, (int)K, path, score, bw);
-  if (KP == 2) { VQHMM_VIT(2) } else if (KP == 4) { VQHMM_VIT(4) } else { VQHMM_VIT(8) }
-#undef VQHMM_VIT
+  if (K < 1 || K > 8 || T < 1 || T > (1 << 28)) return VQHMM_EUNSUPPORTED;
+  if (!ws || ws_bytes < viterbi_ws_bytes(B, T, K)) return VQHMM_EWORKSPACE;
+  const bool w16 = aligned16(log_A) && aligned16(em);
+  switch (K) {
+    case 1: viterbi_go<1, false>(log_pi, log_A, em, lengths, B, T, path, score, ws, s); break;
+    case 2: viterbi_go<2, false>(log_pi, log_A, em, lengths, B, T, path, score, ws, s); break;
+    case 3: viterbi_go<3, false>(log_pi, log_A, em, lengths, B, T, path, score, ws, s); break;
+    case 4:
+      if (w16) viterbi_go<4, true>(log_pi, log_A, em, lengths, B, T, path, score, ws, s);
+      else viterbi_go<4, false>(log_pi, log_A, em, lengths, B, T, path, score, ws, s);
+      break;
+    case 5: viterbi_go<5, false>(log_pi, log_A, em, lengths, B, T, path, score, ws, s); break;
+    case 6: viterbi_go<6, false>(log_pi, log_A, em, lengths, B, T, path, score, ws, s); break;
+    case 7: viterbi_go<7, false>(log_pi, log_A, em, lengths, B, T, path, score, ws, s); break;
+    default:
+      if (w16) viterbi_go<8, true>(log_pi, log_A, em, lengths, B, T, path, score, ws, s);
+      else viterbi_go<8, false>(log_pi, log_A, em, lengths, B, T, path, score, ws, s);
+      break;
+  }
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
 }
 
-// ---------------------------------------------------------- forward-backward
-// Pass 1 (alpha, t ascending) stores the max-normalised alpha_t in ws and the
-// accumulated normaliser; pass 2 (beta, t descending) forms gamma_t =
-// softmax_j(alpha_t + beta_t) and writes it.  Both passes are in one launch
-// (same wave, same sequence), so the alpha tile is re-read from L2.
-template <int KP>
-__global__ __launch_bounds__(64) void fwdbwd_kernel(const float* __restrict__ log_pi, const float* __restrict__ log_A,
-                                                    const float* __restrict__ em, const int64_t* __restrict__ lengths,
-                                                    int64_t B, int T, int K, float* __restrict__ gamma,
-                                                    float* __restrict__ logZ, float* __restrict__ alpha_ws) {
-  constexpr int G = KP * KP, SPW = 64 / G;
-  const int lane = threadIdx.x;
-  const int grp = lane / G, g = lane % G;
-  const int64_t b = (int64_t)blockIdx.x * SPW + grp;
+
+// ------------------------------------------------------------ forward-backward
+// One workgroup = 2 waves on the same SPW sequences: wave 0 runs alpha (t
+// ascending) and wave 1 beta (t descending) at the same time, each streaming
+// the tables through its own ring; both stage their per-step vectors in LDS and
+// flush one chunk at a time to the workspace; then both waves form gamma in
+// parallel over t (no serial dependency left).
+//   alpha: al_0 = log_pi + e_0;
+//          al_t(j) = (LSE_i(al_{t-1}(i) + A_t(i,j)) + e_t(j)) - mu_{t-1},
+//          mu_{t-1} = max_i al_{t-1}(i) (reduced off the chain while step t runs),
+//          S += mu (fp64)  ->  logZ = S + LSE_j al_{L-1}(j)
+//   beta:  be_{L-1} = 0;
+//          be_t(i) = LSE_j((A_{t+1}(i,j) + e_{t+1}(j)) + be_{t+1}(j)) - nu,
+//          nu = max_j be_{t+1}(j)
+//   gamma_t(i) = softmax_i(al_t(i) + be_t(i))
+// The per-step shifts are arbitrary constants of a shift-invariant recursion;
+// these keep every stored vector within one step's increment of 0.
+// Workspace: al [B][T][K], then be' [B][T][K] with be'[t+1] = be_t.
+constexpr float F32_LOWEST = -3.402823466e38f;
+
+template <int K, bool W16>
+__global__ __launch_bounds__(128) void fwdbwd_kernel(const float* __restrict__ log_pi,
+                                                     const float* __restrict__ log_A, const float* __restrict__ em,
+                                                     const int64_t* __restrict__ lengths, int64_t B, int T,
+                                                     float* __restrict__ gamma, float* __restrict__ logZ,
+                                                     float* __restrict__ ws) {
+  using Gm = Geo<K, W16>;
+  using Rg = Ring<K, W16>;
+  constexpr int KP = Gm::KP, G = Gm::G, SPW = Gm::SPW, R = Rg::R, HC = Gm::HC;
+  constexpr int VB = SPW * HC * K;        // per-wave vector buffer (floats)
+  constexpr int PW = R * Gm::SLOT + VB;   // LDS floats per wave
+  __shared__ float lds[2 * PW];           // the only LDS object
+
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, grp = lane / G, g = lane % G;
+  const int64_t b0 = (int64_t)blockIdx.x * SPW;
+  const int64_t b = b0 + grp;
   const bool live = b < B;
   const int64_t Lr = live ? lengths[b] : 0;
   const int L = (int)(Lr <= 0 ? 0 : (Lr < T ? Lr : T));
-  const size_t bo = (size_t)(live ? b : 0);
-  const float* A = log_A + bo * T * K * K;
-  const float* E = em + bo * T * K;
-  float* AL = alpha_ws + bo * T * K;
-  float* GA = gamma + bo * T * K;
+  const int i0 = g % KP;
+  const float lp = i0 < K ? log_pi[i0] : 0.f;
   int Lmax = L;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) Lmax = max(Lmax, __shfl_xor(Lmax, o));
+  Lmax = __builtin_amdgcn_readfirstlane(Lmax);
+  wait_vm<0>();
+  float* ring = lds + wave * PW;
+  float* vbuf = ring + R * Gm::SLOT;
+  float* ws_al = ws;
+  float* ws_be = ws + (size_t)B * T * K;
+  const LaneMap<K, W16> lm(grp, g);
+  const int nchunks = (int)cdiv(Lmax, HC);
 
-  // ---- alpha pass.  After step t the lanes hold alpha_t(state) with state = g % KP
-  // for even t (inner axis) and g / KP for odd t (outer axis).
-  const int i0 = g % KP;
-  float al = (L > 0 && i0 < K) ? log_pi[i0] + E[i0] : NEG_INF;
-  float c = 0.f;  // sum of normalisers
-  if (L > 0) {
-    const float m = allmax<KP, false>(al);  // state on the inner axis at t = 0
-    al -= m;
-    c += m;
-    if (g / KP == 0 && i0 < K) AL[i0] = al;
-  }
-  for (int t = 1; t < Lmax; ++t) {
-    const bool outer = (t & 1) == 0;
-    const int i = outer ? g / KP : g % KP;
-    const int j = outer ? g % KP : g / KP;
-    const bool act = t < L;
-    const float a = (act && i < K && j < K) ? A[(size_t)t * K * K + i * K + j] : NEG_INF;
-    float v = (i < K) ? al + a : NEG_INF;
-    v = outer ? alllse<KP, true>(v) : alllse<KP, false>(v);
-    v += (act && j < K) ? E[(size_t)t * K + j] : 0.f;
-    if (j >= K) v = NEG_INF;
-    // normalise over the states j (the other axis)
-    const float m = outer ? allmax<KP, false>(v) : allmax<KP, true>(v);
-    if (act) {
-      al = v - m;
-      c += m;
-      if (i == 0 && j < K) AL[(size_t)t * K + j] = al;
+  // flush vbuf -> dst rows [t0, t0 + HC) of the wave's sequences (t < T only)
+  auto flush = [&](float* dst, int t0) {
+    constexpr int NF = (VB + 63) / 64;
+#pragma unroll
+    for (int k = 0; k < NF; ++k) {
+      const int idx = k * 64 + lane;
+      if (VB % 64 == 0 || idx < VB) {
+        const int q = idx / (HC * K), r = idx - q * (HC * K), s = r / K;
+        const float v = vbuf[idx];
+        if (b0 + q < B && t0 + s < T) dst[((b0 + q) * (int64_t)T + t0) * K + r] = v;
+      }
     }
-  }
-  // logZ = c + LSE_j alpha_{L-1}(j): the states sit on the inner axis if L-1 is even
-  {
+  };
+
+  if (wave == 0) {
+    // ------------------------------------------------------------ alpha
+    if (nchunks > 0) {
+#pragma unroll
+      for (int c = 0; c < R - 1; ++c)
+        stage_chunk<K, W16>(log_A, em, b0, B, T, min(c, nchunks - 1), ring + c * Gm::SLOT, lane);
+    }
+    float al = NEG_INF;
+    double S = 0.0;
+    for (int c = 0; c < nchunks; ++c) {
+      stage_chunk<K, W16>(log_A, em, b0, B, T, min(c + R - 1, nchunks - 1), ring + ((c + R - 1) % R) * Gm::SLOT,
+                          lane);
+      wait_vm<Rg::WAIT>();
+      const float* sl = ring + (c % R) * Gm::SLOT;
+      const int t0 = c * HC;
+#pragma unroll
+      for (int s = 0; s < HC; ++s) {
+        const int p = s & 1;
+        const int t = t0 + s;
+        float a = sl[lm.a_off[p] + s * K * K];
+        a = lm.a_ok[p] ? a : NEG_INF;
+        float e = sl[lm.e_off[p] + s * K];
+        e = lm.e_ok[p] ? e : 0.f;
+        if (s == 0 && c == 0) {
+          al = (L > 0 && i0 < K) ? lp + e : NEG_INF;
+          if (g < KP && g < K) vbuf[grp * HC * K + g] = al;
+          continue;
+        }
+        const float v = al + a;
+        float m, mu, sm;
+        if (p == 0) {
+          m = allred<KP, false>(v, OpMax{});
+          mu = allred<KP, false>(al, OpMax{});
+        } else {
+          m = allred<KP, true>(v, OpMax{});
+          mu = allred<KP, true>(al, OpMax{});
+        }
+        const float mm = fmaxf(m, F32_LOWEST);
+        const float x = __expf(v - mm);
+        sm = p == 0 ? allred<KP, false>(x, OpAdd{}) : allred<KP, true>(x, OpAdd{});
+        const float r = (mm + __logf(sm)) + e;
+        const float mus = mu == NEG_INF ? 0.f : mu;
+        if (t < L) {
+          al = r - mus;
+          S += (double)mus;
+        }
+        // lanes with i-coordinate 0 hold state j's value once each
+        const bool wr = p == 0 ? (g < KP) : (g % KP == 0);
+        const int js = p == 0 ? g : g / KP;
+        if (wr && js < K) vbuf[grp * HC * K + s * K + js] = al;
+      }
+      flush(ws_al, t0);
+    }
+    // logZ = S + LSE over the state axis held after step L-1
     const int tl = L - 1;
-    const bool inner = (tl <= 0) || ((tl & 1) == 0);
-    const int st = inner ? g % KP : g / KP;
-    float v = (st < K) ? al : NEG_INF;
-    v = inner ? alllse<KP, false>(v) : alllse<KP, true>(v);
-    if (live && g == 0) logZ[b] = L > 0 ? c + v : __builtin_nanf("");
-  }
-  __threadfence_block();
-  // ---- beta pass (t descending); beta_{L-1} = 0.  The backward map mirrors the
-  // forward one: at step t (computing beta_t from beta_{t+1}) the reduction is
-  // over j; lanes hold beta_t(i) afterwards.  We use: step t even -> i = g / KP
-  // (outer), j = g % KP, reduce over j = inner axis; t odd -> i = g % KP, j = g / KP,
-  // reduce over the outer axis.  beta_{t+1} must then be held by state index j:
-  // for even t, j = g % KP = inner — beta_{t+1} (t+1 odd) was produced as
-  // beta(i = g % KP) held on the inner axis  (consistent); similarly for odd t.
-  // Initial beta_{L-1} = 0 everywhere (any axis).
-  for (int k = g; k < (T - L) * K; k += G)
-    if (live) GA[(size_t)L * K + k] = 0.f;  // gamma beyond the length
-  float be = 0.f;
-  for (int t = Lmax - 1; t >= 0; --t) {
-    const bool act = t < L;
-    const bool even = (t & 1) == 0;
-    const int i = even ? g / KP : g % KP;
-    const int j = even ? g % KP : g / KP;
-    float bnew = 0.f;
-    if (t < L - 1) {
-      // beta_t(i) = LSE_j (log_A[t+1, i, j] + e_{t+1}(j) + beta_{t+1}(j))
-      const float a = (i < K && j < K) ? A[(size_t)(t + 1) * K * K + i * K + j] : NEG_INF;
-      const float e = (j < K) ? E[(size_t)(t + 1) * K + j] : 0.f;
-      float v = (j < K) ? a + e + be : NEG_INF;
-      v = even ? alllse<KP, false>(v) : alllse<KP, true>(v);
-      if (i >= K) v = NEG_INF;
-      const float m = even ? allmax<KP, true>(v) : allmax<KP, false>(v);  // over states i
-      bnew = v - m;
-    } else {
-      // butterflies stay inside a sequence's lane group, so groups may diverge here
-      bnew = (i < K) ? 0.f : NEG_INF;
+    const bool held_inner = (tl <= 0) || ((tl & 1) == 0);
+    const int st = held_inner ? g % KP : g / KP;
+    const float x0 = st < K ? al : NEG_INF;
+    const float mx = held_inner ? allred<KP, true>(x0, OpMax{}) : allred<KP, false>(x0, OpMax{});
+    const float mxs = fmaxf(mx, F32_LOWEST);
+    const float ex = __expf(x0 - mxs);
+    const float sx = held_inner ? allred<KP, true>(ex, OpAdd{}) : allred<KP, false>(ex, OpAdd{});
+    if (live && g == 0) logZ[b] = L > 0 ? (float)(S + (double)(mxs + __logf(sx))) : __builtin_bit_cast(float, 0x7fc00000u);
+  } else {
+    // ------------------------------------------------------------ beta
+    // chunk k holds data steps [k HC, k HC + HC); data step d serves beta step t = d - 1
+    if (nchunks > 0) {
+#pragma unroll
+      for (int c = 0; c < R - 1; ++c)
+        stage_chunk<K, W16>(log_A, em, b0, B, T, max(nchunks - 1 - c, 0), ring + c * Gm::SLOT, lane);
     }
-    // gamma_t(i) = softmax_i(alpha_t(i) + beta_t(i)) over the state axis (outer if even)
-    const float alv = (act && i < K) ? AL[(size_t)t * K + i] : NEG_INF;
-    float sv = (act && i < K) ? alv + bnew : NEG_INF;
-    const float mx = even ? allmax<KP, true>(sv) : allmax<KP, false>(sv);
-    const float ex = (act && i < K && mx != NEG_INF) ? __expf(sv - mx) : 0.f;
-    const float sm = even ? allsum<KP, true>(ex) : allsum<KP, false>(ex);
-    if (act) {
-      be = bnew;
-      if (j == 0 && i < K) GA[(size_t)t * K + i] = ex / sm;
+    float be = 0.f;
+    for (int c = 0; c < nchunks; ++c) {
+      const int k = nchunks - 1 - c;
+      stage_chunk<K, W16>(log_A, em, b0, B, T, max(k - (R - 1), 0), ring + ((c + R - 1) % R) * Gm::SLOT, lane);
+      wait_vm<Rg::WAIT>();
+      const float* sl = ring + (c % R) * Gm::SLOT;
+      const int d0 = k * HC;
+#pragma unroll
+      for (int s = HC - 1; s >= 0; --s) {
+        const int t = d0 + s - 1;
+        if (s == 0 && k == 0) continue;  // t = -1
+        const int p = (s + 1) & 1;       // parity of t
+        float a = sl[lm.a_off[p] + s * K * K];
+        a = lm.a_ok[p] ? a : NEG_INF;
+        float e = sl[lm.e_off[p] + s * K];
+        e = lm.e_ok[p] ? e : 0.f;
+        const float v = (a + e) + be;
+        float m, nu, sm;
+        if (p == 0) {  // reduce over j = g % KP
+          m = allred<KP, true>(v, OpMax{});
+          nu = allred<KP, true>(be, OpMax{});
+        } else {
+          m = allred<KP, false>(v, OpMax{});
+          nu = allred<KP, false>(be, OpMax{});
+        }
+        const float mm = fmaxf(m, F32_LOWEST);
+        const float x = __expf(v - mm);
+        sm = p == 0 ? allred<KP, true>(x, OpAdd{}) : allred<KP, false>(x, OpAdd{});
+        const float r = mm + __logf(sm);
+        const float nus = nu == NEG_INF ? 0.f : nu;
+        if (t < L - 1) be = r - nus;
+        // lanes with j-coordinate 0 hold state i's value once each; slot s <-> be'[t + 1]
+        const bool wr = p == 0 ? (g % KP == 0) : (g < KP);
+        const int is = p == 0 ? g / KP : g;
+        if (wr && is < K) vbuf[grp * HC * K + s * K + is] = be;
+      }
+      flush(ws_be, d0);
+    }
+  }
+
+  // ---------------------------------------------------------------- gamma
+  __syncthreads();
+  for (int q = 0; q < SPW; ++q) {
+    const int64_t bq = b0 + q;
+    if (bq >= B) break;
+    const int64_t Lq0 = lengths[bq];
+    const int Lq = (int)(Lq0 <= 0 ? 0 : (Lq0 < T ? Lq0 : T));
+    for (int t = threadIdx.x; t < T; t += 128) {
+      float* gq = gamma + (bq * (int64_t)T + t) * K;
+      if (t >= Lq) {
+#pragma unroll
+        for (int i = 0; i < K; ++i) gq[i] = 0.f;
+        continue;
+      }
+      const float* aq = ws_al + (bq * (int64_t)T + t) * K;
+      const float* bb = ws_be + (bq * (int64_t)T + t + 1) * K;
+      float x[K];
+      float mx = NEG_INF;
+#pragma unroll
+      for (int i = 0; i < K; ++i) {
+        x[i] = aq[i] + (t < Lq - 1 ? bb[i] : 0.f);
+        mx = fmaxf(mx, x[i]);
+      }
+      float sm = 0.f;
+#pragma unroll
+      for (int i = 0; i < K; ++i) {
+        x[i] = mx == NEG_INF ? 0.f : __expf(x[i] - mx);
+        sm += x[i];
+      }
+#pragma unroll
+      for (int i = 0; i < K; ++i) gq[i] = x[i] / sm;
     }
   }
 }
 
+template <int K, bool W16>
+static void fwdbwd_go(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths, int64_t B,
+                      int64_t T, float* gamma, float* logZ, float* ws, hipStream_t s) {
+  const dim3 grid((unsigned)cdiv(B, Geo<K, W16>::SPW));
+  fwdbwd_kernel<K, W16><<<grid, 128, 0, s>>>(log_pi, log_A, em, lengths, B, (int)T, gamma, logZ, ws);
+}
+
+size_t fwdbwd_ws_bytes(int64_t B, int64_t T, int64_t K) { return 2 * (size_t)B * T * K * sizeof(float); }
+
 int launch_fwdbwd(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths, int64_t B,
                   int64_t T, int64_t K, float* gamma, float* logZ, void* ws, size_t ws_bytes, hipStream_t s) {
   if (B == 0) return VQHMM_OK;
-  if (K < 1 || K > 8 || T < 1 || T > INT32_MAX) return VQHMM_EUNSUPPORTED;
-  if (ws_bytes < (size_t)B * T * K * sizeof(float)) return VQHMM_EWORKSPACE;
-  const int KP = K <= 2 ? 2 : K <= 4 ? 4 : 8;
-  const int spw = 64 / (KP * KP);
-  const dim3 grid((unsigned)cdiv(B, spw));
-  float* aw = (float*)ws;
-  if (KP == 2)
-    fwdbwd_kernel<2><<<grid, 64, 0, s>>>(log_pi, log_A, em, lengths, B, (int)T, (int)K, gamma, logZ, aw);
-  else if (KP == 4)
-    fwdbwd_kernel<4><<<grid, 64, 0, s>>>(log_pi, log_A, em, lengths, B, (int)T, (int)K, gamma, logZ, aw);
-  else
-    fwdbwd_kernel<8><<<grid, 64, 0, s>>>(log_pi, log_A, em, lengths, B, (int)T, (int)K, gamma, logZ, aw);
+  if (K < 1 || K > 8 || T < 1 || T > (1 << 28)) return VQHMM_EUNSUPPORTED;
+  if (!ws || ws_bytes < fwdbwd_ws_bytes(B, T, K)) return VQHMM_EWORKSPACE;
+  const bool w16 = aligned16(log_A) && aligned16(em);
+  float* w = (float*)ws;
+  switch (K) {
+    case 1: fwdbwd_go<1, false>(log_pi, log_A, em, lengths, B, T, gamma, logZ, w, s); break;
+    case 2: fwdbwd_go<2, false>(log_pi, log_A, em, lengths, B, T, gamma, logZ, w, s); break;
+    case 3: fwdbwd_go<3, false>(log_pi, log_A, em, lengths, B, T, gamma, logZ, w, s); break;
+    case 4:
+      if (w16) fwdbwd_go<4, true>(log_pi, log_A, em, lengths, B, T, gamma, logZ, w, s);
+      else fwdbwd_go<4, false>(log_pi, log_A, em, lengths, B, T, gamma, logZ, w, s);
+      break;
+    case 5: fwdbwd_go<5, false>(log_pi, log_A, em, lengths, B, T, gamma, logZ, w, s); break;
+    case 6: fwdbwd_go<6, false>(log_pi, log_A, em, lengths, B, T, gamma, logZ, w, s); break;
+    case 7: fwdbwd_go<7, false>(log_pi, log_A, em, lengths, B, T, gamma, logZ, w, s); break;
+    default:
+      if (w16) fwdbwd_go<8, true>(log_pi, log_A, em, lengths, B, T, gamma, logZ, w, s);
+      else fwdbwd_go<8, false>(log_pi, log_A, em, lengths, B, T, gamma, logZ, w, s);
+      break;
+  }
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
 }

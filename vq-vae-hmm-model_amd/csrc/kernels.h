@@ -144,6 +144,7 @@ int launch_log_prior_grad(const float* q0sum, const float* log_prior, int K, flo
 int launch_to_pcl(const float* src, int C, int64_t B, int T, int64_t sc, int64_t st, float* dst, hipStream_t s);
 int launch_log_softmax_vec(const float* x, int K, float* out, hipStream_t s);
 size_t viterbi_ws_bytes(int64_t B, int64_t T, int64_t K);
+size_t fwdbwd_ws_bytes(int64_t B, int64_t T, int64_t K);
 int launch_viterbi(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths, int64_t B,
                    int64_t T, int64_t K, int32_t* path, float* score, void* ws, size_t ws_bytes, hipStream_t s);
 int launch_fwdbwd(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths, int64_t B,
