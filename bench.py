@@ -56,6 +56,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--profile-steps", type=int, default=5)
+    ap.add_argument("--no-hmm", action="store_true", help="skip the Viterbi / forward-backward kernel lines")
     return ap.parse_args()
 
 
@@ -130,6 +131,56 @@ def vq_cfg3(lib):
             "traffic": traffic_for("vq_argmin", "vq_cfg3"), "shape": "B2048 Dv64 T200 K32"}
 
 
+def hmm_kernels(lib):
+    """Viterbi at the cfg5 per-GPU shard (K=8, T=4096, 1024 sequences = 8192 / 8 GPUs) and
+    forward-backward at the cfg4 per-GPU shard (K=8, T=512, 512 sequences = 4096 / 8), HBM roofline.
+    Tables are log_softmax(N(0,1)) over the last dim."""
+    from vqhmm import _ext
+    out = {}
+    sp = _ext.stream_ptr()
+    for name, (B, T, K) in (("viterbi_cfg5", (1024, 4096, 8)), ("fwdbwd_cfg4", (512, 512, 8))):
+        g = torch.Generator(device="cuda").manual_seed(7)
+        log_pi = torch.log_softmax(torch.randn(K, device="cuda", generator=g), -1)
+        log_A = torch.log_softmax(torch.randn(B, T, K, K, device="cuda", generator=g), -1)
+        em = torch.log_softmax(torch.randn(B, T, K, device="cuda", generator=g), -1)
+        L = torch.full((B,), T, dtype=torch.int64, device="cuda")
+        P = _ext.ptr
+        if name.startswith("viterbi"):
+            path = torch.empty(B, T, dtype=torch.int32, device="cuda")
+            score = torch.empty(B, device="cuda")
+            nb = lib.vqhmm_viterbi_workspace_size(B, T, K)
+            ws = torch.empty(max(nb, 1), dtype=torch.uint8, device="cuda")
+            run = lambda: lib.vqhmm_viterbi_f32(P(log_pi), P(log_A), P(em), P(L), B, T, K, P(path), P(score),  # noqa: E731
+                                                P(ws), nb, sp)
+            byts = B * (4.0 * T * K * K + 4.0 * T * K + 4.0 * T) + 4.0 * K
+            kern = "viterbi_kernel<8, true>"
+        else:
+            gamma = torch.empty(B, T, K, device="cuda")
+            logZ = torch.empty(B, device="cuda")
+            nb = lib.vqhmm_fwdbwd_workspace_size(B, T, K)
+            ws = torch.empty(max(nb, 1), dtype=torch.uint8, device="cuda")
+            run = lambda: lib.vqhmm_fwdbwd_f32(P(log_pi), P(log_A), P(em), P(L), B, T, K, P(gamma), P(logZ),  # noqa: E731
+                                               P(ws), nb, sp)
+            byts = B * (4.0 * T * K * K + 4.0 * T * K + 4.0 * T * K) + 4.0 * K
+            kern = "fwdbwd_kernel<8, true>"
+        for _ in range(3):
+            run()
+        s = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(10):
+            run()
+        e1.record(s)
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) / 10 * 1e3
+        gbps = byts / (us * 1e-6) / 1e9
+        out[name] = {"kernel": kern, "bound": "hbm", "avg_us": round(us, 2), "achieved": round(gbps, 1),
+                     "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(gbps / HBM_PEAK_GBPS, 4),
+                     "traffic": traffic_for(name, name), "shape": f"B{B} T{T} K{K}"}
+        del log_A, em, ws
+    return out
+
+
 def cpu_baseline(cfg, seconds):
     """CPU oracle (oracle/ref_model.py) train step on the same shape, this host's cores."""
     from oracle import ref_model as RM
@@ -187,7 +238,7 @@ def main():
     L = torch.full((B,), T, dtype=torch.int64, device="cuda")
     beta = 1.0
 
-    use_graph = world == 1 and not a.no_graph
+    use_graph = not a.no_graph  # N>1: fwd+bwd graph, RCCL all-reduce, Adam graph
     if use_graph:
         step = st.capture(x, u, L, beta)
     else:
@@ -230,6 +281,7 @@ def main():
                      "avg_us": round(dom["us"], 2)})
         kernels = {s["name"]: round(s["us"], 2) for s in stages}
     vq = vq_cfg3(lib) if rank == 0 else None
+    hmm = hmm_kernels(lib) if rank == 0 and not a.no_hmm else {}
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -246,7 +298,7 @@ def main():
                        "hidden_dim2": H2, "u_dim": U, "trans_hidden": TH,
                        "parallelism": f"dp{world}" if world > 1 else "single", "hip_graph": use_graph},
             "roofline": roof, "cpu_baseline": cpu,
-            "step_kernels_us": kernels, "vq_cfg3": vq,
+            "step_kernels_us": kernels, "vq_cfg3": vq, **hmm,
         }
         if cpu:
             line["speedup_vs_cpu"] = round(value / cpu["value"], 1)

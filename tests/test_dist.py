@@ -88,7 +88,7 @@ def test_shard_batch_rejects_uneven():
         dist.shard_batch(torch.zeros(5, 2, 3), torch.zeros(5, 1, 3), torch.zeros(5), 0, 2)
 
 
-def _gpu_worker(rank, world, port, out):
+def _gpu_worker(rank, world, port, out, graph=False):
     _setup(rank, world, port)
     import vqhmm
     from vqhmm import dist
@@ -100,8 +100,11 @@ def _gpu_worker(rank, world, port, out):
     L = torch.full((B,), T)
     xs, us, Ls = dist.shard_batch(x, u, L, rank, world)
     st = vqhmm.TrainState(m, lr=1e-3, distributed=True)
-    for _ in range(3):
-        st.step(xs.cuda(), us.cuda(), Ls, 1.0)
+    if graph:  # 2 warm-up steps + 1 replay of the split graphs (fwd+bwd graph, all-reduce, Adam graph)
+        st.capture(xs.cuda(), us.cuda(), Ls, 1.0, warmup=2)()
+    else:
+        for _ in range(3):
+            st.step(xs.cuda(), us.cuda(), Ls, 1.0)
     torch.cuda.synchronize()
     if rank == 0:
         torch.save(st.flat.cpu(), out)
@@ -109,10 +112,11 @@ def _gpu_worker(rank, world, port, out):
 
 
 @pytest.mark.gpu
-def test_gpu_two_ranks_match_one(tmp_path):
+@pytest.mark.parametrize("graph", [False, True])
+def test_gpu_two_ranks_match_one(tmp_path, graph):
     import vqhmm
     out = str(tmp_path / "dp.pt")
-    mp.start_processes(_gpu_worker, args=(2, free_port(), out), nprocs=2, join=True, start_method="spawn")
+    mp.start_processes(_gpu_worker, args=(2, free_port(), out, graph), nprocs=2, join=True, start_method="spawn")
     torch.manual_seed(0)
     m = vqhmm.VAE_HMM(5, 64, 3, 32, u_dim=4, trans_hidden=128).cuda()
     g = torch.Generator().manual_seed(3)

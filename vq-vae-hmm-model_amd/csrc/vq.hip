@@ -124,12 +124,17 @@ __global__ __launch_bounds__(256) void vq_mfma_kernel(const float* __restrict__ 
 // CB x 4 independent accumulators per tile.  Loads are buffer loads: one VGPR
 // byte offset per tile + the dim-group offset 16 T dg as an SGPR.  Each wave
 // walks a contiguous range of tiles (lines shared by neighbouring tiles stay
-// in one XCD's L2), and reloads dim group dg of the next tile right after the
-// current tile's MFMAs have consumed it.
-template <int DG, int CB, bool PF>  // Dv == 4 DG, K <= 16 CB; PF: double-buffer the next tile in registers
-__global__ __launch_bounds__(256, PF ? 2 : 3) void vq_rows_kernel(const float* __restrict__ z, int64_t B, int Dv, int T,
-                                                      const float* __restrict__ cb, int K, int32_t* __restrict__ idx,
-                                                      float* __restrict__ dmin, int64_t tiles, int64_t nwaves) {
+// in one XCD's L2).  Two register sets ping-pong: ALL loads of tile n+1 are
+// issued before the MFMAs of tile n, so a whole tile of MFMA work covers their
+// latency (with one set the compiler sinks the reloads behind the MFMAs that
+// read the registers and the wave drains its loads at the top of every tile).
+// ||z||^2 (only for dmin) is formed after the MFMAs, so it never pulls a wait
+// forward.
+template <int DG, int CB, bool DMIN, int NBUF>  // Dv == 4 DG, K <= 16 CB; DMIN: dmin requested; NBUF register sets
+__global__ __launch_bounds__(256, NBUF == 2 ? 2 : 1) void vq_rows_kernel(const float* __restrict__ z, int64_t B, int Dv, int T,
+                                                         const float* __restrict__ cb, int K,
+                                                         int32_t* __restrict__ idx, float* __restrict__ dmin,
+                                                         int64_t tiles, int64_t nwaves) {
   constexpr int LDSC = 16 * CB + 4;  // score rows [position][code]
   struct Prologue {
     float cbS[16 * CB][4 * DG + 1];  // codebook, +1 pad: conflict-free per-code rows
@@ -159,8 +164,11 @@ __global__ __launch_bounds__(256, PF ? 2 : 3) void vq_rows_kernel(const float* _
     const int64_t b = n / T;
     return (uint32_t)((b * (int64_t)Dv * T + (n - b * T)) * 4) + goff;
   };
-  auto ld = [&](uint32_t o, int dg) -> f32x4 {
-    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rz, (int)o, dg * gstep, 0));
+  auto load_tile = [&](int64_t tile, f32x4* zr) {
+    const uint32_t o = tile_off(tile);
+#pragma unroll
+    for (int dg = 0; dg < DG; ++dg)
+      zr[dg] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rz, (int)o, dg * gstep, 0));
   };
 
   constexpr int NC = 16 * CB * 4 * DG, NCP = (NC + 255) / 256;
@@ -172,15 +180,12 @@ __global__ __launch_bounds__(256, PF ? 2 : 3) void vq_rows_kernel(const float* _
   // equal share of the tiles per wave (every resident wave gets floor or ceil of tiles / nwaves)
   const int64_t t0 = gw < nwaves ? tiles * gw / nwaves : tiles;
   const int64_t t1 = gw < nwaves ? tiles * (gw + 1) / nwaves : tiles;
-  f32x4 zc[DG];
-  {
-    const uint32_t o = tile_off(t0 < t1 ? t0 : 0);  // unconditional: keeps vmcnt counting exact
-#pragma unroll
-    for (int dg = 0; dg < DG; ++dg) zc[dg] = ld(o, dg);  // in flight during the prologue
-  }
-  // prologue: the codebook crosses HBM once per workgroup (coalesced; loaded
-  // before the first tile so vmcnt can retire it first), then the A fragments
-  // and the ||c||^2 chains are built from LDS
+  f32x4 za[DG], zb[DG], zc3[NBUF == 3 ? DG : 1];
+  auto clampt = [&](int64_t t) { return t < t1 ? t : (t0 < t1 ? t1 - 1 : 0); };
+  load_tile(clampt(t0), za);  // unconditional: in flight during the prologue
+  if constexpr (NBUF == 3) load_tile(clampt(t0 + 1), zb);
+  // prologue: the codebook crosses HBM once per workgroup (coalesced), then the
+  // A fragments and the ||c||^2 chains are built from LDS
 #pragma unroll
   for (int k = 0; k < NCP; ++k) {
     const int i = tid + 256 * k;
@@ -205,18 +210,15 @@ __global__ __launch_bounds__(256, PF ? 2 : 3) void vq_rows_kernel(const float* _
 #pragma unroll
     for (int v = 0; v < 4; ++v) init[c][v] = cnS[16 * c + 4 * g + v];
 
-  // one tile; RELOAD: fetch dim group dg of tile + 1 into zc[dg] right after it
-  // has been consumed (the last tile of the range is peeled off with RELOAD =
-  // false, so the steady-state reload is unconditional and lands in place)
-  auto run_tile = [&](int64_t tile, auto reload) {
-    constexpr bool RELOAD = decltype(reload)::value;
-    const uint32_t no = tile_off(tile + 1);
+  // one tile on zc while the loads of tile + NBUF - 1 land in zn
+  auto run_tile = [&](int64_t tile, const f32x4* zc, f32x4* zn) {
+    load_tile(clampt(tile + NBUF - 1), zn);  // unconditional: keeps the vmcnt counts exact
+    __builtin_amdgcn_sched_barrier(0);                 // pin: the loads go out before the MFMAs
     f32x4 acc[CB][4];
 #pragma unroll
     for (int c = 0; c < CB; ++c)
 #pragma unroll
       for (int m = 0; m < 4; ++m) acc[c][m] = f32x4{init[c][0], init[c][1], init[c][2], init[c][3]};
-    float q[4] = {0.f, 0.f, 0.f, 0.f};  // ||z||^2 chain of residue d = g (mod 4), per position m
 #pragma unroll
     for (int dg = 0; dg < DG; ++dg) {
       float av[CB];
@@ -226,9 +228,6 @@ __global__ __launch_bounds__(256, PF ? 2 : 3) void vq_rows_kernel(const float* _
       for (int m = 0; m < 4; ++m)
 #pragma unroll
         for (int c = 0; c < CB; ++c) acc[c][m] = mfma16x16x4(av[c], zc[dg][m], acc[c][m]);
-#pragma unroll
-      for (int m = 0; m < 4; ++m) q[m] = __builtin_fmaf(zc[dg][m], zc[dg][m], q[m]);
-      if constexpr (RELOAD) zc[dg] = ld(no, dg);
     }
     // scores through LDS as [position][code] so each lane scans ONE position's
     // codes in ascending order (strict <: lowest code wins ties); position
@@ -238,7 +237,15 @@ __global__ __launch_bounds__(256, PF ? 2 : 3) void vq_rows_kernel(const float* _
     for (int m = 0; m < 4; ++m) {
 #pragma unroll
       for (int c = 0; c < CB; ++c) *reinterpret_cast<f32x4*>(sc + (4 * j + m) * LDSC + 16 * c + 4 * g) = acc[c][m];
-      u.loop.qS[wave][(4 * j + m) * 4 + g] = q[m];
+    }
+    if constexpr (DMIN) {
+      float q[4] = {0.f, 0.f, 0.f, 0.f};  // ||z||^2 chain of residue d = g (mod 4), per position m
+#pragma unroll
+      for (int dg = 0; dg < DG; ++dg)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) q[m] = __builtin_fmaf(zc[dg][m], zc[dg][m], q[m]);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) u.loop.qS[wave][(4 * j + m) * 4 + g] = q[m];
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
     __builtin_amdgcn_wave_barrier();
@@ -252,29 +259,31 @@ __global__ __launch_bounds__(256, PF ? 2 : 3) void vq_rows_kernel(const float* _
       for (int e = 0; e < 4; ++e)
         if (v[e] < best) { best = v[e]; arg = 4 * c4 + e; }
     }
-    const f32x4 qq = *reinterpret_cast<const f32x4*>(&u.loop.qS[wave][lane * 4]);
-    const float zz = (qq[0] + qq[1]) + (qq[2] + qq[3]);
     const int64_t n = tile * 64 + lane;
     if (n < N) {
       idx[n] = arg;
-      if (dmin) dmin[n] = best + zz;
+      if constexpr (DMIN) {
+        const f32x4 qq = *reinterpret_cast<const f32x4*>(&u.loop.qS[wave][lane * 4]);
+        dmin[n] = best + ((qq[0] + qq[1]) + (qq[2] + qq[3]));
+      }
     }
     __builtin_amdgcn_wave_barrier();  // the next tile's writes must not pass this tile's reads
   };
-  if (t0 < t1) {
-    if constexpr (PF) {
-      for (int64_t tile = t0; tile + 1 < t1; ++tile) run_tile(tile, std::true_type{});
-      run_tile(t1 - 1, std::false_type{});
-    } else {  // no in-wave prefetch: fewer registers, more resident waves hide the latency
-      for (int64_t tile = t0; tile < t1; ++tile) {
-        if (tile != t0) {
-          const uint32_t o = tile_off(tile);
-#pragma unroll
-          for (int dg = 0; dg < DG; ++dg) zc[dg] = ld(o, dg);
-        }
-        run_tile(tile, std::false_type{});
-      }
+  int64_t tile = t0;
+  if constexpr (NBUF == 2) {
+    for (; tile + 1 < t1; tile += 2) {  // no branch inside the pair: one pending-load state at the latch
+      run_tile(tile, za, zb);
+      run_tile(tile + 1, zb, za);
     }
+    if (tile < t1) run_tile(tile, za, zb);
+  } else {
+    for (; tile + 2 < t1; tile += 3) {
+      run_tile(tile, za, zc3);
+      run_tile(tile + 1, zb, za);
+      run_tile(tile + 2, zc3, zb);
+    }
+    if (tile < t1) run_tile(tile, za, zc3);
+    if (tile + 1 < t1) run_tile(tile + 1, zb, za);
   }
 }
 
@@ -372,14 +381,17 @@ static void launch_mfma(const float* z, int64_t B, int Dv, int T, const float* c
 template <int DG, int CB>
 static void launch_rows(const float* z, int64_t B, int Dv, int T, const float* cb, int K, int32_t* idx, float* dmin,
                         hipStream_t s) {
-  static const int pf = env_int("VQHMM_VQ_PF", 1, 0, 1);  // tuning knob: in-wave double buffer
+  static const int nbuf = env_int("VQHMM_VQ_NBUF", 2, 2, 3);  // tuning knob: register sets in flight
   const int64_t tiles = cdiv(B * (int64_t)T, 64);
-  const int64_t waves = cdiv(persistent_waves(tiles, pf ? 8 : 12), 4) * 4;
+  const int64_t waves = cdiv(persistent_waves(tiles, 4), 4) * 4;  // one wave per SIMD measured best (cfg3)
   const unsigned grid = (unsigned)(waves / 4);
-  if (pf)
-    vq_rows_kernel<DG, CB, true><<<grid, 256, 0, s>>>(z, B, Dv, T, cb, K, idx, dmin, tiles, waves);
-  else
-    vq_rows_kernel<DG, CB, false><<<grid, 256, 0, s>>>(z, B, Dv, T, cb, K, idx, dmin, tiles, waves);
+  if (nbuf == 3) {
+    if (dmin) vq_rows_kernel<DG, CB, true, 3><<<grid, 256, 0, s>>>(z, B, Dv, T, cb, K, idx, dmin, tiles, waves);
+    else vq_rows_kernel<DG, CB, false, 3><<<grid, 256, 0, s>>>(z, B, Dv, T, cb, K, idx, dmin, tiles, waves);
+  } else {
+    if (dmin) vq_rows_kernel<DG, CB, true, 2><<<grid, 256, 0, s>>>(z, B, Dv, T, cb, K, idx, dmin, tiles, waves);
+    else vq_rows_kernel<DG, CB, false, 2><<<grid, 256, 0, s>>>(z, B, Dv, T, cb, K, idx, dmin, tiles, waves);
+  }
 }
 
 // Dv % 4 == 0 only (whole dim groups)

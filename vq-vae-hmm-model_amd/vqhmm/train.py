@@ -116,22 +116,39 @@ class TrainState:
             p.grad = self.grad[self.off[i]:self.off[i + 1]].view_as(p).clone()
 
     def capture(self, x, u, lengths, beta, warmup=2):
-        """Capture one fixed-shape step (single process) into a HIP graph; returns a replay callable."""
-        if self.distributed and self.world > 1:
-            raise RuntimeError("capture(): multi-rank steps run eagerly")
+        """Capture one fixed-shape step into HIP graphs; returns a replay callable.
+
+        Single process: the whole step is one graph.  Multi-rank: forward+backward
+        and Adam are two graphs and the gradient all-reduce runs between them on
+        the same stream (the collective stays outside the graphs, so no
+        graph-capture support is required of the communicator)."""
         x, u, lengths = self.prepare(x, u, lengths)
+        split = self.distributed and self.world > 1
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
-            for _ in range(warmup):
+            for _ in range(warmup):  # warm-up steps are real steps (identical to eager ones)
                 self.forward_backward(x, u, lengths, beta)
+                self.reduce_gradients()
                 self.apply_adam()
         torch.cuda.current_stream(self.device).wait_stream(s)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        if not split:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self.forward_backward(x, u, lengths, beta)
+                self.apply_adam()
+            return g.replay
+        g_fb, g_adam = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g_fb):
             self.forward_backward(x, u, lengths, beta)
+        with torch.cuda.graph(g_adam):
             self.apply_adam()
-        return g.replay
+
+        def replay():
+            g_fb.replay()
+            self.reduce_gradients()
+            g_adam.replay()
+        return replay
 
 
 def train_model(model, dataloader, num_epochs=10, lr=1e-3):
