@@ -245,14 +245,28 @@ __device__ __forceinline__ uint2 bp_map(uint32_t mlo, uint32_t mhi, int q, bool 
   return make_uint2(w[0], w[1]);
 }
 
-// lo[LANE] = bal[31:0], hi[LANE] = bal[63:32].  The s_nop covers the
-// "VALU writes SGPR -> v_writelane reads it" hazard (the ballot's v_cmp may
-// immediately precede; hipcc does not look inside inline asm).
-template <int LANE>
-__device__ __forceinline__ void writelane_pair(uint32_t& lo, uint32_t& hi, uint64_t bal) {
-  asm("s_nop 4\n\tv_writelane_b32 %0, %2, %4\n\tv_writelane_b32 %1, %3, %4"
+// lanes BASE .. BASE+7 of (lo, hi) = the 8 ballots.  One asm block: its
+// s_nop sits after every ballot's v_cmp (they are its inputs), covering the
+// "VALU writes SGPR -> v_writelane reads it" hazard once per 8 steps.
+template <int BASE>
+__device__ __forceinline__ void writelane8(uint32_t& lo, uint32_t& hi, const uint64_t* b) {
+  asm("s_nop 4\n\t"
+      "v_writelane_b32 %0, %2, %18\n\tv_writelane_b32 %1, %3, %18\n\t"
+      "v_writelane_b32 %0, %4, %19\n\tv_writelane_b32 %1, %5, %19\n\t"
+      "v_writelane_b32 %0, %6, %20\n\tv_writelane_b32 %1, %7, %20\n\t"
+      "v_writelane_b32 %0, %8, %21\n\tv_writelane_b32 %1, %9, %21\n\t"
+      "v_writelane_b32 %0, %10, %22\n\tv_writelane_b32 %1, %11, %22\n\t"
+      "v_writelane_b32 %0, %12, %23\n\tv_writelane_b32 %1, %13, %23\n\t"
+      "v_writelane_b32 %0, %14, %24\n\tv_writelane_b32 %1, %15, %24\n\t"
+      "v_writelane_b32 %0, %16, %25\n\tv_writelane_b32 %1, %17, %25"
       : "+v"(lo), "+v"(hi)
-      : "s"((uint32_t)bal), "s"((uint32_t)(bal >> 32)), "i"(LANE));
+      : "s"((uint32_t)b[0]), "s"((uint32_t)(b[0] >> 32)), "s"((uint32_t)b[1]), "s"((uint32_t)(b[1] >> 32)),
+        "s"((uint32_t)b[2]), "s"((uint32_t)(b[2] >> 32)), "s"((uint32_t)b[3]), "s"((uint32_t)(b[3] >> 32)),
+        "s"((uint32_t)b[4]), "s"((uint32_t)(b[4] >> 32)), "s"((uint32_t)b[5]), "s"((uint32_t)(b[5] >> 32)),
+        "s"((uint32_t)b[6]), "s"((uint32_t)(b[6] >> 32)), "s"((uint32_t)b[7]), "s"((uint32_t)(b[7] >> 32)),
+        "i"(BASE), "i"(BASE + 1), "i"(BASE + 2), "i"(BASE + 3), "i"(BASE + 4), "i"(BASE + 5), "i"(BASE + 6),
+        "i"(BASE + 7));
+
 }
 
 __device__ __forceinline__ uint32_t perm_bytes(uint2 m, uint32_t sel) {
@@ -299,41 +313,56 @@ __global__ __launch_bounds__(64) void viterbi_kernel(const float* __restrict__ l
   for (int o = 1; o < 64; o <<= 1) Lmin = min(Lmin, __shfl_xor(Lmin, o));
   Lmin = __builtin_amdgcn_readfirstlane(Lmin);
   uint32_t mlo = 0, mhi = 0;
-  // one chunk of steps: A / em values of the chunk are read from LDS up front
-  // (one wait), then the max-plus chain runs on registers only.  CHECK: some
-  // sequence of the wave ends inside this chunk.
-  auto run_chunk = [&](const float* sl, int t0, bool first, auto check) {
-    constexpr bool CHECK = decltype(check)::value;
-    float av[HC], ev[HC];
+  // A / em values of a chunk are read from LDS up front (one wait per chunk),
+  // then the max-plus chain runs on registers only.  (Reading the next chunk
+  // during this one was measured worse: lgkmcnt counts only 15, and hipcc
+  // shuffles the ping-pong sets through copies that wait early.)  Ballots are
+  // kept in SGPRs for 8 steps and moved into the mask VGPRs in one batch (one
+  // hazard pad per 8 steps instead of one per step).
+  constexpr int HB = 8;  // ballots per hazard-padded writelane batch
+  auto read_vals = [&](const float* sl, float* av, float* ev) {
 #pragma unroll
     for (int s = 0; s < HC; ++s) {
       const int p = s & 1;  // parity of t (t0 even)
       av[s] = lm.a_ok[p] ? sl[lm.a_off[p] + s * K * K] : NEG_INF;
       ev[s] = lm.e_ok[p] ? sl[lm.e_off[p] + s * K] : 0.f;
     }
-    static_for<HC>([&](auto si) {
-      constexpr int s = decltype(si)::value, p = s & 1;
-      if (s == 0 && first) {
-        // delta_0 on the inner axis: lane's i0 = g % KP = the even map's j
-        d = (L > 0 && i0 < K) ? lp + ev[0] : NEG_INF;
-        return;
-      }
-      const float v = d + av[s];
-      const float m = p == 0 ? allred<KP, false>(v, OpMax{}) : allred<KP, true>(v, OpMax{});
-      const uint64_t bal = __builtin_amdgcn_ballot_w64(v == m);
-      writelane_pair<s>(mlo, mhi, bal);
-      if (!CHECK || t0 + s < L) d = m + ev[s];
+  };
+  // CHECK: some sequence of the wave ends inside this chunk
+  auto run_chunk = [&](const float* av, const float* ev, int t0, bool first, auto check) {
+    constexpr bool CHECK = decltype(check)::value;
+    static_for<HC / 8>([&](auto hi) {
+      constexpr int h = decltype(hi)::value;
+      uint64_t bal[HB];
+      static_for<HB>([&](auto si) {
+        constexpr int s = h * HB + decltype(si)::value, p = s & 1;
+        if (s == 0 && first) {
+          // delta_0 on the inner axis: lane's i0 = g % KP = the even map's j
+          d = (L > 0 && i0 < K) ? lp + ev[0] : NEG_INF;
+          bal[0] = 0;
+          return;
+        }
+        const float v = d + av[s];
+        const float m = p == 0 ? allred<KP, false>(v, OpMax{}) : allred<KP, true>(v, OpMax{});
+        bal[s - h * HB] = __builtin_amdgcn_ballot_w64(v == m);
+        if (!CHECK || t0 + s < L) d = m + ev[s];
+      });
+      writelane8<h * HB>(mlo, mhi, bal);
     });
   };
+  auto do_chunk = [&](int c, const float* av, const float* ev) {
+    const int t0 = c * HC;
+    if (t0 + HC <= Lmin) run_chunk(av, ev, t0, c == 0, std::false_type{});
+    else run_chunk(av, ev, t0, c == 0, std::true_type{});
+    if (lane < HC) wmask[t0 + lane] = make_uint2(mlo, mhi);  // masks of steps t0 .. t0 + HC - 1
+  };
+  float av[HC], ev[HC];
   for (int c = 0; c < nchunks; ++c) {
     stage_chunk<K, W16>(log_A, em, b0, B, T, min(c + R - 1, nchunks - 1), ring + ((c + R - 1) % R) * Gm::SLOT,
                         lane);
     wait_vm<Rg::WAIT>();
-    const float* sl = ring + (c % R) * Gm::SLOT;
-    const int t0 = c * HC;
-    if (t0 + HC <= Lmin) run_chunk(sl, t0, c == 0, std::false_type{});
-    else run_chunk(sl, t0, c == 0, std::true_type{});
-    if (lane < HC) wmask[t0 + lane] = make_uint2(mlo, mhi);  // masks of steps t0 .. t0 + HC - 1
+    read_vals(ring + (c % R) * Gm::SLOT, av, ev);
+    do_chunk(c, av, ev);
   }
 
   // final state: first arg-max over the state axis the lanes hold after step L-1
