@@ -98,6 +98,35 @@ def test_forward_backward_long_T_precision():
     assert np.all(np.abs(logZ.cpu().numpy() - rz) <= 1e-5 * np.abs(rz))
 
 
+@pytest.mark.parametrize("K", [3, 8])
+def test_forward_backward_extreme_tables(K):
+    """Tables that push the fast base-2 step out of range, so chunks take the exact
+    max-shifted recomputation: left-to-right transitions (log 0 = -inf), emissions of
+    about -1e3 nats, a window with hundreds of nats of emission spread, and
+    near-deterministic transitions.  Same 1e-5 contract vs the fp64 oracle."""
+    import vqhmm
+    B, T = 6, 150
+    rng = np.random.default_rng(K + 100)
+    log_pi, log_A, em = random_hmm(K + 200, B, T, K)
+    log_A = log_A.astype(np.float64)
+    em = em.astype(np.float64)
+    tri = np.triu(np.ones((K, K), bool))
+    la = np.where(tri, log_A[0], -np.inf)
+    log_A[0] = la - np.logaddexp.reduce(la, axis=-1, keepdims=True)   # b0: left-to-right
+    em[1] = em[1] * 50.0 - 1000.0                                      # b1: huge negative emissions
+    em[2, 40:60] *= 150.0                                              # b2: 300+ nat spread
+    log_A[3] = log_softmax(rng.standard_normal((T, K, K)) * 80.0)      # b3: near-deterministic
+    L = np.array([T, T, T, T, 77, 1], np.int64)
+    log_A = log_A.astype(np.float32)
+    em = em.astype(np.float32)
+    gamma, logZ = vqhmm.forward_backward(*gpu(log_pi, log_A, em), torch.from_numpy(L))
+    with np.errstate(divide="ignore", invalid="ignore"):
+        rg, rz = hmm_ref.forward_backward_f64(log_pi, log_A, em, L)
+    assert np.abs(gamma.cpu().numpy() - rg).max() <= 1e-5
+    z = logZ.cpu().numpy()
+    assert np.all(np.abs(z - rz) <= 1e-5 * np.maximum(1.0, np.abs(rz)))
+
+
 def test_gamma_sums_to_one_and_viterbi_on_model_tables():
     """Use the model's own Prior tables and encoder posteriors as inputs."""
     import vqhmm

@@ -488,18 +488,74 @@ int launch_viterbi(const float* log_pi, const float* log_A, const float* em, con
 // the tables through its own ring; both stage their per-step vectors in LDS and
 // flush one chunk at a time to the workspace; then both waves form gamma in
 // parallel over t (no serial dependency left).
-//   alpha: al_0 = log_pi + e_0;
-//          al_t(j) = (LSE_i(al_{t-1}(i) + A_t(i,j)) + e_t(j)) - mu_{t-1},
-//          mu_{t-1} = max_i al_{t-1}(i) (reduced off the chain while step t runs),
-//          S += mu (fp64)  ->  logZ = S + LSE_j al_{L-1}(j)
-//   beta:  be_{L-1} = 0;
-//          be_t(i) = LSE_j((A_{t+1}(i,j) + e_{t+1}(j)) + be_{t+1}(j)) - nu,
-//          nu = max_j be_{t+1}(j)
+//
+// Everything runs in base 2 (lg = log2; inputs scaled by log2(e) as they are
+// read) with shifts — arbitrary constants of a shift-invariant recursion,
+// chosen so every vector stays within a few steps' spread of 0:
+//   alpha: al_0 = lg pi + (lg e_0 - E_0),
+//          al_t(j) = lg sum_i 2^(al_{t-1}(i) + lg A_t(i,j)) + (lg e_t(j) - E_t) - mu_t
+//          with E_t = max_j lg e_t(j) (from the staged tables, off the chain) and
+//          mu_t = max_i al_{t-1}(i) every FB_NORM-th step (reduced beside the chain), else 0;
+//          logZ = ln2 (sum_t mu_t + lg sum_j 2^al_{L-1}(j)) + sum_t max_j e_t(j)
+//   beta:  be_{L-1} = 0,
+//          be_t(i) = lg sum_j 2^((lg A_{t+1}(i,j) + lg e_{t+1}(j) - E_{t+1}) + be_{t+1}(j)) - nu_t,
+//          nu_t = max_j be_{t+1}(j) every FB_NORM-th step, else 0
 //   gamma_t(i) = softmax_i(al_t(i) + be_t(i))
-// The per-step shifts are arbitrary constants of a shift-invariant recursion;
-// these keep every stored vector within one step's increment of 0.
-// Workspace: al [B][T][K], then be' [B][T][K] with be'[t+1] = be_t.
+// With the shifts, a step's terms stay within a few steps' transition and
+// emission spread of 1, so the serial chain skips the max-subtraction of a
+// log-sum-exp: add, exp2, the add-reduction, log2, add.  A chunk in which a
+// live step's column sum leaves [2^-FB_LIM, 2^FB_LIM] (an over/underflow that
+// may have dropped a significant term, or an all -inf column) is recomputed
+// from its saved start state with the max-shifted log-sum-exp, normalised
+// every step — same contract, rare path.
+// Workspace: al [B][T][K], then be' [B][T][K] with be'[t+1] = be_t (base 2).
 constexpr float F32_LOWEST = -3.402823466e38f;
+constexpr float LOG2E_F = 1.44269504088896341f;
+constexpr double LN2_D = 0.69314718055994531;
+constexpr float FB_LIM = 96.f;  // fast-step column sums must stay within 2^(+-FB_LIM)
+constexpr int FB_NORM = 4;      // fast steps renormalise by the running max every FB_NORM steps
+
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ __forceinline__ float flog2(float x) { return __builtin_amdgcn_logf(x); }
+
+template <int N>
+__device__ __forceinline__ float tree_sum(const float* v) {  // pairwise (fixed order)
+  float t[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) t[i] = v[i];
+#pragma unroll
+  for (int w = N / 2; w >= 1; w /= 2)
+#pragma unroll
+    for (int i = 0; i < w; ++i) t[i] += t[i + w];
+  return t[0];
+}
+
+// a staged chunk into registers (base 2), read up front off the chain.  Per step:
+//   alpha: av = lg A(i,j), dv = lg e(j) - E, xv = max_j e (natural log)
+//   beta:  av = lg A(i,j) + lg e(j) - E      (data step d serves t = d - 1)
+template <int K, bool W16, bool BETA>
+__device__ __forceinline__ void read_fb_chunk(const float* sl, const LaneMap<K, W16>& lm, float* av, float* dv,
+                                              float* xv) {
+  using Gm = Geo<K, W16>;
+  constexpr int KP = Gm::KP, HC = Gm::HC;
+#pragma unroll
+  for (int s = 0; s < HC; ++s) {
+    const int p = (s + (BETA ? 1 : 0)) & 1;  // parity of the step's t
+    const float a = lm.a_ok[p] ? sl[lm.a_off[p] + s * K * K] : NEG_INF;
+    const float e = lm.e_ok[p] ? sl[lm.e_off[p] + s * K] : 0.f;
+    // the outer map's j = g % KP covers every state along the inner axis
+    const float ein = lm.e_ok[0] ? sl[lm.e_off[0] + s * K] : NEG_INF;
+    float emx = allred<KP, true>(ein, OpMax{});
+    emx = emx == NEG_INF ? 0.f : emx;
+    if constexpr (BETA) {
+      av[s] = (a + (e - emx)) * LOG2E_F;
+    } else {
+      av[s] = a * LOG2E_F;
+      dv[s] = (e - emx) * LOG2E_F;
+      xv[s] = emx;
+    }
+  }
+}
 
 template <int K, bool W16>
 __global__ __launch_bounds__(128) void fwdbwd_kernel(const float* __restrict__ log_pi,
@@ -510,7 +566,7 @@ __global__ __launch_bounds__(128) void fwdbwd_kernel(const float* __restrict__ l
   using Gm = Geo<K, W16>;
   using Rg = Ring<K, W16>;
   constexpr int KP = Gm::KP, G = Gm::G, SPW = Gm::SPW, R = Rg::R, HC = Gm::HC;
-  constexpr int VB = SPW * HC * K;        // per-wave vector buffer (floats)
+  constexpr int VB = SPW * HC * KP;       // per-wave vector buffer [SPW][HC][KP] (floats)
   constexpr int PW = R * Gm::SLOT + VB;   // LDS floats per wave
   __shared__ float lds[2 * PW];           // the only LDS object
 
@@ -521,33 +577,44 @@ __global__ __launch_bounds__(128) void fwdbwd_kernel(const float* __restrict__ l
   const bool live = b < B;
   const int64_t Lr = live ? lengths[b] : 0;
   const int L = (int)(Lr <= 0 ? 0 : (Lr < T ? Lr : T));
-  const int i0 = g % KP;
-  const float lp = i0 < K ? log_pi[i0] : 0.f;
-  int Lmax = L;
+  const int jo = g % KP, ji = g / KP;  // lane's inner / outer coordinate
+  const float lp2 = jo < K ? log_pi[jo] * LOG2E_F : 0.f;
+  int Lmax = L, Lmin = L;
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) Lmax = max(Lmax, __shfl_xor(Lmax, o));
+  for (int o = 1; o < 64; o <<= 1) {
+    Lmax = max(Lmax, __shfl_xor(Lmax, o));
+    Lmin = min(Lmin, __shfl_xor(Lmin, o));
+  }
   Lmax = __builtin_amdgcn_readfirstlane(Lmax);
+  Lmin = __builtin_amdgcn_readfirstlane(Lmin);
   wait_vm<0>();
   float* ring = lds + wave * PW;
   float* vbuf = ring + R * Gm::SLOT;
+  float* vrow = vbuf + grp * HC * KP;
   float* ws_al = ws;
   float* ws_be = ws + (size_t)B * T * K;
   const LaneMap<K, W16> lm(grp, g);
   const int nchunks = (int)cdiv(Lmax, HC);
 
-  // flush vbuf -> dst rows [t0, t0 + HC) of the wave's sequences (t < T only)
+  // flush vbuf -> dst rows [t0, t0 + HC) of the wave's sequences (t < T only).
+  // Every lane of a group stores its step value unmasked (lanes sharing a
+  // state write the same word); the wave's LDS ops retire in order.
   auto flush = [&](float* dst, int t0) {
+    asm volatile("" ::: "memory");
     constexpr int NF = (VB + 63) / 64;
 #pragma unroll
     for (int k = 0; k < NF; ++k) {
       const int idx = k * 64 + lane;
       if (VB % 64 == 0 || idx < VB) {
-        const int q = idx / (HC * K), r = idx - q * (HC * K), s = r / K;
+        const int q = idx / (HC * KP), r = idx - q * (HC * KP), s = r / KP, j = r - s * KP;
         const float v = vbuf[idx];
-        if (b0 + q < B && t0 + s < T) dst[((b0 + q) * (int64_t)T + t0) * K + r] = v;
+        if (j < K && b0 + q < B && t0 + s < T) dst[((b0 + q) * (int64_t)T + t0 + s) * K + j] = v;
       }
     }
+    asm volatile("" ::: "memory");
   };
+  float av[HC], dv[HC], xv[HC], mv[HC];
+  float rng = 0.f;  // max |lg column sum| over the chunk's live fast steps
 
   if (wave == 0) {
     // ------------------------------------------------------------ alpha
@@ -557,61 +624,72 @@ __global__ __launch_bounds__(128) void fwdbwd_kernel(const float* __restrict__ l
         stage_chunk<K, W16>(log_A, em, b0, B, T, min(c, nchunks - 1), ring + c * Gm::SLOT, lane);
     }
     float al = NEG_INF;
-    double S = 0.0;
+    double S2 = 0.0, SE = 0.0;  // sum of mu (base 2), sum of E (natural)
+    // EXACT: max-shifted log-sum-exp; CHECK: some sequence ends inside the chunk
+    auto steps = [&](int t0, bool first, auto exact, auto check) {
+      constexpr bool EXACT = decltype(exact)::value, CHECK = decltype(check)::value;
+      static_for<HC>([&](auto si) {
+        constexpr int s = decltype(si)::value, p = s & 1;
+        if (s == 0 && first) {  // al_0 on the inner axis: lane's i = g % KP = the even map's j
+          al = (L > 0 && jo < K) ? lp2 + dv[0] : NEG_INF;
+          mv[0] = 0.f;
+          vrow[jo] = al;
+          return;
+        }
+        const bool upd = !CHECK || t0 + s < L;
+        const float v = al + av[s];
+        float mus = 0.f;
+        if constexpr (EXACT || s % FB_NORM == 0) {
+          const float mu = allred<KP, p == 1>(al, OpMax{});
+          mus = mu == NEG_INF ? 0.f : mu;
+        }
+        float nal;
+        if constexpr (EXACT) {
+          const float mm = fmaxf(allred<KP, p == 1>(v, OpMax{}), F32_LOWEST);
+          const float sm = allred<KP, p == 1>(fexp2(v - mm), OpAdd{});
+          nal = (mm + flog2(sm)) + (dv[s] - mus);
+        } else {
+          const float ls = flog2(allred<KP, p == 1>(fexp2(v), OpAdd{}));
+          nal = ls + (dv[s] - mus);
+          rng = fmaxf(rng, fabsf((lm.e_ok[p] && upd) ? ls : 0.f));
+        }
+        mv[s] = upd ? mus : 0.f;
+        if (upd) al = nal;
+        vrow[s * KP + (p == 0 ? jo : ji)] = al;  // state j = the lane's j-coordinate
+      });
+    };
     for (int c = 0; c < nchunks; ++c) {
       stage_chunk<K, W16>(log_A, em, b0, B, T, min(c + R - 1, nchunks - 1), ring + ((c + R - 1) % R) * Gm::SLOT,
                           lane);
       wait_vm<Rg::WAIT>();
-      const float* sl = ring + (c % R) * Gm::SLOT;
+      read_fb_chunk<K, W16, false>(ring + (c % R) * Gm::SLOT, lm, av, dv, xv);
       const int t0 = c * HC;
-#pragma unroll
-      for (int s = 0; s < HC; ++s) {
-        const int p = s & 1;
-        const int t = t0 + s;
-        float a = sl[lm.a_off[p] + s * K * K];
-        a = lm.a_ok[p] ? a : NEG_INF;
-        float e = sl[lm.e_off[p] + s * K];
-        e = lm.e_ok[p] ? e : 0.f;
-        if (s == 0 && c == 0) {
-          al = (L > 0 && i0 < K) ? lp + e : NEG_INF;
-          if (g < KP && g < K) vbuf[grp * HC * K + g] = al;
-          continue;
-        }
-        const float v = al + a;
-        float m, mu, sm;
-        if (p == 0) {
-          m = allred<KP, false>(v, OpMax{});
-          mu = allred<KP, false>(al, OpMax{});
-        } else {
-          m = allred<KP, true>(v, OpMax{});
-          mu = allred<KP, true>(al, OpMax{});
-        }
-        const float mm = fmaxf(m, F32_LOWEST);
-        const float x = __expf(v - mm);
-        sm = p == 0 ? allred<KP, false>(x, OpAdd{}) : allred<KP, true>(x, OpAdd{});
-        const float r = (mm + __logf(sm)) + e;
-        const float mus = mu == NEG_INF ? 0.f : mu;
-        if (t < L) {
-          al = r - mus;
-          S += (double)mus;
-        }
-        // lanes with i-coordinate 0 hold state j's value once each
-        const bool wr = p == 0 ? (g < KP) : (g % KP == 0);
-        const int js = p == 0 ? g : g / KP;
-        if (wr && js < K) vbuf[grp * HC * K + s * K + js] = al;
+      const float al_c = al;
+      rng = 0.f;
+      if (t0 + HC <= Lmin) steps(t0, c == 0, std::false_type{}, std::false_type{});
+      else steps(t0, c == 0, std::false_type{}, std::true_type{});
+      if (__builtin_amdgcn_ballot_w64(rng > FB_LIM)) {  // rare: recompute the chunk exactly
+        al = al_c;
+        steps(t0, c == 0, std::true_type{}, std::true_type{});
       }
+#pragma unroll
+      for (int s = 0; s < HC; ++s) xv[s] = t0 + s < L ? xv[s] : 0.f;
+      S2 += (double)tree_sum<HC>(mv);
+      SE += (double)tree_sum<HC>(xv);
       flush(ws_al, t0);
     }
-    // logZ = S + LSE over the state axis held after step L-1
+    // logZ from the state axis held after step L-1 (even t: inner)
     const int tl = L - 1;
     const bool held_inner = (tl <= 0) || ((tl & 1) == 0);
-    const int st = held_inner ? g % KP : g / KP;
+    const int st = held_inner ? jo : ji;
     const float x0 = st < K ? al : NEG_INF;
     const float mx = held_inner ? allred<KP, true>(x0, OpMax{}) : allred<KP, false>(x0, OpMax{});
     const float mxs = fmaxf(mx, F32_LOWEST);
-    const float ex = __expf(x0 - mxs);
+    const float ex = fexp2(x0 - mxs);
     const float sx = held_inner ? allred<KP, true>(ex, OpAdd{}) : allred<KP, false>(ex, OpAdd{});
-    if (live && g == 0) logZ[b] = L > 0 ? (float)(S + (double)(mxs + __logf(sx))) : __builtin_bit_cast(float, 0x7fc00000u);
+    if (live && g == 0)
+      logZ[b] = L > 0 ? (float)(LN2_D * (S2 + (double)mxs + (double)flog2(sx)) + SE)
+                      : __builtin_bit_cast(float, 0x7fc00000u);
   } else {
     // ------------------------------------------------------------ beta
     // chunk k holds data steps [k HC, k HC + HC); data step d serves beta step t = d - 1
@@ -621,40 +699,45 @@ __global__ __launch_bounds__(128) void fwdbwd_kernel(const float* __restrict__ l
         stage_chunk<K, W16>(log_A, em, b0, B, T, max(nchunks - 1 - c, 0), ring + c * Gm::SLOT, lane);
     }
     float be = 0.f;
+    auto steps = [&](int d0, bool last, auto exact, auto check) {
+      constexpr bool EXACT = decltype(exact)::value, CHECK = decltype(check)::value;
+      static_for<HC>([&](auto si) {
+        constexpr int s = HC - 1 - decltype(si)::value, p = (s + 1) & 1;  // p = parity of t
+        if (s == 0 && last) return;                                       // t = -1
+        const bool upd = !CHECK || d0 + s - 1 < L - 1;
+        const float v = av[s] + be;
+        float nus = 0.f;
+        if constexpr (EXACT || s % FB_NORM == 0) {
+          const float nu = allred<KP, p == 0>(be, OpMax{});
+          nus = nu == NEG_INF ? 0.f : nu;
+        }
+        float nb;
+        if constexpr (EXACT) {
+          const float mm = fmaxf(allred<KP, p == 0>(v, OpMax{}), F32_LOWEST);
+          const float sm = allred<KP, p == 0>(fexp2(v - mm), OpAdd{});
+          nb = (mm + flog2(sm)) - nus;
+        } else {
+          const float ls = flog2(allred<KP, p == 0>(fexp2(v), OpAdd{}));
+          nb = ls - nus;
+          rng = fmaxf(rng, fabsf((lm.e_ok[p ^ 1] && upd) ? ls : 0.f));  // e_ok[p^1]: lane's i < K
+        }
+        if (upd) be = nb;
+        vrow[s * KP + (p == 0 ? ji : jo)] = be;  // state i = the lane's i-coordinate; slot s <-> be'[t + 1]
+      });
+    };
     for (int c = 0; c < nchunks; ++c) {
       const int k = nchunks - 1 - c;
       stage_chunk<K, W16>(log_A, em, b0, B, T, max(k - (R - 1), 0), ring + ((c + R - 1) % R) * Gm::SLOT, lane);
       wait_vm<Rg::WAIT>();
-      const float* sl = ring + (c % R) * Gm::SLOT;
+      read_fb_chunk<K, W16, true>(ring + (c % R) * Gm::SLOT, lm, av, dv, xv);
       const int d0 = k * HC;
-#pragma unroll
-      for (int s = HC - 1; s >= 0; --s) {
-        const int t = d0 + s - 1;
-        if (s == 0 && k == 0) continue;  // t = -1
-        const int p = (s + 1) & 1;       // parity of t
-        float a = sl[lm.a_off[p] + s * K * K];
-        a = lm.a_ok[p] ? a : NEG_INF;
-        float e = sl[lm.e_off[p] + s * K];
-        e = lm.e_ok[p] ? e : 0.f;
-        const float v = (a + e) + be;
-        float m, nu, sm;
-        if (p == 0) {  // reduce over j = g % KP
-          m = allred<KP, true>(v, OpMax{});
-          nu = allred<KP, true>(be, OpMax{});
-        } else {
-          m = allred<KP, false>(v, OpMax{});
-          nu = allred<KP, false>(be, OpMax{});
-        }
-        const float mm = fmaxf(m, F32_LOWEST);
-        const float x = __expf(v - mm);
-        sm = p == 0 ? allred<KP, true>(x, OpAdd{}) : allred<KP, false>(x, OpAdd{});
-        const float r = mm + __logf(sm);
-        const float nus = nu == NEG_INF ? 0.f : nu;
-        if (t < L - 1) be = r - nus;
-        // lanes with j-coordinate 0 hold state i's value once each; slot s <-> be'[t + 1]
-        const bool wr = p == 0 ? (g % KP == 0) : (g < KP);
-        const int is = p == 0 ? g / KP : g;
-        if (wr && is < K) vbuf[grp * HC * K + s * K + is] = be;
+      const float be_c = be;
+      rng = 0.f;
+      if (d0 + HC <= Lmin) steps(d0, k == 0, std::false_type{}, std::false_type{});
+      else steps(d0, k == 0, std::false_type{}, std::true_type{});
+      if (__builtin_amdgcn_ballot_w64(rng > FB_LIM)) {
+        be = be_c;
+        steps(d0, k == 0, std::true_type{}, std::true_type{});
       }
       flush(ws_be, d0);
     }
@@ -686,7 +769,7 @@ __global__ __launch_bounds__(128) void fwdbwd_kernel(const float* __restrict__ l
       float sm = 0.f;
 #pragma unroll
       for (int i = 0; i < K; ++i) {
-        x[i] = mx == NEG_INF ? 0.f : __expf(x[i] - mx);
+        x[i] = mx == NEG_INF ? 0.f : fexp2(x[i] - mx);
         sm += x[i];
       }
 #pragma unroll
