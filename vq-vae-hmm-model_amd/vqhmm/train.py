@@ -16,18 +16,39 @@ One step = elbo forward (+loss accumulate) -> elbo backward -> [RCCL
 all-reduce of the flat gradient when torch.distributed is initialised] ->
 fused Adam.  Everything in the step is HIP kernels from libvqhmm.so plus the
 collective; nothing syncs the host, so a fixed-shape step can be captured in a
-HIP graph (`capture()`).
+HIP graph (`capture()`).  Optionally (overlap_bwd / VQHMM_BWD_OVERLAP=1) the
+backward's weight gradients run on a side stream beside the data-gradient
+chain (`_backward_overlapped`).
 """
 import ctypes
+import os
 
 import torch
 
 from . import _ext
 from .model import _ptr_array, param_offsets
 
+# Backward stage ids (csrc/api.hip `Stage`).  The data-gradient chain runs on the
+# launch stream; each weight gradient runs on a side stream as soon as the chain
+# stage that produces its dY has run (W_PAR only needs the forward's dpar).
+S_PAR_DG, S_DEC2_DG, S_DEC1_DG, S_LOGIT_BWD, S_LOGIT_DG, S_ENC2_DG = 8, 9, 10, 11, 12, 13
+S_W_PAR, S_W_DEC2, S_W_DEC1, S_W_LOGIT, S_W_ENC2, S_W_ENC1 = 14, 15, 16, 17, 18, 19
+S_REDUCE, S_COMPOSE_BWD, S_LOGPRIOR = 20, 21, 22
+BWD_CHAIN = ((S_PAR_DG, S_W_DEC2), (S_DEC2_DG, S_W_DEC1), (S_DEC1_DG, None), (S_LOGIT_BWD, S_W_LOGIT),
+             (S_LOGIT_DG, S_W_ENC2), (S_ENC2_DG, S_W_ENC1))
+
+
+def _overlap_default():
+    # Off by default: measured on MI355X at cfg2 the overlapped step is slower
+    # (0.702 vs 0.679 ms graphed, 0.686 vs 0.672 ms eager; profiles/r01/bwd_overlap_ab.txt):
+    # every conv/wgrad kernel is persistent and already fills all 256 CUs, so
+    # running two at once only adds contention.
+    return os.environ.get("VQHMM_BWD_OVERLAP", "0") == "1"
+
 
 class TrainState:
-    def __init__(self, model, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, process_group=None, distributed=None):
+    def __init__(self, model, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, process_group=None, distributed=None,
+                 overlap_bwd=None):
         params = model.ordered_parameters()
         dev = params[0].device
         if dev.type != "cuda":
@@ -57,6 +78,9 @@ class TrainState:
         self.distributed = bool(distributed)
         self.pg = process_group
         self.world = torch.distributed.get_world_size(process_group) if self.distributed else 1
+        self.overlap_bwd = _overlap_default() if overlap_bwd is None else bool(overlap_bwd)
+        self._side = None
+        self._bwd_events = None
 
     # ----------------------------------------------------------------- helpers
     def workspace(self, B, T):
@@ -88,8 +112,48 @@ class TrainState:
         _ext.check(self.lib.vqhmm_elbo_fwd_f32(d, self.ptrs, _ext.ptr(x), _ext.ptr(u), lay, _ext.ptr(lengths), B, T,
                                                float(beta), 1, _ext.ptr(ws), ws.numel(), _ext.ptr(self.loss),
                                                _ext.ptr(self.epoch_acc), st), "elbo forward")
-        _ext.check(self.lib.vqhmm_elbo_bwd_f32(d, self.ptrs, _ext.ptr(x), B, T, float(beta), None, _ext.ptr(ws),
-                                               ws.numel(), _ext.ptr(self.grad), st), "elbo backward")
+        if self.overlap_bwd:
+            self._backward_overlapped(x, B, T, beta, ws)
+        else:
+            _ext.check(self.lib.vqhmm_elbo_bwd_f32(d, self.ptrs, _ext.ptr(x), B, T, float(beta), None, _ext.ptr(ws),
+                                                   ws.numel(), _ext.ptr(self.grad), st), "elbo backward")
+
+    def _backward_overlapped(self, x, B, T, beta, ws):
+        """vqhmm_elbo_bwd_f32's stages with the weight gradients on a side stream.
+
+        A wgrad only reads its chain dY buffer and saved activations and writes its
+        own slabs, so each starts right after its dY is produced and runs beside the
+        next dgrads; the side stream joins before reduce_slabs.  Same kernels, same
+        fixed-order slab sums: bit-identical to the serial order.  Works eagerly and
+        under HIP-graph capture (the fork/join become graph edges)."""
+        main = torch.cuda.current_stream(self.device)
+        if self._side is None:
+            self._side = torch.cuda.Stream(self.device)
+            self._bwd_events = [torch.cuda.Event() for _ in range(len(BWD_CHAIN) + 1)]
+        side, ev = self._side, self._bwd_events
+        d = ctypes.byref(self.dims)
+        xp, wsp, gp = _ext.ptr(x), _ext.ptr(ws), _ext.ptr(self.grad)
+
+        def run(stage, stream):
+            _ext.check(self.lib.vqhmm_elbo_stage_f32(d, self.ptrs, xp, None, 0, None, B, T, float(beta), wsp,
+                                                     ws.numel(), gp, stage, ctypes.c_void_p(stream.cuda_stream)),
+                       "elbo backward")
+
+        ev[0].record(main)
+        side.wait_event(ev[0])
+        run(S_W_PAR, side)
+        k = 1
+        for chain_stage, wgrad in BWD_CHAIN:
+            run(chain_stage, main)
+            if wgrad is not None:
+                ev[k].record(main)
+                side.wait_event(ev[k])
+                run(wgrad, side)
+                k += 1
+        ev[k].record(side)
+        main.wait_event(ev[k])
+        for stage in (S_REDUCE, S_COMPOSE_BWD, S_LOGPRIOR):
+            run(stage, main)
 
     def reduce_gradients(self):
         if self.distributed and self.world > 1:
