@@ -1,7 +1,7 @@
 """Turn a tools/pmc.py result (per-kernel mean FETCH_SIZE / WRITE_SIZE per dispatch) into
 profiles/pmc_traffic.json, the per-stage HBM traffic bench.py reports as roofline.traffic.
 
-    python tools/make_pmc_traffic.py gpurun_out/pmc_step.json profiles/pmc_traffic.json
+    python tools/make_pmc_traffic.py SRC.json [SRC2.json ...] profiles/pmc_traffic.json
 
 Only stages that are ONE kernel launch (and whose kernel serves no other stage) are mapped.
 FETCH_SIZE and WRITE_SIZE are rocprofv3 derived counters in KB; on gfx950 FETCH_SIZE counts half the
@@ -17,13 +17,17 @@ MAP = {
     ("cfg2", "inputs_to_pcl"): "to_pcl_kernel",
     ("cfg2", "reduce_slabs"): "reduce_slabs_kernel",
     ("cfg2", "logits_bwd"): "logits_bwd_kernel",
-    ("vq_cfg3", "vq_argmin"): "vq_rows_kernel<16, 2",
+    ("vq_cfg3", "vq_argmin"): "vq_rows_kernel<16, 2, false",
+    ("viterbi_cfg5", "viterbi_cfg5"): "viterbi_kernel<8, true>",
+    ("fwdbwd_cfg4", "fwdbwd_cfg4"): "fwdbwd_kernel<8, true>",
 }
 
 
 def main():
-    src, dst = sys.argv[1], sys.argv[2]
-    per_kernel = json.load(open(src))
+    srcs, dst = sys.argv[1:-1], sys.argv[-1]
+    per_kernel = {}
+    for src in srcs:
+        per_kernel.update(json.load(open(src)))
     out = {}
     for (sec, key), sub in MAP.items():
         hits = [v for k, v in per_kernel.items() if sub in k]
@@ -32,7 +36,7 @@ def main():
         h = hits[0]
         out.setdefault(sec, {})[key] = round(2 * h["FETCH_SIZE"] * 1024 + h["WRITE_SIZE"] * 1024)
     out["_note"] = ("HBM bytes per launch = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (rocprofv3 --pmc, separate passes, "
-                    "gfx950 FETCH correction); source " + src)
+                    "gfx950 FETCH correction); sources " + ", ".join(srcs))
     json.dump(out, open(dst, "w"), indent=1, sort_keys=True)
     print(json.dumps(out, indent=1))
 
