@@ -149,6 +149,15 @@ int vqhmm_adam_f32(float* param, const float* grad, float* exp_avg, float* exp_a
                    double lr, double beta1, double beta2, double eps, int64_t* step, float grad_scale,
                    void* stream);
 
+/* ---------------------------------------------------------- data step ----
+ * RandomChunkDataset.__getitem__ (:25-29) + collate_fn (:164-179) on the
+ * device: out (B, C, Tmax) = zero-padded chunks, out[i,c,t] = t < L_i ?
+ * src[base_i + c*n_i + s_i + t] : 0, with meta (B x 4 int64, device) =
+ * {base_i, n_i, s_i, L_i} per sample (a row-major (C, n_i) sequence at element
+ * base_i of src, chunk start s_i, length L_i).  Bit-identical to collate_fn. */
+int vqhmm_gather_chunks_f32(const float* src, const int64_t* meta, int64_t B, int64_t C, int64_t Tmax,
+                            float* out, void* stream);
+
 /* ---------------------------------------------------------- inference ----
  * VAE_HMM.encode (:100, Encoder.forward :38-41): x (B,D,T) -> logits (B,K,T)
  * VAE_HMM.decode (:103, Decoder.forward :81-90): q (B,K,T) -> mu, logvar (B,D,T)

@@ -235,3 +235,27 @@ def test_backward_overlap_bit_identical():
     torch.cuda.synchronize()
     assert torch.equal(serial.grad, graphed.grad)
     assert torch.equal(serial.flat, graphed.flat)
+
+
+def test_infer_and_hard_regimes():
+    """inference_api/app.py:56-73 response and backtesting.py:154-155 regimes."""
+    import vqhmm
+    g = load_golden("cfg1_trained")
+    m = make_model(g)
+    x = torch.tensor(g["x"])
+    out = vqhmm.infer(m, x[0].tolist())
+    assert set(out) == {"mu", "logvar", "regime_probs"}
+    with torch.no_grad():
+        (mu, lv), q = m(x[:1].cuda())
+    assert np.array_equal(np.array(out["mu"], np.float32), mu[0].cpu().numpy())
+    assert np.array_equal(np.array(out["regime_probs"], np.float32), q[0].cpu().numpy())
+    assert_close(np.array(out["regime_probs"]), g["forward/q"][0], 1e-6, "q", atol=1e-7)
+    reg, q = vqhmm.hard_regimes(m, x.cuda())
+    ref = torch.softmax(torch.tensor(g["fwd/logits"]), dim=1).argmax(dim=1)
+    srt = np.sort(q.cpu().numpy(), axis=1)
+    clear = (srt[:, -1] - srt[:, -2]) > 1e-6  # positions whose top-2 are not within fp32 noise
+    assert np.array_equal(reg.cpu().numpy()[clear], ref.numpy()[clear])
+    assert torch.equal(reg, q.argmax(dim=1))
+    u = torch.tensor(g["u"]).cuda()
+    path, score = vqhmm.viterbi_regimes(m, x.cuda(), u)
+    assert path.shape == x[:, 0].shape and (path >= 0).all() and (path < q.shape[1]).all()

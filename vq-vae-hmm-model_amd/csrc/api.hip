@@ -530,6 +530,13 @@ int vqhmm_adam_f32(float* param, const float* grad, float* exp_avg, float* exp_a
                      (hipStream_t)stream);
 }
 
+int vqhmm_gather_chunks_f32(const float* src, const int64_t* meta, int64_t B, int64_t C, int64_t Tmax, float* out,
+                            void* stream) {
+  if (B < 0 || C < 0 || Tmax < 0 || C > INT32_MAX || Tmax > INT32_MAX) return VQHMM_EINVAL;
+  if (B * C * Tmax > 0 && (!src || !meta || !out)) return VQHMM_EINVAL;
+  return launch_gather_chunks(src, meta, B, C, Tmax, out, (hipStream_t)stream);
+}
+
 // ---------------------------------------------------------------- inference surface
 int vqhmm_infer_workspace_size(const vqhmm_dims_t* d, int64_t B, int64_t T, size_t* bytes) {
   if (!dims_ok(d) || B < 0 || T < 0 || !bytes) return VQHMM_EINVAL;

@@ -142,6 +142,8 @@ int launch_log_prior_grad(const float* q0sum, const float* log_prior, int K, flo
 // CF / (B,T,C) tensor -> PCL (R, ld4(C)) with zero pad rows / channels:
 // dst[b*(T+2)+1+t][c] = src[b*C*T + c*sc + t*st]
 int launch_to_pcl(const float* src, int C, int64_t B, int T, int64_t sc, int64_t st, float* dst, hipStream_t s);
+int launch_gather_chunks(const float* src, const int64_t* meta, int64_t B, int64_t C, int64_t Tm, float* out,
+                         hipStream_t s);
 int launch_log_softmax_vec(const float* x, int K, float* out, hipStream_t s);
 size_t viterbi_ws_bytes(int64_t B, int64_t T, int64_t K);
 size_t fwdbwd_ws_bytes(int64_t B, int64_t T, int64_t K);

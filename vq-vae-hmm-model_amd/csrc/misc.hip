@@ -299,3 +299,33 @@ int launch_to_pcl(const float* src, int C, int64_t B, int T, int64_t sc, int64_t
   return VQHMM_OK;
 }
 }  // namespace vqhmm
+
+// ------------------------------------------------------------ data step
+// Device-side RandomChunkDataset.__getitem__ + collate_fn (VQ_VAE_HMM_fixed.py:
+// 25-29, 164-179): out (B, C, Tm) with
+//   out[i, c, t] = t < L_i ? src[base_i + c * n_i + s_i + t] : 0,
+// meta_i = {base_i, n_i, s_i, L_i}: sample i is columns [s_i, s_i + L_i) of a
+// row-major (C, n_i) sequence stored at element base_i of src.  Consecutive
+// threads walk t, so reads and writes are contiguous runs.
+namespace vqhmm {
+__global__ __launch_bounds__(256) void gather_chunks_kernel(const float* __restrict__ src,
+                                                            const int64_t* __restrict__ meta, int64_t B, int C,
+                                                            int Tm, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= B * C * (int64_t)Tm) return;
+  const int t = (int)(i % Tm);
+  const int64_t r = i / Tm;
+  const int c = (int)(r % C);
+  const int64_t* m = meta + (r / C) * 4;
+  out[i] = t < m[3] ? src[m[0] + c * m[1] + m[2] + t] : 0.f;
+}
+
+int launch_gather_chunks(const float* src, const int64_t* meta, int64_t B, int64_t C, int64_t Tm, float* out,
+                         hipStream_t s) {
+  const int64_t n = B * C * Tm;
+  if (n == 0) return VQHMM_OK;
+  gather_chunks_kernel<<<(unsigned)cdiv(n, 256), 256, 0, s>>>(src, meta, B, (int)C, (int)Tm, out);
+  VQHMM_LAUNCH_CHECK();
+  return VQHMM_OK;
+}
+}  // namespace vqhmm
