@@ -91,7 +91,7 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a, int64_t m0, in
             if (n0 + v < a.N) a.out_cf[(b * a.N + n0 + v) * a.T + t] = y[v];
         }
       }
-      if (tail) {
+      if (tail) {  // compile-time in every caller
         // z^T (16 c2 x 16 rows) = tW (16 x N) @ Y^T: B operand = the fragments above
         f32x4 z = tb0;
 #pragma unroll
@@ -140,8 +140,17 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a, int64_t m0, in
     }
 }
 
-template <int NB, int KCP, int KS, int PB>
-__global__ __launch_bounds__(256, 1) void conv2_kernel(ConvArgs a, int64_t ntiles) {
+// Waves per SIMD the register budget is sized for: the narrow-input layers are
+// latency/HBM-bound and their LDS footprint allows 4 workgroups per CU, so they
+// are held to 128 VGPRs (ACT / TAIL are template parameters, so a variant only
+// keeps the epilogue state it uses); the 64-wide layers are LDS-limited to 2 per CU.
+template <int NB, int KCP, bool TAIL>
+struct C2Occ {
+  static constexpr int W = (KCP <= 2 && !TAIL) ? 4 : 1;
+};
+
+template <int NB, int KCP, int KS, int PB, int ACT, bool TAIL>
+__global__ __launch_bounds__(256, (C2Occ<NB, KCP, TAIL>::W)) void conv2_kernel(ConvArgs a, int64_t ntiles) {
   using C = C2Cfg<NB, KCP, KS, PB>;
   extern __shared__ float4 smem4[];
   float* Ws = reinterpret_cast<float*>(smem4);  // [KS][NW][LDX]
@@ -166,10 +175,10 @@ __global__ __launch_bounds__(256, 1) void conv2_kernel(ConvArgs a, int64_t ntile
       const int n = nb * 16 + 4 * lg4 + v;
       bias_r[nb][v] = (a.bias && n < a.N) ? a.bias[n] : 0.f;
     }
-  const bool tail = a.tW != nullptr;
+  constexpr bool tail = TAIL;
   float tw[NB][4];
   f32x4 tb0 = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (tail) {
+  if constexpr (TAIL) {
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
@@ -203,7 +212,7 @@ __global__ __launch_bounds__(256, 1) void conv2_kernel(ConvArgs a, int64_t ntile
     __syncthreads();
     // epilogue operands of THIS tile first (older than the prefetch in the vmcnt order)
     float4 auxv[NB][PB] = {};
-    if (a.act == 2) {
+    if constexpr (ACT == 2) {
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
@@ -252,12 +261,7 @@ __global__ __launch_bounds__(256, 1) void conv2_kernel(ConvArgs a, int64_t ntile
           }
       }
     }
-    if (a.act == 2)
-      conv2_epilogue<NB, PB, 2>(a, m0, wave, lg4, l16, acc, auxv, bias_r, tw, tb0, sc, tail);
-    else if (a.act == 1)
-      conv2_epilogue<NB, PB, 1>(a, m0, wave, lg4, l16, acc, auxv, bias_r, tw, tb0, sc, tail);
-    else
-      conv2_epilogue<NB, PB, 0>(a, m0, wave, lg4, l16, acc, auxv, bias_r, tw, tb0, sc, tail);
+    conv2_epilogue<NB, PB, ACT>(a, m0, wave, lg4, l16, acc, auxv, bias_r, tw, tb0, sc, tail);
     tile = next;
   }
 }
@@ -266,36 +270,40 @@ bool conv2_supported(const ConvArgs& a) {
   return !a.src_cf && a.N <= 64 && a.Kc <= 64 && (a.tW == nullptr || a.C2 <= 16);
 }
 
-template <int NB, int KCP, int KS, int PB>
-static int launch_c2p(const ConvArgs& a, hipStream_t s) {
+template <int NB, int KCP, int KS, int PB, int ACT, bool TAIL>
+static int launch_c2v(const ConvArgs& a, hipStream_t s) {
   using C = C2Cfg<NB, KCP, KS, PB>;
   const int64_t ntiles = cdiv(a.R, C::BM);
   int per_cu = (int)((160 * 1024) / C::LDS);
   if (per_cu < 1) return VQHMM_EUNSUPPORTED;
   if (per_cu > 4) per_cu = 4;
   const int64_t grid = ntiles < 256LL * per_cu ? ntiles : 256LL * per_cu;
-  conv2_kernel<NB, KCP, KS, PB><<<(unsigned)grid, 256, C::LDS, s>>>(a, ntiles);
+  conv2_kernel<NB, KCP, KS, PB, ACT, TAIL><<<(unsigned)grid, 256, C::LDS, s>>>(a, ntiles);
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
 }
 
-// rows per tile = 64*PB; PB = 1 halves the X tile so two workgroups fit per CU
-// (tuning override: VQHMM_CONV2_PB=1|2, read once)
-static int conv2_pb() {
-  static int pb = [] {
-    const char* e = getenv("VQHMM_CONV2_PB");
-    return (e && e[0] == '1') ? 1 : (e && e[0] == '2') ? 2 : 0;
-  }();
-  return pb;
+// epilogue variants in use: forward ReLU (+ fused 1x1 tail on k=3), dgrad with
+// the producer's ReLU mask, plain dgrad
+template <int NB, int KCP, int KS, int PB>
+static int launch_c2p(const ConvArgs& a, hipStream_t s) {
+  const bool tail = a.tW != nullptr;
+  if (tail) {
+    if constexpr (KS == 3) {
+      if (a.act == 1) return launch_c2v<NB, KCP, KS, PB, 1, true>(a, s);
+    }
+    return VQHMM_EUNSUPPORTED;
+  }
+  if (a.act == 2) return launch_c2v<NB, KCP, KS, PB, 2, false>(a, s);
+  if (a.act == 1) return launch_c2v<NB, KCP, KS, PB, 1, false>(a, s);
+  return launch_c2v<NB, KCP, KS, PB, 0, false>(a, s);
 }
 
+// rows per tile = 64*PB; PB = 1 (measured best: it halves the X tile so more
+// workgroups fit per CU)
 template <int NB, int KCP, int KS>
 static int launch_c2(const ConvArgs& a, hipStream_t s) {
-  const int pb = conv2_pb();
-  const bool big = NB * KCP >= 8;  // default: PB=1 for the 64x64 layers (2 WG/CU), PB=2 otherwise
-  (void)big;
-  if (pb != 2) return launch_c2p<NB, KCP, KS, 1>(a, s);
-  return launch_c2p<NB, KCP, KS, 2>(a, s);
+  return launch_c2p<NB, KCP, KS, 1>(a, s);
 }
 
 template <int NB, int KS>
