@@ -73,8 +73,8 @@ def stage_timings(lib, st, x, u, L, B, T, beta, nsteps):
     for k in range(nsteps):
         for s in range(n):
             ev[k][s].record(stream)
-            _ext.check(lib.vqhmm_elbo_stage_f32(d, st.ptrs, _ext.ptr(x), _ext.ptr(u), lay, _ext.ptr(L), B, T,
-                                                float(beta), _ext.ptr(ws), ws.numel(), _ext.ptr(st.grad), s, sp),
+            _ext.check(lib.vqhmm_elbo_stage_f32(d, st.ptrs, _ext.ptr(x), _ext.ptr(u), lay, _ext.ptr(L), None, B,
+                                                T, float(beta), _ext.ptr(ws), ws.numel(), _ext.ptr(st.grad), s, sp),
                        "stage")
         ev[k][n].record(stream)
         st.apply_adam()

@@ -113,15 +113,20 @@ int vqhmm_fwdbwd_f32(const float* log_pi, const float* log_A, const float* em, c
  * loss: device fp32 scalar; loss_accum (nullable): device fp64 scalar += loss
  *   (train_model's epoch_loss, :158, without a per-step host sync).
  * need_grad = 0 computes only the loss.
+ * norm: NULL, or a device int64[2] {valid_count, batch} replacing the batch's own
+ *   loss normalisers mask.sum() (:120) and B (:131, :135).  Pass the GLOBAL batch's
+ *   values when this batch is one shard of it: the shards' losses and gradients then
+ *   SUM to the global batch's exactly (data parallel over ragged batches).  The
+ *   backward must get the same norm as its forward.
  * Backward: grad (flat fp32, vqhmm_param_layout order) = grad_scale * dloss/dparams,
  *   grad_scale a device fp32 scalar (autograd's grad_output) or NULL for 1. */
 int vqhmm_elbo_workspace_size(const vqhmm_dims_t* dims, int64_t B, int64_t T, size_t* bytes);
 int vqhmm_elbo_fwd_f32(const vqhmm_dims_t* dims, const float* const* params, const float* x,
-                       const float* u, int u_layout, const int64_t* lengths, int64_t B, int64_t T,
+                       const float* u, int u_layout, const int64_t* lengths, const int64_t* norm, int64_t B, int64_t T,
                        float beta, int need_grad, void* workspace, size_t ws_bytes,
                        float* loss, double* loss_accum, void* stream);
 int vqhmm_elbo_bwd_f32(const vqhmm_dims_t* dims, const float* const* params, const float* x,
-                       int64_t B, int64_t T, float beta, const float* grad_scale,
+                       const int64_t* norm, int64_t B, int64_t T, float beta, const float* grad_scale,
                        void* workspace, size_t ws_bytes, float* grad, void* stream);
 /* Device addresses (inside the workspace) of the last forward's loss and of its
  * pieces [recon, prior, entropy] (for tests).  Host-only, no GPU access. */
@@ -136,8 +141,8 @@ int vqhmm_elbo_num_stages(void);
 int vqhmm_elbo_stage_info(const vqhmm_dims_t* dims, int64_t B, int64_t T, int stage, char* name,
                           size_t name_len, double* flops, double* bytes, int* mfma_bound);
 int vqhmm_elbo_stage_f32(const vqhmm_dims_t* dims, const float* const* params, const float* x,
-                         const float* u, int u_layout, const int64_t* lengths, int64_t B, int64_t T,
-                         float beta, void* workspace, size_t ws_bytes, float* grad, int stage,
+                         const float* u, int u_layout, const int64_t* lengths, const int64_t* norm,
+                         int64_t B, int64_t T, float beta, void* workspace, size_t ws_bytes, float* grad, int stage,
                          void* stream);
 
 /* torch.optim.Adam step (no weight decay / amsgrad; train_model uses the

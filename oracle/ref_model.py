@@ -89,8 +89,12 @@ def decoder_params(p, q):
     return out[:, :half, :], out[:, half:, :]
 
 
-def elbo_terms(p, x, u, lengths, K, u_dim):
-    """Returns the named pieces of the mean-field ELBO (reference :106-135)."""
+def elbo_terms(p, x, u, lengths, K, u_dim, norm=None):
+    """Returns the named pieces of the mean-field ELBO (reference :106-135).
+
+    norm=(valid_count, batch) replaces the batch's own normalisers mask.sum()
+    (:120) and B (:131 .mean(), :135) by a global batch's (data-parallel shard
+    of it; the product's `norm` argument, include/vqhmm.h).  None = reference."""
     nb, nc, nt = x.shape
     if lengths is None:
         raise ValueError("lengths required")
@@ -102,7 +106,10 @@ def elbo_terms(p, x, u, lengths, K, u_dim):
 
     var = logvar.exp().clamp(min=1e-8)
     nll = 0.5 * (torch.log(2 * math.pi * var) + (mu - x) ** 2 / var)
-    recon = (nll * valid.unsqueeze(1).float()).sum() / (valid.sum() * nc).clamp(min=1.0)
+    if norm is None:
+        recon = (nll * valid.unsqueeze(1).float()).sum() / (valid.sum() * nc).clamp(min=1.0)
+    else:
+        recon = (nll * valid.unsqueeze(1).float()).sum() / max(float(norm[0]) * nc, 1.0)
 
     first = (q[:, :, 0] * log_pi.unsqueeze(0)).sum(dim=1)
     q_from = q[:, :, :-1].permute(0, 2, 1).unsqueeze(-1)
@@ -110,17 +117,17 @@ def elbo_terms(p, x, u, lengths, K, u_dim):
     step = (q_from * q_to * log_A[:, 1:]).sum(dim=(2, 3))
     pair_valid = (valid[:, 1:] & valid[:, :-1]).float()
     chain = (step * pair_valid).sum(dim=1)
-    prior_loss = -(first + chain).mean()
+    prior_loss = -(first + chain).mean() if norm is None else -(first + chain).sum() / float(norm[1])
 
     ent = -(q * F.log_softmax(logits, dim=1)).sum(dim=1)
-    ent = (ent * valid.float()).sum() / nb
+    ent = (ent * valid.float()).sum() / (nb if norm is None else float(norm[1]))
     return dict(recon=recon, prior=prior_loss, entropy=ent, logits=logits, q=q,
                 mu=mu, logvar=logvar, log_pi=log_pi, log_A=log_A)
 
 
-def elbo(p, x, u, lengths, beta, K, u_dim):
+def elbo(p, x, u, lengths, beta, K, u_dim, norm=None):
     """Scalar loss = recon + beta*(prior - entropy).  Reference :137."""
-    t = elbo_terms(p, x, u, lengths, K, u_dim)
+    t = elbo_terms(p, x, u, lengths, K, u_dim, norm)
     return t["recon"] + beta * (t["prior"] - t["entropy"])
 
 

@@ -145,7 +145,7 @@ ConvArgs conv_base(const ElboPlan& p) {
 
 extern "C" {
 
-int32_t vqhmm_abi_version(void) { return 1; }
+int32_t vqhmm_abi_version(void) { return 2; }
 
 int vqhmm_param_layout(const vqhmm_dims_t* d, int64_t off[VQHMM_NPARAMS + 1]) {
   if (!dims_ok(d) || !off) return VQHMM_EINVAL;
@@ -233,6 +233,7 @@ struct StepCtx {
   const float* u;
   int u_layout;
   const int64_t* lengths;
+  const int64_t* norm;  // null or device {valid_count, batch} (kernels.h loss_norm_batch)
   float beta;
   int need_grad;
   float* loss;
@@ -298,7 +299,7 @@ int run_staged_head(const ElboPlan& p, const StepCtx& c, const float* const* w, 
   h.B = p.B; h.T = p.T; h.R = p.R; h.D = p.D; h.K = p.K;
   h.x = p.xp; h.par = p.par; h.logits = p.logits; h.q = p.q; h.lengths = c.lengths;
   h.log_prior = w[LOG_PRIOR]; h.log_pi = p.logpi; h.lgA = p.lgA; h.nx = p.nx; h.dqc = p.dqc; h.trw = p.trw;
-  h.cpri = -c.beta / (float)p.B; h.cent = c.beta / (float)p.B; h.need_grad = c.need_grad;
+  h.beta = c.beta; h.norm = c.norm; h.need_grad = c.need_grad;
   h.dpar = p.dpar; h.dlx = p.dlx; h.dqx = p.dqx; h.part = p.part; h.q0 = p.sq0;
   if ((rc = launch_staged_head(h, p.hgrid, s))) return rc;
   if (!c.need_grad) return VQHMM_OK;
@@ -342,13 +343,13 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       h.x = p.xp; h.u = p.up;
       h.lengths = c.lengths; h.par = p.par; h.logits = p.logits; h.q = p.q;
       h.W1 = w[TN0_W]; h.b1 = w[TN0_B]; h.W2 = w[TN2_W]; h.b2 = w[TN2_B]; h.log_prior = w[LOG_PRIOR];
-      h.beta = c.beta; h.need_grad = c.need_grad;
+      h.beta = c.beta; h.norm = c.norm; h.need_grad = c.need_grad;
       h.dpar = p.dpar; h.dqx = p.dqx; h.dlx = p.dlx; h.part = p.part;
       h.slab_W1 = p.sW1; h.slab_b1 = p.sb1; h.slab_W2 = p.sW2; h.slab_b2 = p.sb2; h.slab_q0 = p.sq0;
       return launch_head(h, p.hgrid, s);
     }
     case S_FINAL:
-      return launch_finalize_loss(p.part, p.hgrid, c.lengths, p.B, p.T, p.D, c.beta, c.loss, c.loss_accum,
+      return launch_finalize_loss(p.part, p.hgrid, c.lengths, c.norm, p.B, p.T, p.D, c.beta, c.loss, c.loss_accum,
                                   p.pieces, s);
     case S_LOGIT_BWD:
       return launch_logits_bwd(p.q, p.dqd, p.dqx, p.dlx, c.gscale, p.R, p.K, p.dlog, s);
@@ -411,7 +412,7 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       int64_t off[VQHMM_NPARAMS + 1];
       vqhmm_dims_t d{p.D, p.H, p.K, p.H2, p.U, p.TH};
       vqhmm_param_layout(&d, off);
-      return launch_log_prior_grad(p.q0sum, w[LOG_PRIOR], p.K, -c.beta / (float)p.B, c.gscale, c.g + off[LOG_PRIOR],
+      return launch_log_prior_grad(p.q0sum, w[LOG_PRIOR], p.K, c.beta, c.norm, p.B, c.gscale, c.g + off[LOG_PRIOR],
                                    s);
     }
   }
@@ -461,25 +462,26 @@ void stage_work(const ElboPlan& p, int st, double* flops, double* bytes, int* mf
 extern "C" {
 
 int vqhmm_elbo_fwd_f32(const vqhmm_dims_t* d, const float* const* w, const float* x, const float* u, int u_layout,
-                       const int64_t* lengths, int64_t B, int64_t T, float beta, int need_grad, void* ws,
-                       size_t ws_bytes, float* loss, double* loss_accum, void* stream) {
+                       const int64_t* lengths, const int64_t* norm, int64_t B, int64_t T, float beta, int need_grad,
+                       void* ws, size_t ws_bytes, float* loss, double* loss_accum, void* stream) {
   if (!dims_ok(d) || !w || B <= 0 || T <= 0 || !x || !u || !lengths || !ws || !loss) return VQHMM_EINVAL;
   for (int i = 0; i < VQHMM_NPARAMS; ++i)
     if (!w[i]) return VQHMM_EINVAL;
   ElboPlan p = plan_elbo(d, B, T, ws);
   if (ws_bytes < p.bytes) return VQHMM_EWORKSPACE;
-  StepCtx c{w, x, u, u_layout, lengths, beta, need_grad, loss, loss_accum, nullptr, nullptr};
+  StepCtx c{w, x, u, u_layout, lengths, norm, beta, need_grad, loss, loss_accum, nullptr, nullptr};
   for (int st = FWD_FIRST; st <= FWD_LAST; ++st)
     if (int rc = run_stage(p, c, st, (hipStream_t)stream)) return rc;
   return VQHMM_OK;
 }
 
-int vqhmm_elbo_bwd_f32(const vqhmm_dims_t* d, const float* const* w, const float* x, int64_t B, int64_t T,
-                       float beta, const float* grad_scale, void* ws, size_t ws_bytes, float* g, void* stream) {
+int vqhmm_elbo_bwd_f32(const vqhmm_dims_t* d, const float* const* w, const float* x, const int64_t* norm, int64_t B,
+                       int64_t T, float beta, const float* grad_scale, void* ws, size_t ws_bytes, float* g,
+                       void* stream) {
   if (!dims_ok(d) || !w || B <= 0 || T <= 0 || !x || !ws || !g) return VQHMM_EINVAL;
   ElboPlan p = plan_elbo(d, B, T, ws);
   if (ws_bytes < p.bytes) return VQHMM_EWORKSPACE;
-  StepCtx c{w, x, nullptr, 0, nullptr, beta, 1, nullptr, nullptr, grad_scale, g};
+  StepCtx c{w, x, nullptr, 0, nullptr, norm, beta, 1, nullptr, nullptr, grad_scale, g};
   for (int st = BWD_FIRST; st <= BWD_LAST; ++st)
     if (int rc = run_stage(p, c, st, (hipStream_t)stream)) return rc;
   return VQHMM_OK;
@@ -505,12 +507,12 @@ int vqhmm_elbo_stage_info(const vqhmm_dims_t* d, int64_t B, int64_t T, int stage
 }
 
 int vqhmm_elbo_stage_f32(const vqhmm_dims_t* d, const float* const* w, const float* x, const float* u, int u_layout,
-                         const int64_t* lengths, int64_t B, int64_t T, float beta, void* ws, size_t ws_bytes,
-                         float* grad, int stage, void* stream) {
+                         const int64_t* lengths, const int64_t* norm, int64_t B, int64_t T, float beta, void* ws,
+                         size_t ws_bytes, float* grad, int stage, void* stream) {
   if (!dims_ok(d) || !w || !ws || stage < 0 || stage >= S_COUNT) return VQHMM_EINVAL;
   ElboPlan p = plan_elbo(d, B, T, ws);
   if (ws_bytes < p.bytes) return VQHMM_EWORKSPACE;
-  StepCtx c{w, x, u, u_layout, lengths, beta, 1, p.loss, nullptr, nullptr, grad};
+  StepCtx c{w, x, u, u_layout, lengths, norm, beta, 1, p.loss, nullptr, nullptr, grad};
   return run_stage(p, c, stage, (hipStream_t)stream);
 }
 

@@ -66,8 +66,9 @@ __global__ __launch_bounds__(256) void elbo_head_kernel(HeadArgs a) {
 
   const int tid = threadIdx.x;
   const int K = a.K, KK = K * K, D = a.D;
-  const float cpri = -a.beta / (float)a.B;  // d loss / d (init + trans)[b]
-  const float cent = a.beta / (float)a.B;   // d loss / d (sum q*log q)
+  const float Bn = loss_norm_batch(a.norm, a.B);
+  const float cpri = -a.beta / Bn;  // d loss / d (init + trans)[b]
+  const float cent = a.beta / Bn;   // d loss / d (sum q*log q)
 
   // log_pi = log_softmax(log_prior); valid-count for the recon normaliser
   if (tid == 0) {
@@ -77,12 +78,12 @@ __global__ __launch_bounds__(256) void elbo_head_kernel(HeadArgs a) {
     for (int k = 0; k < K; ++k) s += __expf(a.log_prior[k] - m);
     const float l = m + __logf(s);
     for (int k = 0; k < K; ++k) lpS[k] = a.log_prior[k] - l;
-    cntS = 0;
+    cntS = a.norm ? (unsigned long long)a.norm[0] : 0ull;
   }
   __syncthreads();
   {
     unsigned long long c = 0;
-    for (int64_t b = tid; b < a.B; b += 256) {
+    for (int64_t b = tid; !a.norm && b < a.B; b += 256) {
       const int64_t L = a.lengths[b];
       c += (unsigned long long)(L <= 0 ? 0 : (L < a.T ? L : a.T));
     }

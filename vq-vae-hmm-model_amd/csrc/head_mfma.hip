@@ -88,8 +88,9 @@ __global__ __launch_bounds__(256, 2) void elbo_head_mfma_kernel(HeadArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lg4 = lane >> 4, l16 = lane & 15;
   const int U = a.U, D = a.D;
-  const float cpri = -a.beta / (float)a.B;
-  const float cent = a.beta / (float)a.B;
+  const float Bn = loss_norm_batch(a.norm, a.B);
+  const float cpri = -a.beta / Bn;  // d loss / d (init + trans)[b]
+  const float cent = a.beta / Bn;   // d loss / d (sum q*log q)
 
   // ---- one-time: weights to LDS / registers, log_pi, valid count
   for (int i = tid; i < 16 * S::LDW2; i += 256) {
@@ -103,7 +104,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_mfma_kernel(HeadArgs a) {
     for (int k = 0; k < K; ++k) s += __expf(a.log_prior[k] - m);
     const float l = m + __logf(s);
     for (int k = 0; k < K; ++k) sh.lpS[k] = a.log_prior[k] - l;
-    sh.cnt = 0;
+    sh.cnt = a.norm ? (unsigned long long)a.norm[0] : 0ull;
   }
   for (int i = tid; i < TH * 8; i += 256) {
     const int h = i >> 3, c = i & 7;
@@ -117,7 +118,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_mfma_kernel(HeadArgs a) {
   __syncthreads();
   {
     unsigned long long c = 0;
-    for (int64_t b = tid; b < a.B; b += 256) {
+    for (int64_t b = tid; !a.norm && b < a.B; b += 256) {
       const int64_t L = a.lengths[b];
       c += (unsigned long long)(L <= 0 ? 0 : (L < a.T ? L : a.T));
     }

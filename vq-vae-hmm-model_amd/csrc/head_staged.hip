@@ -85,7 +85,7 @@ __global__ __launch_bounds__(256) void head_l1_kernel(StagedHeadArgs a) {
     }
     // log_softmax backward of d tr / d log_A = cpri w q_{t-1,i} q_{t,j}
     if (lane < K) {
-      const float ci = a.cpri * w * qp;
+      const float ci = -a.beta / loss_norm_batch(a.norm, a.B) * w * qp;
       const float rs = ci * sq;
       float* dst = row + lane * K;
 #pragma unroll
@@ -102,11 +102,11 @@ __global__ __launch_bounds__(256) void head_l2_kernel(StagedHeadArgs a) {
   __shared__ unsigned long long cnt;
   const int tid = threadIdx.x;
   const int K = a.K, D = a.D, LQ = ld4(K), LP = ld4(2 * D), LX = ld4(D);
-  if (tid == 0) cnt = 0;
+  if (tid == 0) cnt = a.norm ? (unsigned long long)a.norm[0] : 0ull;
   __syncthreads();
   {  // valid positions (the recon normaliser mask.sum() * C, VQ_VAE_HMM_fixed.py:120)
     unsigned long long c = 0;
-    for (int64_t b = tid; b < a.B; b += 256) {
+    for (int64_t b = tid; !a.norm && b < a.B; b += 256) {
       const int64_t L = a.lengths[b];
       c += (unsigned long long)(L <= 0 ? 0 : (L < a.T ? L : a.T));
     }
@@ -114,6 +114,7 @@ __global__ __launch_bounds__(256) void head_l2_kernel(StagedHeadArgs a) {
   }
   __syncthreads();
   const float inv_n = 1.0f / fmaxf((float)(cnt * (unsigned long long)D), 1.0f);
+  const float cpri = -a.beta / loss_norm_batch(a.norm, a.B), cent = a.beta / loss_norm_batch(a.norm, a.B);
   float s_rec = 0.f, s_init = 0.f, s_tr = 0.f, s_ent = 0.f;
   for (int64_t r = (int64_t)blockIdx.x * 256 + tid; r < a.R; r += (int64_t)gridDim.x * 256) {
     int64_t b;
@@ -152,10 +153,10 @@ __global__ __launch_bounds__(256) void head_l2_kernel(StagedHeadArgs a) {
       float dl = 0.f, dq = 0.f;
       if (valid && k < K) {
         const float qk = a.q[r * LQ + k];
-        if (m) dl = a.cent * qk * ((a.logits[r * LQ + k] - lse) - f);
-        dq = a.cpri * (a.dqc[r * LQ + k] + wn * a.nx[(r + 1) * LQ + k]);  // dqc already carries w_t
+        if (m) dl = cent * qk * ((a.logits[r * LQ + k] - lse) - f);
+        dq = cpri * (a.dqc[r * LQ + k] + wn * a.nx[(r + 1) * LQ + k]);  // dqc already carries w_t
         if (t == 0) {
-          dq = fmaf(a.cpri, a.log_pi[k], dq);
+          dq = fmaf(cpri, a.log_pi[k], dq);
           s_init = fmaf(qk, a.log_pi[k], s_init);
         }
       }

@@ -34,6 +34,14 @@ struct ConvArgs {
   float* q_cf;       // CF softmax of the tail
 };
 
+// Loss normalisers of compute_loss (VQ_VAE_HMM_fixed.py:120 mask.sum()*C, :131/:135 B).
+// norm == null: the batch's own valid count and B.  norm = device int64 {valid_count, batch}:
+// the normalisers of a larger global batch this batch is a shard of, so per-shard losses and
+// gradients SUM (all-reduce) to exactly the global batch's (data parallel over ragged batches).
+__device__ __forceinline__ float loss_norm_batch(const int64_t* norm, int64_t B) {
+  return norm ? (float)norm[1] : (float)B;
+}
+
 struct WgradArgs {
   const float* dy;   // PCL (R, ld4(N)) output gradient (pad rows zero)
   const float* x;    // layer input: PCL (R, ld4(C)) or CF (B, C, T) (generic kernel only)
@@ -63,6 +71,7 @@ struct HeadArgs {
   const float* b2;       // (K*K)
   const float* log_prior;// (K)
   float beta;
+  const int64_t* norm;   // null, or device {valid_count, batch}: global normalisers (see loss_norm)
   int need_grad;
   float* dpar;           // PCL (R, ld4(2D))
   float* dqx;            // PCL (R, ld4(K))  dL/dq from the prior term
@@ -114,7 +123,8 @@ struct StagedHeadArgs {
   float* log_pi;                      // (K) scratch
   float* lgA;                         // PCL (R, ld4(K*K)): transition logits in, d logits out
   float *nx, *dqc, *trw;              // PCL (R, ld4(K)) x2, (R)
-  float cpri, cent;                   // -beta / B, beta / B
+  float beta;
+  const int64_t* norm;                // null, or device {valid_count, batch} (see loss_norm)
   int need_grad;
   float *dpar, *dlx, *dqx;
   double* part;                       // [l2grid][4]
@@ -130,15 +140,15 @@ int launch_head_mfma(const HeadArgs& a, int grid, hipStream_t s);
 int launch_head(const HeadArgs& a, int grid, hipStream_t s);
 int launch_prior_fwd(const PriorArgs& p, hipStream_t s);
 int launch_reduce_slabs(const SlabSeg* segs, int n, hipStream_t s);
-int launch_finalize_loss(const double* part, int nblk, const int64_t* lengths, int64_t B, int T, int D, float beta,
-                         float* loss, double* accum, float* pieces, hipStream_t s);
+int launch_finalize_loss(const double* part, int nblk, const int64_t* lengths, const int64_t* norm, int64_t B, int T,
+                         int D, float beta, float* loss, double* accum, float* pieces, hipStream_t s);
 int launch_compose_fwd(const float* W, const float* E, int H, int K, float* Wc, hipStream_t s);
 int launch_compose_bwd(const float* dWc, const float* W, const float* E, int H, int K, float* dW, float* dE,
                        hipStream_t s);
 int launch_logits_bwd(const float* q, const float* dq_dec, const float* dqx, const float* dlx, const float* scale,
                       int64_t R, int K, float* dlog, hipStream_t s);
-int launch_log_prior_grad(const float* q0sum, const float* log_prior, int K, float c, const float* scale, float* out,
-                          hipStream_t s);
+int launch_log_prior_grad(const float* q0sum, const float* log_prior, int K, float beta, const int64_t* norm,
+                          int64_t B, const float* scale, float* out, hipStream_t s);
 // CF / (B,T,C) tensor -> PCL (R, ld4(C)) with zero pad rows / channels:
 // dst[b*(T+2)+1+t][c] = src[b*C*T + c*sc + t*st]
 int launch_to_pcl(const float* src, int C, int64_t B, int T, int64_t sc, int64_t st, float* dst, hipStream_t s);

@@ -62,13 +62,13 @@ int launch_reduce_slabs(const SlabSeg* segs, int n, hipStream_t s) {
 
 // ------------------------------------------------------------ loss finalize
 // part[nblk][4] = recon_sum, init_sum, trans_sum, ent_sum (ent_sum = sum of -sum_k q log q).
-__global__ void finalize_loss_kernel(const double* part, int nblk, const int64_t* lengths, int64_t B, int T, int D,
-                                     float beta, float* loss, double* accum, float* pieces) {
+__global__ void finalize_loss_kernel(const double* part, int nblk, const int64_t* lengths, const int64_t* norm,
+                                     int64_t B, int T, int D, float beta, float* loss, double* accum, float* pieces) {
   __shared__ double red[5][256];
   double v[5] = {0, 0, 0, 0, 0};
   for (int i = threadIdx.x; i < nblk; i += 256)
     for (int k = 0; k < 4; ++k) v[k] += part[i * 4 + k];
-  for (int64_t b = threadIdx.x; b < B; b += 256) {
+  for (int64_t b = threadIdx.x; !norm && b < B; b += 256) {
     const int64_t L = lengths[b];
     v[4] += (double)(L <= 0 ? 0 : (L < T ? L : T));
   }
@@ -80,10 +80,12 @@ __global__ void finalize_loss_kernel(const double* part, int nblk, const int64_t
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    const float ncount = fmaxf((float)(red[4][0] * D), 1.0f);
+    const double cnt = norm ? (double)norm[0] : red[4][0];
+    const double Bn = norm ? (double)norm[1] : (double)B;
+    const float ncount = fmaxf((float)(cnt * D), 1.0f);
     const float recon = (float)red[0][0] / ncount;
-    const float prior = -(float)((red[1][0] + red[2][0]) / (double)B);
-    const float ent = (float)(red[3][0] / (double)B);
+    const float prior = -(float)((red[1][0] + red[2][0]) / Bn);
+    const float ent = (float)(red[3][0] / Bn);
     const float l = recon + beta * (prior - ent);
     *loss = l;
     if (accum) *accum += (double)l;
@@ -91,9 +93,9 @@ __global__ void finalize_loss_kernel(const double* part, int nblk, const int64_t
   }
 }
 
-int launch_finalize_loss(const double* part, int nblk, const int64_t* lengths, int64_t B, int T, int D, float beta,
-                         float* loss, double* accum, float* pieces, hipStream_t s) {
-  finalize_loss_kernel<<<1, 256, 0, s>>>(part, nblk, lengths, B, T, D, beta, loss, accum, pieces);
+int launch_finalize_loss(const double* part, int nblk, const int64_t* lengths, const int64_t* norm, int64_t B, int T,
+                         int D, float beta, float* loss, double* accum, float* pieces, hipStream_t s) {
+  finalize_loss_kernel<<<1, 256, 0, s>>>(part, nblk, lengths, norm, B, T, D, beta, loss, accum, pieces);
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
 }
@@ -198,9 +200,10 @@ int launch_logits_bwd(const float* q, const float* dq_dec, const float* dqx, con
 
 // ------------------------------------------------------------ log_prior grad
 // dlog_prior = dlp - softmax(log_prior) * sum(dlp),  dlp = c * sum_b q[b,:,0],  c = -beta/B (:71,:123,:131)
-__global__ void log_prior_grad_kernel(const float* q0sum, const float* log_prior, int K, float c, const float* scale,
-                                      float* out) {
+__global__ void log_prior_grad_kernel(const float* q0sum, const float* log_prior, int K, float beta,
+                                      const int64_t* norm, int64_t B, const float* scale, float* out) {
   if (threadIdx.x != 0) return;
+  const float c = -beta / loss_norm_batch(norm, B);
   const float sc = scale ? *scale : 1.f;
   float m = -__builtin_inff();
   for (int k = 0; k < K; ++k) m = fmaxf(m, log_prior[k]);
@@ -211,9 +214,9 @@ __global__ void log_prior_grad_kernel(const float* q0sum, const float* log_prior
   for (int k = 0; k < K; ++k) out[k] = sc * (c * q0sum[k] - __expf(log_prior[k] - m) / se * tot);
 }
 
-int launch_log_prior_grad(const float* q0sum, const float* log_prior, int K, float c, const float* scale, float* out,
-                          hipStream_t s) {
-  log_prior_grad_kernel<<<1, 64, 0, s>>>(q0sum, log_prior, K, c, scale, out);
+int launch_log_prior_grad(const float* q0sum, const float* log_prior, int K, float beta, const int64_t* norm,
+                          int64_t B, const float* scale, float* out, hipStream_t s) {
+  log_prior_grad_kernel<<<1, 64, 0, s>>>(q0sum, log_prior, K, beta, norm, B, scale, out);
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
 }

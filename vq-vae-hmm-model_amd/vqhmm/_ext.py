@@ -12,7 +12,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libvqhmm.so")
 NPARAMS = 18
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 _ERRORS = {-1: "invalid argument", -2: "kernel launch failed", -3: "workspace too small",
            -4: "unsupported shape"}
@@ -43,8 +43,9 @@ _SIGS = {
     "vqhmm_fwdbwd_f32": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "vqhmm_elbo_workspace_size": (ctypes.c_int, [ctypes.POINTER(Dims), c_i64, c_i64, ctypes.POINTER(c_sz)]),
     "vqhmm_elbo_fwd_f32": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(c_vp), c_vp, c_vp, ctypes.c_int,
-                                          c_vp, c_i64, c_i64, c_f32, ctypes.c_int, c_vp, c_sz, c_vp, c_vp, c_vp]),
-    "vqhmm_elbo_bwd_f32": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(c_vp), c_vp, c_i64, c_i64, c_f32,
+                                          c_vp, c_vp, c_i64, c_i64, c_f32, ctypes.c_int, c_vp, c_sz, c_vp, c_vp,
+                                          c_vp]),
+    "vqhmm_elbo_bwd_f32": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(c_vp), c_vp, c_vp, c_i64, c_i64, c_f32,
                                           c_vp, c_vp, c_sz, c_vp, c_vp]),
     "vqhmm_elbo_pieces": (ctypes.c_int, [ctypes.POINTER(Dims), c_i64, c_i64, c_vp, ctypes.POINTER(c_vp),
                                          ctypes.POINTER(c_vp)]),
@@ -55,7 +56,7 @@ _SIGS = {
                                              ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                              ctypes.POINTER(ctypes.c_int)]),
     "vqhmm_elbo_stage_f32": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(c_vp), c_vp, c_vp, ctypes.c_int,
-                                            c_vp, c_i64, c_i64, c_f32, c_vp, c_sz, c_vp, ctypes.c_int, c_vp]),
+                                            c_vp, c_vp, c_i64, c_i64, c_f32, c_vp, c_sz, c_vp, ctypes.c_int, c_vp]),
     "vqhmm_gather_chunks_f32": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "vqhmm_infer_workspace_size": (ctypes.c_int, [ctypes.POINTER(Dims), c_i64, c_i64, ctypes.POINTER(c_sz)]),
     "vqhmm_encode_f32": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(c_vp), c_vp, c_i64, c_i64, c_vp,

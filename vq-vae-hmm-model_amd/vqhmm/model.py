@@ -204,7 +204,7 @@ class _ElboLoss(torch.autograd.Function):
         need_grad = any(ctx.needs_input_grad[5:])
         ptrs = _ptr_array(params)
         _ext.check(lib.vqhmm_elbo_fwd_f32(ctypes.byref(d), ptrs, _ext.ptr(x), _ext.ptr(u), lay, _ext.ptr(lengths),
-                                          B, T, float(beta), int(need_grad), _ext.ptr(ws), nb.value,
+                                          None, B, T, float(beta), int(need_grad), _ext.ptr(ws), nb.value,
                                           _ext.ptr(loss), None, _ext.stream_ptr(x.device)), "compute_loss forward")
         ctx.state = (d, ws, nb.value, B, T, float(beta))
         ctx.save_for_backward(x, *params)
@@ -218,8 +218,8 @@ class _ElboLoss(torch.autograd.Function):
         off = param_offsets(d)
         grad = torch.empty(off[-1], device=x.device)
         gl = gloss.contiguous().float()
-        _ext.check(lib.vqhmm_elbo_bwd_f32(ctypes.byref(d), _ptr_array(params), _ext.ptr(x), B, T, beta,
-                                          _ext.ptr(gl), _ext.ptr(ws), nbytes, _ext.ptr(grad),
+        _ext.check(lib.vqhmm_elbo_bwd_f32(ctypes.byref(d), _ptr_array(params), _ext.ptr(x), None, B, T,
+                                          beta, _ext.ptr(gl), _ext.ptr(ws), nbytes, _ext.ptr(grad),
                                           _ext.stream_ptr(x.device)), "compute_loss backward")
         grads = [grad[off[i]:off[i + 1]].view_as(p) for i, p in enumerate(params)]
         return (None, None, None, None, None, *grads)

@@ -102,23 +102,28 @@ class TrainState:
         return x, u, lengths
 
     # -------------------------------------------------------------- the step
-    def forward_backward(self, x, u, lengths, beta):
-        """Loss (accumulated into epoch_acc) and flat gradient of one batch."""
+    def forward_backward(self, x, u, lengths, beta, norm=None):
+        """Loss (accumulated into epoch_acc) and flat gradient of one batch.
+
+        norm: None, or a device int64 {valid_count, batch} of the global batch this
+        batch is a shard of (vqhmm.dist.global_norm); the loss and gradient are
+        then this shard's share of the global batch's, and shares SUM to it."""
         B, _, T = x.shape
         lay = self.model.prior.u_layout(u)
         ws = self.workspace(B, T)
         st = _ext.stream_ptr(self.device)
         d = ctypes.byref(self.dims)
-        _ext.check(self.lib.vqhmm_elbo_fwd_f32(d, self.ptrs, _ext.ptr(x), _ext.ptr(u), lay, _ext.ptr(lengths), B, T,
-                                               float(beta), 1, _ext.ptr(ws), ws.numel(), _ext.ptr(self.loss),
-                                               _ext.ptr(self.epoch_acc), st), "elbo forward")
+        _ext.check(self.lib.vqhmm_elbo_fwd_f32(d, self.ptrs, _ext.ptr(x), _ext.ptr(u), lay, _ext.ptr(lengths),
+                                               _ext.ptr(norm), B, T, float(beta), 1, _ext.ptr(ws), ws.numel(),
+                                               _ext.ptr(self.loss), _ext.ptr(self.epoch_acc), st), "elbo forward")
         if self.overlap_bwd:
-            self._backward_overlapped(x, B, T, beta, ws)
+            self._backward_overlapped(x, B, T, beta, ws, norm)
         else:
-            _ext.check(self.lib.vqhmm_elbo_bwd_f32(d, self.ptrs, _ext.ptr(x), B, T, float(beta), None, _ext.ptr(ws),
-                                                   ws.numel(), _ext.ptr(self.grad), st), "elbo backward")
+            _ext.check(self.lib.vqhmm_elbo_bwd_f32(d, self.ptrs, _ext.ptr(x), _ext.ptr(norm), B, T, float(beta), None,
+                                                   _ext.ptr(ws), ws.numel(), _ext.ptr(self.grad), st),
+                       "elbo backward")
 
-    def _backward_overlapped(self, x, B, T, beta, ws):
+    def _backward_overlapped(self, x, B, T, beta, ws, norm=None):
         """vqhmm_elbo_bwd_f32's stages with the weight gradients on a side stream.
 
         A wgrad only reads its chain dY buffer and saved activations and writes its
@@ -132,10 +137,10 @@ class TrainState:
             self._bwd_events = [torch.cuda.Event() for _ in range(len(BWD_CHAIN) + 1)]
         side, ev = self._side, self._bwd_events
         d = ctypes.byref(self.dims)
-        xp, wsp, gp = _ext.ptr(x), _ext.ptr(ws), _ext.ptr(self.grad)
+        xp, wsp, gp, np_ = _ext.ptr(x), _ext.ptr(ws), _ext.ptr(self.grad), _ext.ptr(norm)
 
         def run(stage, stream):
-            _ext.check(self.lib.vqhmm_elbo_stage_f32(d, self.ptrs, xp, None, 0, None, B, T, float(beta), wsp,
+            _ext.check(self.lib.vqhmm_elbo_stage_f32(d, self.ptrs, xp, None, 0, None, np_, B, T, float(beta), wsp,
                                                      ws.numel(), gp, stage, ctypes.c_void_p(stream.cuda_stream)),
                        "elbo backward")
 
@@ -159,19 +164,26 @@ class TrainState:
         if self.distributed and self.world > 1:
             torch.distributed.all_reduce(self.grad, op=torch.distributed.ReduceOp.SUM, group=self.pg)
 
-    def apply_adam(self):
+    def apply_adam(self, global_norm=False):
+        """Adam on the (all-reduced) gradient.  Shards normalised by their own batch
+        average over ranks (1/world); shards normalised by the global batch
+        (global_norm) already sum to the global gradient (scale 1)."""
         b1, b2 = self.betas
+        scale = 1.0 if global_norm else 1.0 / self.world
         _ext.check(self.lib.vqhmm_adam_f32(_ext.ptr(self.flat), _ext.ptr(self.grad), _ext.ptr(self.exp_avg),
                                            _ext.ptr(self.exp_avg_sq), self.flat.numel(), self.lr, b1, b2, self.eps,
-                                           _ext.ptr(self.step_dev), 1.0 / self.world, _ext.stream_ptr(self.device)),
+                                           _ext.ptr(self.step_dev), scale, _ext.stream_ptr(self.device)),
                    "adam")
 
-    def step(self, x, u, lengths, beta):
-        """zero_grad + compute_loss + backward + (all-reduce) + Adam.step (:154-157)."""
+    def step(self, x, u, lengths, beta, norm=None):
+        """zero_grad + compute_loss + backward + (all-reduce) + Adam.step (:154-157).
+
+        norm (device int64 {valid_count, batch} of the global batch, or None): see
+        forward_backward.  With it, the ranks' summed gradient IS the global batch's."""
         x, u, lengths = self.prepare(x, u, lengths)
-        self.forward_backward(x, u, lengths, beta)
+        self.forward_backward(x, u, lengths, beta, norm)
         self.reduce_gradients()
-        self.apply_adam()
+        self.apply_adam(global_norm=norm is not None)
         return self.loss
 
     def publish_grads(self):
@@ -179,7 +191,7 @@ class TrainState:
         for i, p in enumerate(self.model.ordered_parameters()):
             p.grad = self.grad[self.off[i]:self.off[i + 1]].view_as(p).clone()
 
-    def capture(self, x, u, lengths, beta, warmup=2):
+    def capture(self, x, u, lengths, beta, warmup=2, norm=None):
         """Capture one fixed-shape step into HIP graphs; returns a replay callable.
 
         Single process: the whole step is one graph.  Multi-rank: forward+backward
@@ -192,21 +204,21 @@ class TrainState:
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
             for _ in range(warmup):  # warm-up steps are real steps (identical to eager ones)
-                self.forward_backward(x, u, lengths, beta)
+                self.forward_backward(x, u, lengths, beta, norm)
                 self.reduce_gradients()
-                self.apply_adam()
+                self.apply_adam(norm is not None)
         torch.cuda.current_stream(self.device).wait_stream(s)
         if not split:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                self.forward_backward(x, u, lengths, beta)
-                self.apply_adam()
+                self.forward_backward(x, u, lengths, beta, norm)
+                self.apply_adam(norm is not None)
             return g.replay
         g_fb, g_adam = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         with torch.cuda.graph(g_fb):
-            self.forward_backward(x, u, lengths, beta)
+            self.forward_backward(x, u, lengths, beta, norm)
         with torch.cuda.graph(g_adam):
-            self.apply_adam()
+            self.apply_adam(norm is not None)
 
         def replay():
             g_fb.replay()
