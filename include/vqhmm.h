@@ -148,7 +148,9 @@ int vqhmm_elbo_stage_f32(const vqhmm_dims_t* dims, const float* const* params, c
 /* torch.optim.Adam step (no weight decay / amsgrad; train_model uses the
  * defaults, :146) over n contiguous fp32 elements.  `step` is a DEVICE int64
  * step counter that this call increments before the update (so a captured
- * graph replays correct bias corrections); the gradient is multiplied by
+ * graph replays correct bias corrections).  The update and the increment are
+ * one launch: during it the upper 32 bits hold a completion ticket, so between
+ * calls *step is the plain step count and must stay below 2^32.  The gradient is multiplied by
  * grad_scale first (1/world_size after a SUM all-reduce, else 1). */
 int vqhmm_adam_f32(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
                    double lr, double beta1, double beta2, double eps, int64_t* step, float grad_scale,

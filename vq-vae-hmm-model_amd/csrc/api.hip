@@ -222,10 +222,12 @@ enum Stage {
 };
 const int FWD_FIRST = S_TOPCL, FWD_LAST = S_FINAL, BWD_FIRST = S_PAR_DG, BWD_LAST = S_LOGPRIOR;
 const char* kStageNames[S_COUNT] = {
-    "inputs_to_pcl", "compose_fwd", "enc_conv1", "enc_conv2+to_logits", "dec_conv1(composed)", "dec_conv2+to_params",
-    "elbo_head", "finalize_loss", "to_params_dgrad", "dec_conv2_dgrad", "dec_conv1_dgrad", "logits_bwd",
+    "inputs_to_pcl+compose_fwd", "(compose_fwd: in prologue)", "enc_conv1", "enc_conv2+to_logits",
+    "dec_conv1(composed)", "dec_conv2+to_params",
+    "elbo_head", "finalize_loss", "to_params_dgrad", "dec_conv2_dgrad", "dec_conv1_dgrad+logits_bwd", "(logits_bwd: in dec_conv1_dgrad)",
     "to_logits_dgrad", "enc_conv2_dgrad", "to_params_wgrad", "dec_conv2_wgrad", "dec_conv1_wgrad",
-    "to_logits_wgrad", "enc_conv2_wgrad", "enc_conv1_wgrad", "reduce_slabs", "compose_bwd", "log_prior_grad"};
+    "to_logits_wgrad", "enc_conv2_wgrad", "enc_conv1_wgrad", "reduce_slabs", "compose_bwd+log_prior_grad",
+    "(log_prior_grad: in compose_bwd)"};
 
 struct StepCtx {
   const float* const* w;
@@ -319,18 +321,33 @@ int run_staged_head(const ElboPlan& p, const StepCtx& c, const float* const* w, 
   return VQHMM_OK;
 }
 
+// The softmax backward (logits_bwd) rides in the dec_conv1 dgrad epilogue when that
+// conv runs on conv2 and a row's K <= 4 channels sit in one lane.
+bool logits_bwd_fused(const ElboPlan& p) { return p.K <= 4 && conv2_supported(conv_of(p, nullptr, S_DEC1_DG)); }
+
 int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
   const float* const* w = c.w;
   switch (st) {
-    case S_TOPCL: {
-      if (int rc = launch_to_pcl(c.x, p.D, p.B, p.T, p.T, 1, p.xp, s)) return rc;
-      const int64_t sc = c.u_layout == 0 ? p.T : 1, stt = c.u_layout == 0 ? 1 : p.U;
-      return launch_to_pcl(c.u, p.U, p.B, p.T, sc, stt, p.up, s);
+    case S_TOPCL: {  // x, u -> PCL and the composed decoder conv1 weight, one launch
+      PrologueArgs a{};
+      a.x = c.x; a.D = p.D; a.xsc = p.T; a.xst = 1; a.xp = p.xp;
+      a.u = c.u; a.U = p.U; a.usc = c.u_layout == 0 ? p.T : 1; a.ust = c.u_layout == 0 ? 1 : p.U; a.up = p.up;
+      a.B = p.B; a.T = p.T;
+      a.W = w[DEC1_W]; a.E = w[EMB]; a.H = p.H; a.K = p.K; a.Wc = p.Wc;
+      return launch_prologue(a, s);
     }
-    case S_COMPOSE:
-      return launch_compose_fwd(w[DEC1_W], w[EMB], p.H, p.K, p.Wc, s);
-    case S_ENC1: case S_ENC2: case S_DEC1: case S_DEC2: case S_DEC2_DG: case S_DEC1_DG: case S_LOGIT_DG: case S_ENC2_DG:
+    case S_COMPOSE:  // runs inside S_TOPCL's launch
+      return VQHMM_OK;
+    case S_ENC1: case S_ENC2: case S_DEC1: case S_DEC2: case S_DEC2_DG: case S_LOGIT_DG: case S_ENC2_DG:
       return launch_conv(conv_of(p, w, st), s);
+    case S_DEC1_DG: {
+      ConvArgs a = conv_of(p, w, st);
+      if (logits_bwd_fused(p)) {  // + logits_bwd in the epilogue
+        a.act = 3;
+        a.lb_q = p.q; a.lb_dqx = p.dqx; a.lb_dlx = p.dlx; a.lb_scale = c.gscale; a.lb_dlog = p.dlog;
+      }
+      return launch_conv(a, s);
+    }
     case S_PAR_DG: {
       ConvArgs a = conv_of(p, w, st);
       a.scale = c.gscale;  // dpar is the head's gradient for dloss = 1
@@ -352,6 +369,7 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       return launch_finalize_loss(p.part, p.hgrid, c.lengths, c.norm, p.B, p.T, p.D, c.beta, c.loss, c.loss_accum,
                                   p.pieces, s);
     case S_LOGIT_BWD:
+      if (logits_bwd_fused(p)) return VQHMM_OK;  // ran in S_DEC1_DG's epilogue
       return launch_logits_bwd(p.q, p.dqd, p.dqx, p.dlx, c.gscale, p.R, p.K, p.dlog, s);
     case S_W_PAR: case S_W_DEC2: case S_W_DEC1: case S_W_LOGIT: case S_W_ENC2: case S_W_ENC1: {
       const int i = st - S_W_PAR;
@@ -406,15 +424,11 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       int64_t off[VQHMM_NPARAMS + 1];
       vqhmm_dims_t d{p.D, p.H, p.K, p.H2, p.U, p.TH};
       vqhmm_param_layout(&d, off);
-      return launch_compose_bwd(p.dWc, w[DEC1_W], w[EMB], p.H, p.K, c.g + off[DEC1_W], c.g + off[EMB], s);
+      const LogPriorGradArgs lp{p.q0sum, w[LOG_PRIOR], p.K, c.beta, c.norm, p.B, c.gscale, c.g + off[LOG_PRIOR]};
+      return launch_compose_bwd(p.dWc, w[DEC1_W], w[EMB], p.H, p.K, c.g + off[DEC1_W], c.g + off[EMB], lp, s);
     }
-    case S_LOGPRIOR: {
-      int64_t off[VQHMM_NPARAMS + 1];
-      vqhmm_dims_t d{p.D, p.H, p.K, p.H2, p.U, p.TH};
-      vqhmm_param_layout(&d, off);
-      return launch_log_prior_grad(p.q0sum, w[LOG_PRIOR], p.K, c.beta, c.norm, p.B, c.gscale, c.g + off[LOG_PRIOR],
-                                   s);
-    }
+    case S_LOGPRIOR:  // runs inside S_COMPOSE_BWD's launch
+      return VQHMM_OK;
   }
   return VQHMM_EINVAL;
 }

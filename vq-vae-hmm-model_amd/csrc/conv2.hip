@@ -56,7 +56,8 @@ __device__ __forceinline__ float4 x_mask(const ConvArgs& a, int64_t m0, int s, i
 
 }  // namespace
 
-// Epilogue of one tile (ACT: 0 none, 1 ReLU, 2 ReLU-backward mask by aux).
+// Epilogue of one tile (ACT: 0 none, 1 ReLU, 2 ReLU-backward mask by aux, 3 none + the softmax
+// backward of the row, see ConvArgs::lb_*).
 template <int NB, int PB, int ACT>
 __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a, int64_t m0, int wave, int lg4, int l16,
                                                f32x4 (&acc)[NB][PB], const float4 (&auxv)[NB][PB],
@@ -84,6 +85,26 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a, int64_t m0, in
         }
         acc[nb][pb] = y;
         const int n0 = nb * 16 + 4 * lg4;
+        if constexpr (ACT == 3) {  // softmax backward of the row (lanes lg4 = 0 hold channels 0..3)
+          if (nb == 0 && lg4 == 0 && r < a.R) {
+            const float lsc = a.lb_scale ? *a.lb_scale : 1.f;
+            const float4 q4 = *reinterpret_cast<const float4*>(a.lb_q + r * 4);
+            const float4 x4 = *reinterpret_cast<const float4*>(a.lb_dqx + r * 4);
+            const float4 l4 = *reinterpret_cast<const float4*>(a.lb_dlx + r * 4);
+            const float qk[4] = {q4.x, q4.y, q4.z, q4.w}, xk[4] = {x4.x, x4.y, x4.z, x4.w};
+            const float lk[4] = {l4.x, l4.y, l4.z, l4.w};
+            float dq[4], sdot = 0.f;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              dq[k] = y[k] + lsc * xk[k];
+              sdot = fmaf(qk[k], dq[k], sdot);
+            }
+            f32x4 dl;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) dl[k] = qk[k] * (dq[k] - sdot) + lsc * lk[k];
+            *reinterpret_cast<f32x4*>(a.lb_dlog + r * 4) = dl;
+          }
+        }
         if (a.out && r < a.R && n0 < ld4(a.N)) *reinterpret_cast<f32x4*>(a.out + r * ld4(a.N) + n0) = y;
         if (a.out_cf && valid) {
 #pragma unroll
@@ -292,6 +313,10 @@ static int launch_c2p(const ConvArgs& a, hipStream_t s) {
     if constexpr (KS == 3) {
       if (a.act == 1) return launch_c2v<NB, KCP, KS, PB, 1, true>(a, s);
     }
+    return VQHMM_EUNSUPPORTED;
+  }
+  if (a.act == 3) {
+    if constexpr (NB == 1 && KS == 3) return launch_c2v<NB, KCP, KS, PB, 3, false>(a, s);
     return VQHMM_EUNSUPPORTED;
   }
   if (a.act == 2) return launch_c2v<NB, KCP, KS, PB, 2, false>(a, s);

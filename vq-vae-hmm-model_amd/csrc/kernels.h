@@ -32,6 +32,14 @@ struct ConvArgs {
   int t_split;
   float* q_out;      // PCL softmax of the tail
   float* q_cf;       // CF softmax of the tail
+  // act == 3 (conv2 only, N <= 4): the output y = dL/dq of the decoder path is also
+  // pushed through the softmax backward (logits_bwd_kernel's formula):
+  // lb_dlog = q * (dq - <q, dq>) + scale * lb_dlx,  dq = y + scale * lb_dqx
+  const float* lb_q;
+  const float* lb_dqx;
+  const float* lb_dlx;
+  const float* lb_scale;
+  float* lb_dlog;
 };
 
 // Loss normalisers of compute_loss (VQ_VAE_HMM_fixed.py:120 mask.sum()*C, :131/:135 B).
@@ -40,6 +48,41 @@ struct ConvArgs {
 // gradients SUM (all-reduce) to exactly the global batch's (data parallel over ragged batches).
 __device__ __forceinline__ float loss_norm_batch(const int64_t* norm, int64_t B) {
   return norm ? (float)norm[1] : (float)B;
+}
+
+// finalize_loss: loss = recon + beta*(prior - entropy) (VQ_VAE_HMM_fixed.py:137) from the head's
+// per-workgroup partials part[nblk][4] = recon_sum, init_sum, trans_sum, ent_sum; run by the 256
+// threads of ONE workgroup; red = 5*256 doubles of LDS.
+__device__ inline void finalize_loss_block(const double* part, int nblk, const int64_t* lengths, const int64_t* norm,
+                                           int64_t B, int T, int D, float beta, float* loss, double* accum,
+                                           float* pieces, double* red) {
+  const int tid = threadIdx.x;
+  double v[5] = {0, 0, 0, 0, 0};
+  for (int i = tid; i < nblk; i += 256)
+    for (int k = 0; k < 4; ++k) v[k] += part[i * 4 + k];
+  for (int64_t b = tid; !norm && b < B; b += 256) {
+    const int64_t L = lengths[b];
+    v[4] += (double)(L <= 0 ? 0 : (L < T ? L : T));
+  }
+  for (int k = 0; k < 5; ++k) red[k * 256 + tid] = v[k];
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if (tid < st)
+      for (int k = 0; k < 5; ++k) red[k * 256 + tid] += red[k * 256 + tid + st];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const double cnt = norm ? (double)norm[0] : red[4 * 256];
+    const double Bn = norm ? (double)norm[1] : (double)B;
+    const float ncount = fmaxf((float)(cnt * D), 1.0f);
+    const float recon = (float)red[0] / ncount;
+    const float prior = -(float)((red[1 * 256] + red[2 * 256]) / Bn);
+    const float ent = (float)(red[3 * 256] / Bn);
+    const float l = recon + beta * (prior - ent);
+    *loss = l;
+    if (accum) *accum += (double)l;
+    if (pieces) { pieces[0] = recon; pieces[1] = prior; pieces[2] = ent; }
+  }
 }
 
 struct WgradArgs {
@@ -143,8 +186,18 @@ int launch_reduce_slabs(const SlabSeg* segs, int n, hipStream_t s);
 int launch_finalize_loss(const double* part, int nblk, const int64_t* lengths, const int64_t* norm, int64_t B, int T,
                          int D, float beta, float* loss, double* accum, float* pieces, hipStream_t s);
 int launch_compose_fwd(const float* W, const float* E, int H, int K, float* Wc, hipStream_t s);
+struct LogPriorGradArgs {  // log_prior gradient (misc.hip log_prior_grad_body); out == null: skipped
+  const float* q0sum;
+  const float* log_prior;
+  int K;
+  float beta;
+  const int64_t* norm;
+  int64_t B;
+  const float* scale;
+  float* out;
+};
 int launch_compose_bwd(const float* dWc, const float* W, const float* E, int H, int K, float* dW, float* dE,
-                       hipStream_t s);
+                       const LogPriorGradArgs& lp, hipStream_t s);
 int launch_logits_bwd(const float* q, const float* dq_dec, const float* dqx, const float* dlx, const float* scale,
                       int64_t R, int K, float* dlog, hipStream_t s);
 int launch_log_prior_grad(const float* q0sum, const float* log_prior, int K, float beta, const int64_t* norm,
@@ -152,6 +205,14 @@ int launch_log_prior_grad(const float* q0sum, const float* log_prior, int K, flo
 // CF / (B,T,C) tensor -> PCL (R, ld4(C)) with zero pad rows / channels:
 // dst[b*(T+2)+1+t][c] = src[b*C*T + c*sc + t*st]
 int launch_to_pcl(const float* src, int C, int64_t B, int T, int64_t sc, int64_t st, float* dst, hipStream_t s);
+struct PrologueArgs {  // step prologue: x, u -> PCL and the composed decoder conv1 weight (misc.hip)
+  const float* x; int D; int64_t xsc, xst; float* xp;
+  const float* u; int U; int64_t usc, ust; float* up;
+  int64_t B; int T;
+  const float* W; const float* E; int H, K; float* Wc;
+  unsigned nbx, nbu;  // set by launch_prologue
+};
+int launch_prologue(PrologueArgs a, hipStream_t s);
 int launch_gather_chunks(const float* src, const int64_t* meta, int64_t B, int64_t C, int64_t Tm, float* out,
                          hipStream_t s);
 int launch_log_softmax_vec(const float* x, int K, float* out, hipStream_t s);

@@ -64,33 +64,8 @@ int launch_reduce_slabs(const SlabSeg* segs, int n, hipStream_t s) {
 // part[nblk][4] = recon_sum, init_sum, trans_sum, ent_sum (ent_sum = sum of -sum_k q log q).
 __global__ void finalize_loss_kernel(const double* part, int nblk, const int64_t* lengths, const int64_t* norm,
                                      int64_t B, int T, int D, float beta, float* loss, double* accum, float* pieces) {
-  __shared__ double red[5][256];
-  double v[5] = {0, 0, 0, 0, 0};
-  for (int i = threadIdx.x; i < nblk; i += 256)
-    for (int k = 0; k < 4; ++k) v[k] += part[i * 4 + k];
-  for (int64_t b = threadIdx.x; !norm && b < B; b += 256) {
-    const int64_t L = lengths[b];
-    v[4] += (double)(L <= 0 ? 0 : (L < T ? L : T));
-  }
-  for (int k = 0; k < 5; ++k) red[k][threadIdx.x] = v[k];
-  __syncthreads();
-  for (int st = 128; st > 0; st >>= 1) {
-    if (threadIdx.x < st)
-      for (int k = 0; k < 5; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + st];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    const double cnt = norm ? (double)norm[0] : red[4][0];
-    const double Bn = norm ? (double)norm[1] : (double)B;
-    const float ncount = fmaxf((float)(cnt * D), 1.0f);
-    const float recon = (float)red[0][0] / ncount;
-    const float prior = -(float)((red[1][0] + red[2][0]) / Bn);
-    const float ent = (float)(red[3][0] / Bn);
-    const float l = recon + beta * (prior - ent);
-    *loss = l;
-    if (accum) *accum += (double)l;
-    if (pieces) { pieces[0] = recon; pieces[1] = prior; pieces[2] = ent; }
-  }
+  __shared__ double red[5 * 256];
+  finalize_loss_block(part, nblk, lengths, norm, B, T, D, beta, loss, accum, pieces, red);
 }
 
 int launch_finalize_loss(const double* part, int nblk, const int64_t* lengths, const int64_t* norm, int64_t B, int T,
@@ -103,11 +78,10 @@ int launch_finalize_loss(const double* part, int nblk, const int64_t* lengths, c
 // ------------------------------------------------------------ composed decoder conv1
 // Wc[o][k][tap] = sum_h W[o][h][tap] * E[k][h];  W (H,H,3), E (K,H), Wc (H,K,3).
 // One block per output channel o; W[o] and E staged in LDS.
-__global__ __launch_bounds__(256) void compose_fwd_kernel(const float* W, const float* E, int H, int K, float* Wc) {
-  extern __shared__ float cs[];
+__device__ __forceinline__ void compose_fwd_block(const float* W, const float* E, int H, int K, float* Wc, int o,
+                                                  float* cs) {
   float* wo = cs;          // [H*3]
   float* es = cs + H * 3;  // [K*H]
-  const int o = blockIdx.x;
   for (int i = threadIdx.x; i < H * 3; i += 256) wo[i] = W[(int64_t)o * H * 3 + i];
   for (int i = threadIdx.x; i < K * H; i += 256) es[i] = E[i];
   __syncthreads();
@@ -118,12 +92,24 @@ __global__ __launch_bounds__(256) void compose_fwd_kernel(const float* W, const 
     Wc[(int64_t)o * K * 3 + i] = s;
   }
 }
+__global__ __launch_bounds__(256) void compose_fwd_kernel(const float* W, const float* E, int H, int K, float* Wc) {
+  extern __shared__ float cs[];
+  compose_fwd_block(W, E, H, K, Wc, blockIdx.x, cs);
+}
 // dW[o][h][tap] = sum_k dWc[o][k][tap] E[k][h]       (blocks 0..H-1, one per o)
 // dE[k][h] = sum_{o,tap} dWc[o][k][tap] W[o][h][tap]  (blocks H..H+K-1, one per k;
 //            4 thread groups split o, combined in fixed order)
+__device__ void log_prior_grad_body(const LogPriorGradArgs& a);
+
+// Block H + K (when lp.out is set) also runs log_prior_grad_kernel's work: both are
+// the step's last, tiny reductions, so they share one launch.
 __global__ __launch_bounds__(256) void compose_bwd_kernel(const float* dWc, const float* W, const float* E, int H,
-                                                          int K, float* dW, float* dE) {
+                                                          int K, float* dW, float* dE, LogPriorGradArgs lp) {
   extern __shared__ float cs[];
+  if ((int)blockIdx.x == H + K) {
+    if (threadIdx.x == 0) log_prior_grad_body(lp);
+    return;
+  }
   if ((int)blockIdx.x < H) {
     const int o = blockIdx.x;
     float* dwo = cs;           // [K*3]
@@ -162,10 +148,10 @@ int launch_compose_fwd(const float* W, const float* E, int H, int K, float* Wc, 
   return VQHMM_OK;
 }
 int launch_compose_bwd(const float* dWc, const float* W, const float* E, int H, int K, float* dW, float* dE,
-                       hipStream_t s) {
+                       const LogPriorGradArgs& lp, hipStream_t s) {
   size_t lds = (size_t)(K * 3 + K * H) * 4;
   if ((size_t)4 * H * 4 > lds) lds = (size_t)4 * H * 4;
-  compose_bwd_kernel<<<(unsigned)(H + K), 256, lds, s>>>(dWc, W, E, H, K, dW, dE);
+  compose_bwd_kernel<<<(unsigned)(H + K + (lp.out ? 1 : 0)), 256, lds, s>>>(dWc, W, E, H, K, dW, dE, lp);
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
 }
@@ -200,18 +186,23 @@ int launch_logits_bwd(const float* q, const float* dq_dec, const float* dqx, con
 
 // ------------------------------------------------------------ log_prior grad
 // dlog_prior = dlp - softmax(log_prior) * sum(dlp),  dlp = c * sum_b q[b,:,0],  c = -beta/B (:71,:123,:131)
+__device__ void log_prior_grad_body(const LogPriorGradArgs& a) {
+  const int K = a.K;
+  const float c = -a.beta / loss_norm_batch(a.norm, a.B);
+  const float sc = a.scale ? *a.scale : 1.f;
+  float m = -__builtin_inff();
+  for (int k = 0; k < K; ++k) m = fmaxf(m, a.log_prior[k]);
+  float se = 0.f;
+  for (int k = 0; k < K; ++k) se += __expf(a.log_prior[k] - m);
+  float tot = 0.f;
+  for (int k = 0; k < K; ++k) tot += c * a.q0sum[k];
+  for (int k = 0; k < K; ++k) a.out[k] = sc * (c * a.q0sum[k] - __expf(a.log_prior[k] - m) / se * tot);
+}
+
 __global__ void log_prior_grad_kernel(const float* q0sum, const float* log_prior, int K, float beta,
                                       const int64_t* norm, int64_t B, const float* scale, float* out) {
   if (threadIdx.x != 0) return;
-  const float c = -beta / loss_norm_batch(norm, B);
-  const float sc = scale ? *scale : 1.f;
-  float m = -__builtin_inff();
-  for (int k = 0; k < K; ++k) m = fmaxf(m, log_prior[k]);
-  float se = 0.f;
-  for (int k = 0; k < K; ++k) se += __expf(log_prior[k] - m);
-  float tot = 0.f;
-  for (int k = 0; k < K; ++k) tot += c * q0sum[k];
-  for (int k = 0; k < K; ++k) out[k] = sc * (c * q0sum[k] - __expf(log_prior[k] - m) / se * tot);
+  log_prior_grad_body(LogPriorGradArgs{q0sum, log_prior, K, beta, norm, B, scale, out});
 }
 
 int launch_log_prior_grad(const float* q0sum, const float* log_prior, int K, float beta, const int64_t* norm,
@@ -225,34 +216,44 @@ int launch_log_prior_grad(const float* q0sum, const float* log_prior, int K, flo
 // torch.optim.Adam (no weight decay, no amsgrad), as its foreach/fused CUDA path computes it:
 //   m = m + (1-b1)*(g-m);  v = b2*v + (1-b2)*g*g;
 //   denom = sqrt(v)/sqrt(1-b2^t) + eps;  p = p - (lr/(1-b1^t)) * m/denom
-// The step count t lives on the device (incremented by adam_step_kernel) so a
-// captured HIP graph replays correct bias corrections.  gmul scales the
+// The step count t lives on the device so a captured HIP graph replays correct
+// bias corrections, and the increment rides in the update's own launch: every
+// workgroup reads t = (*step & 0xffffffff) + 1, then takes a ticket in the upper
+// 32 bits; the last workgroup to do so (all reads are behind it) stores t with a
+// zero ticket.  Between launches *step is the plain step count.  gmul scales the
 // gradient first (1/world_size after a SUM all-reduce).
-__global__ void adam_step_kernel(int64_t* step) { *step += 1; }
-
-__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-                            float* __restrict__ v, int64_t n, double lr, double b1, double b2, double eps,
-                            const int64_t* __restrict__ step, float gmul) {
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                   double lr, double b1, double b2, double eps, int64_t* step,
+                                                   float gmul) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  const double t = (double)*step;
-  const float step_size = (float)(lr / (1.0 - pow(b1, t)));
-  const float bc2s = (float)sqrt(1.0 - pow(b2, t));
-  const float gi = g[i] * gmul;
-  const float mi = m[i] + (float)(1.0 - b1) * (gi - m[i]);
-  const float vi = v[i] * (float)b2 + (float)(1.0 - b2) * gi * gi;
-  m[i] = mi;
-  v[i] = vi;
-  const float denom = sqrtf(vi) / bc2s + (float)eps;
-  p[i] = p[i] + (-step_size) * (mi / denom);
+  const int64_t tn = (*step & 0xffffffffll) + 1;
+  if (i < n) {
+    const double t = (double)tn;
+    const float step_size = (float)(lr / (1.0 - pow(b1, t)));
+    const float bc2s = (float)sqrt(1.0 - pow(b2, t));
+    const float gi = g[i] * gmul;
+    const float mi = m[i] + (float)(1.0 - b1) * (gi - m[i]);
+    const float vi = v[i] * (float)b2 + (float)(1.0 - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float denom = sqrtf(vi) / bc2s + (float)eps;
+    p[i] = p[i] + (-step_size) * (mi / denom);
+  }
+  // No fence: the ticket orders only the reads of *step (all returned before the
+  // barrier), not this workgroup's parameter writes.
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    auto* st = reinterpret_cast<unsigned long long*>(step);
+    const unsigned long long old = atomicAdd(st, 1ull << 32);
+    if ((old >> 32) == gridDim.x - 1) atomicExch(st, (unsigned long long)tn);
+  }
 }
 
 int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, double lr, double beta1, double beta2,
                 double eps, int64_t* step, float gmul, hipStream_t s) {
-  adam_step_kernel<<<1, 1, 0, s>>>(step);
-  VQHMM_LAUNCH_CHECK();
-  if (n == 0) return VQHMM_OK;
-  adam_kernel<<<(unsigned)cdiv(n, 256), 256, 0, s>>>(p, g, m, v, n, lr, beta1, beta2, eps, step, gmul);
+  const int64_t nb = n > 0 ? cdiv(n, 256) : 1;  // one workgroup still advances the step when n == 0
+  adam_kernel<<<(unsigned)nb, 256, 0, s>>>(p, g, m, v, n, lr, beta1, beta2, eps, step, gmul);
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
 }
@@ -277,11 +278,10 @@ int launch_log_softmax_vec(const float* x, int K, float* out, hipStream_t s) {
 }  // namespace vqhmm
 
 namespace vqhmm {
-__global__ __launch_bounds__(256) void to_pcl_kernel(const float* __restrict__ src, int C, int64_t B, int T,
-                                                     int64_t sc, int64_t st, float* __restrict__ dst) {
+__device__ __forceinline__ void to_pcl_slot(const float* __restrict__ src, int C, int64_t B, int T, int64_t sc,
+                                            int64_t st, float* __restrict__ dst, int64_t i) {  // i: float4 slot
   const int L4 = ld4(C) / 4;
   const int64_t R = B * (int64_t)(T + 2);
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // float4 slot
   if (i >= R * L4) return;
   const int64_t r = i / L4;
   const int c0 = (int)(i - r * L4) * 4;
@@ -293,6 +293,33 @@ __global__ __launch_bounds__(256) void to_pcl_kernel(const float* __restrict__ s
   for (int k = 0; k < 4; ++k)
     e[k] = (valid && c0 + k < C) ? src[b * (int64_t)C * T + (c0 + k) * sc + (int64_t)t * st] : 0.f;
   reinterpret_cast<float4*>(dst)[i] = make_float4(e[0], e[1], e[2], e[3]);
+}
+__global__ __launch_bounds__(256) void to_pcl_kernel(const float* __restrict__ src, int C, int64_t B, int T,
+                                                     int64_t sc, int64_t st, float* __restrict__ dst) {
+  to_pcl_slot(src, C, B, T, sc, st, dst, (int64_t)blockIdx.x * 256 + threadIdx.x);
+}
+// Step prologue in ONE launch (the step's first three tiny pieces of work): blocks
+// [0, nbx) convert x and [nbx, nbx + nbu) convert u to PCL (to_pcl_kernel), the last H
+// blocks compose the decoder conv1 weight (compose_fwd_kernel).
+__global__ __launch_bounds__(256) void prologue_kernel(PrologueArgs a) {
+  extern __shared__ float cs[];
+  const unsigned bx = blockIdx.x;
+  if (bx < a.nbx) {
+    to_pcl_slot(a.x, a.D, a.B, a.T, a.xsc, a.xst, a.xp, (int64_t)bx * 256 + threadIdx.x);
+  } else if (bx < a.nbx + a.nbu) {
+    to_pcl_slot(a.u, a.U, a.B, a.T, a.usc, a.ust, a.up, (int64_t)(bx - a.nbx) * 256 + threadIdx.x);
+  } else {
+    compose_fwd_block(a.W, a.E, a.H, a.K, a.Wc, (int)(bx - a.nbx - a.nbu), cs);
+  }
+}
+int launch_prologue(PrologueArgs a, hipStream_t s) {
+  const int64_t R = a.B * (int64_t)(a.T + 2);
+  a.nbx = (unsigned)cdiv(R * (ld4(a.D) / 4), 256);
+  a.nbu = (unsigned)cdiv(R * (ld4(a.U) / 4), 256);
+  const size_t lds = (size_t)(a.H * 3 + a.K * a.H) * 4;
+  prologue_kernel<<<a.nbx + a.nbu + (unsigned)a.H, 256, lds, s>>>(a);
+  VQHMM_LAUNCH_CHECK();
+  return VQHMM_OK;
 }
 int launch_to_pcl(const float* src, int C, int64_t B, int T, int64_t sc, int64_t st, float* dst, hipStream_t s) {
   const int64_t n = B * (int64_t)(T + 2) * (ld4(C) / 4);
