@@ -224,7 +224,8 @@ const int FWD_FIRST = S_TOPCL, FWD_LAST = S_FINAL, BWD_FIRST = S_PAR_DG, BWD_LAS
 const char* kStageNames[S_COUNT] = {
     "inputs_to_pcl+compose_fwd", "(compose_fwd: in prologue)", "enc_conv1", "enc_conv2+to_logits",
     "dec_conv1(composed)", "dec_conv2+to_params",
-    "elbo_head", "finalize_loss", "to_params_dgrad", "dec_conv2_dgrad", "dec_conv1_dgrad+logits_bwd", "(logits_bwd: in dec_conv1_dgrad)",
+    "elbo_head", "finalize_loss", "to_params_dgrad", "dec_conv2_dgrad", "dec_conv1_dgrad(+logits_bwd if K<=4)",
+    "logits_bwd(K>4)",
     "to_logits_dgrad", "enc_conv2_dgrad", "to_params_wgrad", "dec_conv2_wgrad", "dec_conv1_wgrad",
     "to_logits_wgrad", "enc_conv2_wgrad", "enc_conv1_wgrad", "reduce_slabs", "compose_bwd+log_prior_grad",
     "(log_prior_grad: in compose_bwd)"};
