@@ -200,8 +200,6 @@ int launch_compose_bwd(const float* dWc, const float* W, const float* E, int H, 
                        const LogPriorGradArgs& lp, hipStream_t s);
 int launch_logits_bwd(const float* q, const float* dq_dec, const float* dqx, const float* dlx, const float* scale,
                       int64_t R, int K, float* dlog, hipStream_t s);
-int launch_log_prior_grad(const float* q0sum, const float* log_prior, int K, float beta, const int64_t* norm,
-                          int64_t B, const float* scale, float* out, hipStream_t s);
 // CF / (B,T,C) tensor -> PCL (R, ld4(C)) with zero pad rows / channels:
 // dst[b*(T+2)+1+t][c] = src[b*C*T + c*sc + t*st]
 int launch_to_pcl(const float* src, int C, int64_t B, int T, int64_t sc, int64_t st, float* dst, hipStream_t s);

@@ -3,7 +3,9 @@
 //                    into the flat gradient buffer (fixed chunk order, no atomics)
 //   finalize_loss    loss = recon + beta*(prior - entropy)  (VQ_VAE_HMM_fixed.py:137)
 //   compose_fwd/bwd  decoder embedding folded into decoder.conv1:
-//                    conv1(q^T E) == conv1'(q) with W'[o,k,tap] = sum_h W[o,h,tap] E[k,h]
+//                    conv1(q^T E) == conv1'(q) with W'[o,k,tap] = sum_h W[o,h,tap] E[k,h];
+//                    compose_bwd's extra workgroup also does the log_prior gradient
+//   prologue         x, u -> PCL + compose_fwd in one launch (the step's first stage)
 //   logits_bwd       softmax backward of q = softmax(logits) (:114) + entropy's direct term
 //   adam             torch.optim.Adam update (defaults of train_model, :146)
 #include "kernels.h"
@@ -101,8 +103,8 @@ __global__ __launch_bounds__(256) void compose_fwd_kernel(const float* W, const 
 //            4 thread groups split o, combined in fixed order)
 __device__ void log_prior_grad_body(const LogPriorGradArgs& a);
 
-// Block H + K (when lp.out is set) also runs log_prior_grad_kernel's work: both are
-// the step's last, tiny reductions, so they share one launch.
+// Block H + K (when lp.out is set) computes the log_prior gradient
+// (log_prior_grad_body): both are the step's last, tiny reductions, so they share one launch.
 __global__ __launch_bounds__(256) void compose_bwd_kernel(const float* dWc, const float* W, const float* E, int H,
                                                           int K, float* dW, float* dE, LogPriorGradArgs lp) {
   extern __shared__ float cs[];
@@ -197,19 +199,6 @@ __device__ void log_prior_grad_body(const LogPriorGradArgs& a) {
   float tot = 0.f;
   for (int k = 0; k < K; ++k) tot += c * a.q0sum[k];
   for (int k = 0; k < K; ++k) a.out[k] = sc * (c * a.q0sum[k] - __expf(a.log_prior[k] - m) / se * tot);
-}
-
-__global__ void log_prior_grad_kernel(const float* q0sum, const float* log_prior, int K, float beta,
-                                      const int64_t* norm, int64_t B, const float* scale, float* out) {
-  if (threadIdx.x != 0) return;
-  log_prior_grad_body(LogPriorGradArgs{q0sum, log_prior, K, beta, norm, B, scale, out});
-}
-
-int launch_log_prior_grad(const float* q0sum, const float* log_prior, int K, float beta, const int64_t* norm,
-                          int64_t B, const float* scale, float* out, hipStream_t s) {
-  log_prior_grad_kernel<<<1, 64, 0, s>>>(q0sum, log_prior, K, beta, norm, B, scale, out);
-  VQHMM_LAUNCH_CHECK();
-  return VQHMM_OK;
 }
 
 // ------------------------------------------------------------ Adam
