@@ -20,28 +20,76 @@ struct SlabSegs {
   int nseg;
 };
 
-// One workgroup = 64 consecutive columns x all chunks; 4 chunk phases combined in fixed order.
+// One workgroup = 64 consecutive columns x all chunks.  Where a segment's rows are
+// float4-aligned (len % 4 == 0, 16-B slab base), 16 lanes x float4 cover the 64
+// columns and 16 chunk phases keep 16 x 8 wide loads in flight per column group;
+// otherwise 64 lanes x 4 phases of scalar loads.  Phases combine in a fixed order
+// (deterministic, no atomics).
 __global__ __launch_bounds__(256) void reduce_slabs_kernel(SlabSegs segs) {
-  __shared__ float part[4][64];
+  __shared__ float part[16][64];
   int si = 0;
   while (si + 1 < segs.nseg && (int64_t)blockIdx.x >= segs.blk_start[si + 1]) ++si;
   const SlabSeg& sg = segs.s[si];
-  const int64_t col = ((int64_t)blockIdx.x - segs.blk_start[si]) * 64 + (threadIdx.x & 63);
-  const int ph = threadIdx.x >> 6;
-  float p8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (col < sg.len) {
-    int64_t c = ph;
-    for (; c + 28 < sg.nchunks; c += 32) {
+  const int64_t col0 = ((int64_t)blockIdx.x - segs.blk_start[si]) * 64;
+  const bool vec = (sg.len % 4 == 0) && ((reinterpret_cast<uintptr_t>(sg.slab) & 15) == 0);
+  int nph;
+  if (vec) {
+    nph = 16;
+    const int ph = threadIdx.x >> 4, cg = (threadIdx.x & 15) * 4;
+    const int64_t col = col0 + cg;
+    float4 p8[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) p8[k] += sg.slab[(c + 4 * k) * sg.len + col];
+    for (int k = 0; k < 8; ++k) p8[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (col < sg.len) {  // len % 4 == 0: the whole float4 is in range
+      const float4* sl = reinterpret_cast<const float4*>(sg.slab + col);
+      const int64_t ld = sg.len / 4;
+      int64_t c = ph;
+      for (; c + 112 < sg.nchunks; c += 128) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float4 v = sl[(c + 16 * k) * ld];
+          p8[k].x += v.x; p8[k].y += v.y; p8[k].z += v.z; p8[k].w += v.w;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {  // < 8 rows left per phase
+        if (c + 16 * k < sg.nchunks) {
+          const float4 v = sl[(c + 16 * k) * ld];
+          p8[k].x += v.x; p8[k].y += v.y; p8[k].z += v.z; p8[k].w += v.w;
+        }
+      }
     }
-    for (int k = 0; c < sg.nchunks; c += 4, ++k) p8[k & 7] += sg.slab[c * sg.len + col];
+    float acc[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      auto g = [&](int k) { return e == 0 ? p8[k].x : e == 1 ? p8[k].y : e == 2 ? p8[k].z : p8[k].w; };
+      acc[e] = ((g(0) + g(1)) + (g(2) + g(3))) + ((g(4) + g(5)) + (g(6) + g(7)));
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) part[ph][cg + e] = acc[e];
+  } else {
+    nph = 4;
+    const int64_t col = col0 + (threadIdx.x & 63);
+    const int ph = threadIdx.x >> 6;
+    float p8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (col < sg.len) {
+      int64_t c = ph;
+      for (; c + 28 < sg.nchunks; c += 32) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) p8[k] += sg.slab[(c + 4 * k) * sg.len + col];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k)  // < 8 rows left per phase
+        if (c + 4 * k < sg.nchunks) p8[k] += sg.slab[(c + 4 * k) * sg.len + col];
+    }
+    part[ph][threadIdx.x & 63] = ((p8[0] + p8[1]) + (p8[2] + p8[3])) + ((p8[4] + p8[5]) + (p8[6] + p8[7]));
   }
-  const float acc = ((p8[0] + p8[1]) + (p8[2] + p8[3])) + ((p8[4] + p8[5]) + (p8[6] + p8[7]));
-  part[ph][threadIdx.x & 63] = acc;
   __syncthreads();
-  if (ph == 0 && col < sg.len) {
-    float v = ((part[0][threadIdx.x] + part[1][threadIdx.x]) + part[2][threadIdx.x]) + part[3][threadIdx.x];
+  const int64_t col = col0 + threadIdx.x;
+  if (threadIdx.x < 64 && col < sg.len) {
+    float v = 0.f;
+    for (int h = 0; h < nph; h += 4)
+      v += ((part[h][threadIdx.x] + part[h + 1][threadIdx.x]) + part[h + 2][threadIdx.x]) + part[h + 3][threadIdx.x];
     if (sg.scale) v *= *sg.scale;
     sg.out[col] = v;
   }
