@@ -184,6 +184,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_mfma_kernel(HeadArgs a) {
   // operand (no transposes).
   auto phase_c = [&](auto np_tag, int blk0, int blk1) {
     constexpr int NP = decltype(np_tag)::value;
+    constexpr int SD = (KK + 3) / 4;  // 4-wide contraction steps over ij that hold nonzero dlg
     const int p0[2] = {blk0 * 16, blk1 * 16};
     float ua[NP][2], dla[NP][4], dlt[NP][4], ub[NP][4];
 #pragma unroll
@@ -219,7 +220,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_mfma_kernel(HeadArgs a) {
 #pragma unroll
       for (int i = 0; i < NP; ++i) h[i] = mfma16x16x4(ua[i][1], w1b[1], h[i]);
 #pragma unroll
-      for (int s = 1; s < 4; ++s)
+      for (int s = 1; s < SD; ++s)  // ij >= K*K are zero: the steps past them add exact zeros
 #pragma unroll
         for (int i = 0; i < NP; ++i) dh[i] = mfma16x16x4(dla[i][s], w2b[s], dh[i]);
 #pragma unroll
