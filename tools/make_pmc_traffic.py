@@ -14,9 +14,8 @@ import sys
 # (bench.py section, stage / kernel key) -> substring of the profiled kernel name
 MAP = {
     ("cfg2", "elbo_head"): "elbo_head_mfma_kernel<3, 8, 8>",
-    ("cfg2", "inputs_to_pcl"): "to_pcl_kernel",
+    ("cfg2", "inputs_to_pcl+compose_fwd"): "prologue_kernel",
     ("cfg2", "reduce_slabs"): "reduce_slabs_kernel",
-    ("cfg2", "logits_bwd"): "logits_bwd_kernel",
     ("vq_cfg3", "vq_argmin"): "vq_rows_kernel<16, 2, false",
     ("viterbi_cfg5", "viterbi_cfg5"): "viterbi_kernel<8, true>",
     ("fwdbwd_cfg4", "fwdbwd_cfg4"): "fwdbwd_kernel<8, true>",
