@@ -156,6 +156,15 @@ int vqhmm_adam_f32(float* param, const float* grad, float* exp_avg, float* exp_a
                    double lr, double beta1, double beta2, double eps, int64_t* step, float grad_scale,
                    void* stream);
 
+/* torch.nn.utils.clip_grad_norm_(parameters, max_norm) over the flat gradient
+ * (Trainer.train_epoch, src/training/trainer.py:32): grad *= pre_scale, then
+ * total = ||grad||_2 and grad *= min(max_norm / (total + 1e-6), 1), all on the
+ * device.  total_norm (nullable, device fp32) receives the norm, which is what
+ * clip_grad_norm_ returns.  pre_scale folds the 1/world of a SUM all-reduce in
+ * before the norm.  Follow with vqhmm_adam_f32(..., grad_scale = 1). */
+int vqhmm_clip_grad_norm_f32(float* grad, int64_t n, float pre_scale, float max_norm, float* total_norm,
+                             void* stream);
+
 /* ---------------------------------------------------------- data step ----
  * RandomChunkDataset.__getitem__ (:25-29) + collate_fn (:164-179) on the
  * device: out (B, C, Tmax) = zero-padded chunks, out[i,c,t] = t < L_i ?

@@ -1,0 +1,115 @@
+"""GPU parity of the clip-norm training loop (the reference's Trainer,
+src/training/trainer.py:9-47): the native clip_grad_norm_ kernel against
+torch.nn.utils.clip_grad_norm_, and vqhmm.Trainer against the CPU oracle running
+compute_loss + backward + clip_grad_norm_(1.0) + Adam on the same batches.
+
+Tolerances: clipped gradient and total norm 1e-6 relative (double-accumulated
+norm vs torch's fp32 one); trained parameters as test_gpu_model's train_model
+check (1e-4 of the tensor scale + 1e-6), epoch loss 1e-4.
+"""
+import contextlib
+import io
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_dims, load_golden
+from oracle import ref_model as RM
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("scale, pre", [(1.0, 1.0), (1e-3, 1.0), (3.0, 0.5)])
+def test_clip_grad_norm_matches_torch(scale, pre):
+    import vqhmm
+    from vqhmm import _ext
+    m = vqhmm.VAE_HMM(5, 64, 3, 32, u_dim=4, trans_hidden=128)
+    shapes = [p.shape for p in m.ordered_parameters()]
+    n = sum(int(np.prod(s)) for s in shapes)
+    gen = torch.Generator().manual_seed(7)
+    flat = torch.randn(n, generator=gen) * scale * 0.01
+    ref = [t.clone().reshape(s) for t, s in zip(torch.split(flat * pre, [int(np.prod(s)) for s in shapes]), shapes)]
+    params = [torch.nn.Parameter(torch.zeros(s)) for s in shapes]
+    for p, r in zip(params, ref):
+        p.grad = r
+    tn_ref = torch.nn.utils.clip_grad_norm_(params, 1.0)
+    ref_flat = torch.cat([p.grad.reshape(-1) for p in params])
+    g = flat.cuda()
+    tn = torch.zeros((), device="cuda")
+    lib = _ext.load()
+    _ext.check(lib.vqhmm_clip_grad_norm_f32(_ext.ptr(g), n, pre, 1.0, _ext.ptr(tn), _ext.stream_ptr()), "clip")
+    torch.cuda.synchronize()
+    assert abs(tn.item() - tn_ref.item()) <= 1e-6 * tn_ref.item()
+    err = (g.cpu() - ref_flat).abs().max().item()
+    assert err <= 1e-6 * ref_flat.abs().max().item()
+
+
+def test_trainer_matches_oracle_clip_loop():
+    import vqhmm
+    g = load_golden("cfg1_seeded")
+    d = golden_dims(g)
+    w0 = {k[2:]: torch.tensor(v) for k, v in g.items() if k.startswith("w/")}
+    x, u, L = torch.tensor(g["x"]), torch.tensor(g["u"]), torch.tensor(g["lengths"])
+    h = x.shape[0] // 2
+    loader = [(x[:h], u[:h], L[:h]), (x[h:], u[h:], L[h:])]
+    epochs = 3
+
+    # oracle: Trainer.train with compute_loss -> backward -> clip_grad_norm_(1.0) -> Adam.step
+    p = {k: w0[k].clone().requires_grad_(True) for k in RM.PARAM_ORDER}
+    plist = [p[k] for k in RM.PARAM_ORDER]
+    opt = torch.optim.Adam(plist, lr=1e-3)
+    ref_lines = []
+    for ep in range(epochs):
+        beta = min(1.0, 2.0 * (ep + 1) / epochs)
+        tot = 0.0
+        for xb, ub, Lb in loader:
+            opt.zero_grad()
+            loss = RM.elbo(p, xb, ub, Lb, beta, d["K"], d["u_dim"])
+            loss.backward()
+            torch.nn.utils.clip_grad_norm_(plist, 1.0)
+            opt.step()
+            tot += loss.item()
+        ref_lines.append((ep, tot / len(loader), beta))
+
+    m = vqhmm.VAE_HMM(d["input_dim"], d["hidden_dim"], d["K"], d["hidden_dim2"], u_dim=d["u_dim"],
+                      trans_hidden=d["trans_hidden"])
+    m.load_state_dict(w0)
+    tr = vqhmm.Trainer(m, lr=1e-3, device="cuda")
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf), contextlib.redirect_stderr(io.StringIO()):
+        tr.train(loader, num_epochs=epochs)
+    lines = [ln for ln in buf.getvalue().strip().splitlines() if ln.startswith("Epoch")]
+    assert len(lines) == epochs
+    for ln, (ep, ref_loss, beta) in zip(lines, ref_lines):
+        assert ln.startswith(f"Epoch {ep+1}/{epochs}, Loss: ") and ln.endswith(f", Beta: {beta:.2f}"), ln
+        got = float(ln.split("Loss:")[1].split(",")[0])
+        assert abs(got - ref_loss) <= 1e-4 * max(1.0, abs(ref_loss)) + 1e-4, (ln, ref_loss)
+    sd = m.state_dict()
+    for k in RM.PARAM_ORDER:
+        ref = p[k].detach().numpy().astype(np.float64)
+        got = sd[k].cpu().numpy().astype(np.float64)
+        assert np.abs(got - ref).max() <= 1e-4 * max(np.abs(ref).max(), 1e-30) + 1e-6, k
+
+
+def test_trainer_custom_loss_fn_matches_default():
+    """Trainer.train_epoch(loss_fn=...) (autograd path, native clip + Adam) equals the default path."""
+    import vqhmm
+    g = load_golden("cfg1_seeded")
+    d = golden_dims(g)
+    w0 = {k[2:]: torch.tensor(v) for k, v in g.items() if k.startswith("w/")}
+    x, u, L = torch.tensor(g["x"]), torch.tensor(g["u"]), torch.tensor(g["lengths"])
+    loader = [(x, u, L)] * 2
+    out = []
+    for fn in (None, lambda mod, xb, ub, Lb: mod.compute_loss(xb, ub, Lb, 0.5)):
+        m = vqhmm.VAE_HMM(d["input_dim"], d["hidden_dim"], d["K"], d["hidden_dim2"], u_dim=d["u_dim"],
+                          trans_hidden=d["trans_hidden"])
+        m.load_state_dict(w0)
+        tr = vqhmm.Trainer(m, lr=1e-3, device="cuda")
+        with contextlib.redirect_stderr(io.StringIO()):
+            loss = tr.train_epoch(loader, loss_fn=fn, beta=0.5)
+        out.append((loss, {k: v.cpu().clone() for k, v in m.state_dict().items()}))
+    assert abs(out[0][0] - out[1][0]) <= 1e-5 * abs(out[0][0])
+    for k in RM.PARAM_ORDER:
+        a, b = out[0][1][k], out[1][1][k]
+        assert (a - b).abs().max().item() <= 1e-4 * max(b.abs().max().item(), 1e-30) + 1e-6, k

@@ -547,6 +547,12 @@ int vqhmm_adam_f32(float* param, const float* grad, float* exp_avg, float* exp_a
                      (hipStream_t)stream);
 }
 
+int vqhmm_clip_grad_norm_f32(float* grad, int64_t n, float pre_scale, float max_norm, float* total_norm,
+                              void* stream) {
+  if (n < 0 || (n > 0 && !grad) || !(max_norm > 0.f)) return VQHMM_EINVAL;
+  return launch_clip_grad_norm(grad, n, pre_scale, max_norm, total_norm, (hipStream_t)stream);
+}
+
 int vqhmm_gather_chunks_f32(const float* src, const int64_t* meta, int64_t B, int64_t C, int64_t Tmax, float* out,
                             void* stream) {
   if (B < 0 || C < 0 || Tmax < 0 || C > INT32_MAX || Tmax > INT32_MAX) return VQHMM_EINVAL;

@@ -220,6 +220,7 @@ int launch_viterbi(const float* log_pi, const float* log_A, const float* em, con
                    int64_t T, int64_t K, int32_t* path, float* score, void* ws, size_t ws_bytes, hipStream_t s);
 int launch_fwdbwd(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths, int64_t B,
                   int64_t T, int64_t K, float* gamma, float* logZ, void* ws, size_t ws_bytes, hipStream_t s);
+int launch_clip_grad_norm(float* g, int64_t n, float pre_scale, float max_norm, float* total_out, hipStream_t s);
 int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, double lr, double beta1, double beta2,
                 double eps, int64_t* step, float gmul, hipStream_t s);
 

@@ -287,6 +287,44 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
   }
 }
 
+// ------------------------------------------------------------ gradient clipping
+// torch.nn.utils.clip_grad_norm_(params, max_norm) over the flat gradient (src/training/trainer.py:32):
+//   g *= pre_scale;  total = ||g||_2;  g *= min(max_norm / (total + 1e-6), 1)
+// One 1024-thread workgroup (the flat buffer is ~35k floats at cfg2): squares summed in double per
+// thread, combined in a fixed order, then the same workgroup scales g in place.  The norm stays on the
+// device (no host sync, graph-capturable).
+__global__ __launch_bounds__(1024) void clip_grad_norm_kernel(float* g, int64_t n, float pre_scale, float max_norm,
+                                                              float* total_out) {
+  __shared__ double red[1024];
+  __shared__ float coef;
+  const int tid = threadIdx.x;
+  double ss = 0.0;
+  for (int64_t i = tid; i < n; i += 1024) {
+    const float v = g[i] * pre_scale;
+    ss += (double)v * (double)v;
+  }
+  red[tid] = ss;
+  __syncthreads();
+  for (int st = 512; st > 0; st >>= 1) {
+    if (tid < st) red[tid] += red[tid + st];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const float total = (float)sqrt(red[0]);
+    if (total_out) *total_out = total;
+    coef = fminf(max_norm / (total + 1e-6f), 1.0f);
+  }
+  __syncthreads();
+  const float c = coef * pre_scale;
+  for (int64_t i = tid; i < n; i += 1024) g[i] *= c;
+}
+
+int launch_clip_grad_norm(float* g, int64_t n, float pre_scale, float max_norm, float* total_out, hipStream_t s) {
+  clip_grad_norm_kernel<<<1, 1024, 0, s>>>(g, n, pre_scale, max_norm, total_out);
+  VQHMM_LAUNCH_CHECK();
+  return VQHMM_OK;
+}
+
 int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, double lr, double beta1, double beta2,
                 double eps, int64_t* step, float gmul, hipStream_t s) {
   const int64_t nb = n > 0 ? cdiv(n, 256) : 1;  // one workgroup still advances the step when n == 0

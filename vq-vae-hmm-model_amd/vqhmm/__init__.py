@@ -12,8 +12,8 @@ from .data import DeviceChunkLoader, RandomChunkDataset, collate_fn  # noqa: F40
 from .hmm import forward_backward, quantize, viterbi, vq_argmin  # noqa: F401
 from .infer import hard_regimes, infer, viterbi_regimes  # noqa: F401
 from .model import PARAM_ORDER, VAE_HMM, Decoder, Encoder, Prior  # noqa: F401
-from .train import TrainState, train_model  # noqa: F401
+from .train import Trainer, TrainState, train_model  # noqa: F401
 
-__all__ = ["VAE_HMM", "Encoder", "Prior", "Decoder", "train_model", "TrainState", "RandomChunkDataset",
+__all__ = ["VAE_HMM", "Encoder", "Prior", "Decoder", "train_model", "Trainer", "TrainState", "RandomChunkDataset",
            "collate_fn", "DeviceChunkLoader", "vq_argmin", "quantize", "viterbi", "forward_backward", "PARAM_ORDER",
            "save_checkpoint", "load_checkpoint", "infer", "hard_regimes", "viterbi_regimes"]

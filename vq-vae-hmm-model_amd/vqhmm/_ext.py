@@ -57,6 +57,7 @@ _SIGS = {
                                              ctypes.POINTER(ctypes.c_int)]),
     "vqhmm_elbo_stage_f32": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(c_vp), c_vp, c_vp, ctypes.c_int,
                                             c_vp, c_vp, c_i64, c_i64, c_f32, c_vp, c_sz, c_vp, ctypes.c_int, c_vp]),
+    "vqhmm_clip_grad_norm_f32": (ctypes.c_int, [c_vp, c_i64, c_f32, c_f32, c_vp, c_vp]),
     "vqhmm_gather_chunks_f32": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "vqhmm_infer_workspace_size": (ctypes.c_int, [ctypes.POINTER(Dims), c_i64, c_i64, ctypes.POINTER(c_sz)]),
     "vqhmm_encode_f32": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(c_vp), c_vp, c_i64, c_i64, c_vp,

@@ -164,26 +164,47 @@ class TrainState:
         if self.distributed and self.world > 1:
             torch.distributed.all_reduce(self.grad, op=torch.distributed.ReduceOp.SUM, group=self.pg)
 
-    def apply_adam(self, global_norm=False):
-        """Adam on the (all-reduced) gradient.  Shards normalised by their own batch
-        average over ranks (1/world); shards normalised by the global batch
-        (global_norm) already sum to the global gradient (scale 1)."""
+    def grad_scale(self, global_norm=False):
+        """Factor turning the (all-reduced) gradient buffer into the batch gradient: shards
+        normalised by their own batch average over ranks (1/world); shards normalised by the
+        global batch (global_norm) already sum to the global gradient (1)."""
+        return 1.0 if global_norm else 1.0 / self.world
+
+    def clip_grad_norm(self, max_norm, global_norm=False):
+        """nn.utils.clip_grad_norm_(params, max_norm) on the flat gradient, on the device
+        (src/training/trainer.py:32); leaves the gradient fully scaled (Adam then uses 1).
+        The total norm (clip_grad_norm_'s return value) stays in self.total_norm."""
+        if not hasattr(self, "total_norm"):
+            self.total_norm = torch.zeros((), device=self.device)
+        _ext.check(self.lib.vqhmm_clip_grad_norm_f32(_ext.ptr(self.grad), self.grad.numel(),
+                                                     self.grad_scale(global_norm), float(max_norm),
+                                                     _ext.ptr(self.total_norm), _ext.stream_ptr(self.device)),
+                   "clip_grad_norm")
+        return self.total_norm
+
+    def apply_adam(self, global_norm=False, scale=None):
+        """Adam on the (all-reduced) gradient, scaled by grad_scale() unless `scale` is given."""
         b1, b2 = self.betas
-        scale = 1.0 if global_norm else 1.0 / self.world
+        scale = self.grad_scale(global_norm) if scale is None else float(scale)
         _ext.check(self.lib.vqhmm_adam_f32(_ext.ptr(self.flat), _ext.ptr(self.grad), _ext.ptr(self.exp_avg),
                                            _ext.ptr(self.exp_avg_sq), self.flat.numel(), self.lr, b1, b2, self.eps,
                                            _ext.ptr(self.step_dev), scale, _ext.stream_ptr(self.device)),
                    "adam")
 
-    def step(self, x, u, lengths, beta, norm=None):
-        """zero_grad + compute_loss + backward + (all-reduce) + Adam.step (:154-157).
+    def step(self, x, u, lengths, beta, norm=None, max_norm=None):
+        """zero_grad + compute_loss + backward + (all-reduce) + [clip_grad_norm_] + Adam.step
+        (:154-157; with max_norm, Trainer.train_epoch's src/training/trainer.py:23-33).
 
         norm (device int64 {valid_count, batch} of the global batch, or None): see
         forward_backward.  With it, the ranks' summed gradient IS the global batch's."""
         x, u, lengths = self.prepare(x, u, lengths)
         self.forward_backward(x, u, lengths, beta, norm)
         self.reduce_gradients()
-        self.apply_adam(global_norm=norm is not None)
+        if max_norm is None:
+            self.apply_adam(global_norm=norm is not None)
+        else:
+            self.clip_grad_norm(max_norm, global_norm=norm is not None)
+            self.apply_adam(scale=1.0)
         return self.loss
 
     def publish_grads(self):
@@ -241,3 +262,64 @@ def train_model(model, dataloader, num_epochs=10, lr=1e-3):
         print(f"Epoch {ep+1}/{num_epochs}, Loss: {epoch_loss/len(dataloader):.4f}")
     state.publish_grads()
     return model
+
+
+class Trainer:
+    """Drop-in for the reference's Trainer (src/training/trainer.py:9-47): Adam(lr),
+    compute_loss + backward + clip_grad_norm_(1.0) + step per batch, tqdm progress,
+    `Epoch e/E, Loss: L, Beta: b` print.  Runs on TrainState (native HIP step, clip and
+    Adam on the device); the epoch loss is accumulated on the device and read once
+    per epoch (same double-precision sum of the same per-step losses as loss.item()).
+
+    loss_fn(model, x, u, lengths) -> loss: a custom objective goes through autograd
+    (vqhmm's compute_loss is differentiable); its parameter .grads are gathered into
+    the flat gradient, then clipped and applied natively."""
+
+    def __init__(self, model, lr=1e-3, device="cuda"):
+        self.model = model.to(device)
+        self.device = device
+        self.state = TrainState(self.model, lr=lr)
+        self.max_norm = 1.0
+
+    def _custom_step(self, loss_fn, x, u, lengths):
+        st = self.state
+        x, u, lengths = st.prepare(x, u, lengths)
+        params = self.model.ordered_parameters()
+        for p in params:
+            p.grad = None
+        loss = loss_fn(self.model, x, u, lengths)
+        loss.backward()
+        with torch.no_grad():
+            for i, p in enumerate(params):
+                g = st.grad[st.off[i]:st.off[i + 1]]
+                if p.grad is None:
+                    g.zero_()
+                else:
+                    g.copy_(p.grad.reshape(-1))
+            st.epoch_acc += loss.detach().double()
+        st.reduce_gradients()
+        st.clip_grad_norm(self.max_norm)
+        st.apply_adam(scale=1.0)
+
+    def train_epoch(self, dataloader, loss_fn=None, beta=1.0):
+        try:
+            from tqdm import tqdm
+            it = tqdm(dataloader, desc="Training")
+        except ImportError:  # progress bar only
+            it = dataloader
+        self.model.train()
+        st = self.state
+        st.epoch_acc.zero_()
+        for x, u, lengths in it:
+            if loss_fn is None:
+                st.step(x, u, lengths, beta, max_norm=self.max_norm)
+            else:
+                self._custom_step(loss_fn, x, u, lengths)
+        return st.epoch_acc.item() / len(dataloader)
+
+    def train(self, dataloader, num_epochs=100, use_beta_warmup=True):
+        for ep in range(num_epochs):
+            beta = min(1.0, 2.0 * (ep + 1) / num_epochs) if use_beta_warmup else 1.0
+            avg_loss = self.train_epoch(dataloader, beta=beta)
+            print(f"Epoch {ep+1}/{num_epochs}, Loss: {avg_loss:.4f}, Beta: {beta:.2f}")
+        self.state.publish_grads()
