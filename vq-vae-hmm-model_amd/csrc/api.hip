@@ -224,9 +224,9 @@ const int FWD_FIRST = S_TOPCL, FWD_LAST = S_FINAL, BWD_FIRST = S_PAR_DG, BWD_LAS
 const char* kStageNames[S_COUNT] = {
     "inputs_to_pcl+compose_fwd", "(compose_fwd: in prologue)", "enc_conv1", "enc_conv2+to_logits",
     "dec_conv1(composed)", "dec_conv2+to_params",
-    "elbo_head", "finalize_loss", "to_params_dgrad", "dec_conv2_dgrad", "dec_conv1_dgrad(+logits_bwd if K<=4)",
+    "elbo_head", "finalize_loss", "to_params_dgrad", "dec_conv2_dgrad", "dec_conv1_dgrad(+logits_bwd, to_logits_dgrad if K<=4)",
     "logits_bwd(K>4)",
-    "to_logits_dgrad", "enc_conv2_dgrad", "to_params_wgrad", "dec_conv2_wgrad", "dec_conv1_wgrad",
+    "to_logits_dgrad(K>4)", "enc_conv2_dgrad", "to_params_wgrad", "dec_conv2_wgrad", "dec_conv1_wgrad",
     "to_logits_wgrad", "enc_conv2_wgrad", "enc_conv1_wgrad", "reduce_slabs", "compose_bwd+log_prior_grad",
     "(log_prior_grad: in compose_bwd)"};
 
@@ -325,6 +325,8 @@ int run_staged_head(const ElboPlan& p, const StepCtx& c, const float* const* w, 
 // The softmax backward (logits_bwd) rides in the dec_conv1 dgrad epilogue when that
 // conv runs on conv2 and a row's K <= 4 channels sit in one lane.
 bool logits_bwd_fused(const ElboPlan& p) { return p.K <= 4 && conv2_supported(conv_of(p, nullptr, S_DEC1_DG)); }
+// ... and to_logits' dgrad too when the encoder conv2 width splits into float4s over the 4 lane groups.
+bool logits_dg_fused(const ElboPlan& p) { return logits_bwd_fused(p) && ld4(p.H2) % 16 == 0; }
 
 int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
   const float* const* w = c.w;
@@ -339,13 +341,19 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
     }
     case S_COMPOSE:  // runs inside S_TOPCL's launch
       return VQHMM_OK;
-    case S_ENC1: case S_ENC2: case S_DEC1: case S_DEC2: case S_DEC2_DG: case S_LOGIT_DG: case S_ENC2_DG:
+    case S_ENC1: case S_ENC2: case S_DEC1: case S_DEC2: case S_DEC2_DG: case S_ENC2_DG:
+      return launch_conv(conv_of(p, w, st), s);
+    case S_LOGIT_DG:
+      if (logits_dg_fused(p)) return VQHMM_OK;  // ran in S_DEC1_DG's epilogue
       return launch_conv(conv_of(p, w, st), s);
     case S_DEC1_DG: {
       ConvArgs a = conv_of(p, w, st);
       if (logits_bwd_fused(p)) {  // + logits_bwd in the epilogue
         a.act = 3;
         a.lb_q = p.q; a.lb_dqx = p.dqx; a.lb_dlx = p.dlx; a.lb_scale = c.gscale; a.lb_dlog = p.dlog;
+        if (logits_dg_fused(p)) {  // + to_logits_dgrad
+          a.lb_W = w[LOGIT_W]; a.lb_h = p.h2e; a.lb_dh = p.dh2; a.lb_C = p.H2;
+        }
       }
       return launch_conv(a, s);
     }

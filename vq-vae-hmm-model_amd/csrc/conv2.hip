@@ -85,24 +85,50 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a, int64_t m0, in
         }
         acc[nb][pb] = y;
         const int n0 = nb * 16 + 4 * lg4;
-        if constexpr (ACT == 3) {  // softmax backward of the row (lanes lg4 = 0 hold channels 0..3)
-          if (nb == 0 && lg4 == 0 && r < a.R) {
-            const float lsc = a.lb_scale ? *a.lb_scale : 1.f;
-            const float4 q4 = *reinterpret_cast<const float4*>(a.lb_q + r * 4);
-            const float4 x4 = *reinterpret_cast<const float4*>(a.lb_dqx + r * 4);
-            const float4 l4 = *reinterpret_cast<const float4*>(a.lb_dlx + r * 4);
-            const float qk[4] = {q4.x, q4.y, q4.z, q4.w}, xk[4] = {x4.x, x4.y, x4.z, x4.w};
-            const float lk[4] = {l4.x, l4.y, l4.z, l4.w};
-            float dq[4], sdot = 0.f;
+        if constexpr (ACT == 3) {  // softmax backward of the row, then (optionally) to_logits' dgrad
+          if (nb == 0) {
+            // channels 0..3 of row l16 sit in lane l16 (lg4 = 0): broadcast them to the row's 4 lanes
+            float yk[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              dq[k] = y[k] + lsc * xk[k];
-              sdot = fmaf(qk[k], dq[k], sdot);
+            for (int k = 0; k < 4; ++k) yk[k] = __shfl(y[k], l16);
+            if (r < a.R) {
+              const float lsc = a.lb_scale ? *a.lb_scale : 1.f;
+              const float4 q4 = *reinterpret_cast<const float4*>(a.lb_q + r * 4);
+              const float4 x4 = *reinterpret_cast<const float4*>(a.lb_dqx + r * 4);
+              const float4 l4 = *reinterpret_cast<const float4*>(a.lb_dlx + r * 4);
+              const float qk[4] = {q4.x, q4.y, q4.z, q4.w}, xk[4] = {x4.x, x4.y, x4.z, x4.w};
+              const float lk[4] = {l4.x, l4.y, l4.z, l4.w};
+              float dq[4], sdot = 0.f;
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                dq[k] = yk[k] + lsc * xk[k];
+                sdot = fmaf(qk[k], dq[k], sdot);
+              }
+              f32x4 dl;
+#pragma unroll
+              for (int k = 0; k < 4; ++k) dl[k] = qk[k] * (dq[k] - sdot) + lsc * lk[k];
+              if (lg4 == 0) *reinterpret_cast<f32x4*>(a.lb_dlog + r * 4) = dl;
+              if (a.lb_dh) {
+                // dh[r][c] = (h[r][c] > 0) * sum_k W[k][c] dl[k]: to_logits (1x1, K -> C) dgrad with the
+                // ReLU mask of its input h, the same k-ordered fma chain as the MFMA path; lane group
+                // lg4 takes channels [lg4 * L / 4, (lg4 + 1) * L / 4) of the ld4(C) = L row
+                const int C = a.lb_C, L = ld4(C), per = L / 4;
+                for (int c0 = lg4 * per; c0 < (lg4 + 1) * per; c0 += 4) {
+                  const float4 h4 = *reinterpret_cast<const float4*>(a.lb_h + r * L + c0);
+                  const float hv[4] = {h4.x, h4.y, h4.z, h4.w};
+                  f32x4 o;
+#pragma unroll
+                  for (int v = 0; v < 4; ++v) {
+                    const int c = c0 + v;
+                    float sacc = 0.f;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) sacc = fmaf(c < C && k < a.N ? a.lb_W[k * C + c] : 0.f, dl[k], sacc);
+                    o[v] = hv[v] > 0.f ? sacc : 0.f;
+                  }
+                  *reinterpret_cast<f32x4*>(a.lb_dh + r * L + c0) = o;
+                }
+              }
             }
-            f32x4 dl;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) dl[k] = qk[k] * (dq[k] - sdot) + lsc * lk[k];
-            *reinterpret_cast<f32x4*>(a.lb_dlog + r * 4) = dl;
           }
         }
         if (a.out && r < a.R && n0 < ld4(a.N)) *reinterpret_cast<f32x4*>(a.out + r * ld4(a.N) + n0) = y;

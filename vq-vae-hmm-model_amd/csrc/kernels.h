@@ -40,6 +40,12 @@ struct ConvArgs {
   const float* lb_dlx;
   const float* lb_scale;
   float* lb_dlog;
+  // ... and, when lb_dh is set (ld4(lb_C) % 16 == 0), to_logits' dgrad with the ReLU mask of its
+  // input: lb_dh = (lb_h > 0) * (lb_W^T @ lb_dlog), lb_W the (N, lb_C) to_logits weight
+  const float* lb_W;
+  const float* lb_h;
+  float* lb_dh;
+  int lb_C;
 };
 
 // Loss normalisers of compute_loss (VQ_VAE_HMM_fixed.py:120 mask.sum()*C, :131/:135 B).
