@@ -326,7 +326,7 @@ int run_staged_head(const ElboPlan& p, const StepCtx& c, const float* const* w, 
 // conv runs on conv2 and a row's K <= 4 channels sit in one lane.
 bool logits_bwd_fused(const ElboPlan& p) { return p.K <= 4 && conv2_supported(conv_of(p, nullptr, S_DEC1_DG)); }
 // ... and to_logits' dgrad too when the encoder conv2 width splits into float4s over the 4 lane groups.
-bool logits_dg_fused(const ElboPlan& p) { return logits_bwd_fused(p) && ld4(p.H2) % 16 == 0; }
+bool logits_dg_fused(const ElboPlan& p) { return logits_bwd_fused(p) && ld4(p.H2) % 16 == 0 && p.H2 <= 64; }
 
 int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
   const float* const* w = c.w;
