@@ -133,6 +133,13 @@ int vqhmm_elbo_bwd_f32(const vqhmm_dims_t* dims, const float* const* params, con
 int vqhmm_elbo_pieces(const vqhmm_dims_t* dims, int64_t B, int64_t T, const void* workspace,
                       const float** loss, const float** pieces);
 
+/* Device addresses (inside the workspace) of the step's PCL activation and gradient
+ * buffers, in this order: x, h1, h2, logits, q, g1, g2, par (mu|logvar), dpar, dg2, dg1,
+ * dq(decoder), dlogits, dh2, dh1, dq(prior).  Row r = b*(T+2)+1+t, stride ld4(channels).
+ * Host-only, for accuracy diagnostics (tools/grad_accuracy.py). */
+int vqhmm_elbo_debug_buffers(const vqhmm_dims_t* dims, int64_t B, int64_t T, const void* workspace,
+                             const float** buffers16);
+
 /* Stage table of the training step (forward stages then backward stages, in
  * launch order).  stage_info: name, algorithmic FLOPs and bytes of ONE launch
  * (host-only); stage_f32 re-runs one stage on a workspace holding a completed
@@ -191,6 +198,19 @@ int vqhmm_forward_f32(const vqhmm_dims_t* dims, const float* const* params, cons
                       size_t ws_bytes, void* stream);
 int vqhmm_prior_f32(const vqhmm_dims_t* dims, const float* const* params, const float* u, int u_layout,
                     int64_t B, int64_t T, float* log_pi, float* log_A, void* stream);
+
+/* ------------------------------------------------------- hard regimes ----
+ * regime_probs.argmax(dim=1) of softmax(encode(x), dim=1) — backtesting.py:154-155,
+ * src/backtesting.py:105-107, VQ_VAE+HMM.ipynb:830, visualize.ipynb:74.  One fused
+ * pass: the encoder's to_logits epilogue computes q and its first argmax.
+ * x (B,D,T) -> regimes (B,T) int32 and, if q != NULL, q (B,K,T) fp32 (the probabilities
+ * the argmax was taken over).  Argmax rule = torch.argmax: NaN is the maximum, the
+ * lowest index wins ties; so regimes == q.argmax(dim=1) bit for bit.  Workspace:
+ * vqhmm_infer_workspace_size. */
+int vqhmm_regimes_f32(const vqhmm_dims_t* dims, const float* const* params, const float* x, int64_t B, int64_t T,
+                      float* q, int32_t* regimes, void* workspace, size_t ws_bytes, void* stream);
+/* Same argmax rule over the channel axis of any CF tensor: q (B,K,T) -> idx (B,T) int32. */
+int vqhmm_argmax_f32(const float* q, int64_t B, int64_t K, int64_t T, int32_t* idx, void* stream);
 
 #ifdef __cplusplus
 }

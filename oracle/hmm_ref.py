@@ -41,6 +41,32 @@ def vq_argmin_np(z, codebook):
     return d.argmin(axis=1).astype(np.int32), d.min(axis=1)
 
 
+def quantize_f32(z, codebook, idx, beta=0.25):
+    """pseudocode.txt:11-18 in fp32 numpy on channels-first z (B, Dv, T), given the
+    argmin indices idx (B, T) (c_oracle.vq_argmin: the kernel contract):
+      z_q      = codebook[idx]                         (quantize, :11)
+      z_q_st   = z + (z_q - z)   [value of z_e + (z_q - z_e).detach(), :12]
+      commit   = beta * mean((z - z_q)^2)               (:16)
+      cb_loss  = mean((z_q - z)^2)                      (:17)
+    and the gradients autograd gives them for a loss sum(w * z_q_st) + commit + cb_loss:
+      dz        = w + beta * 2 (z - z_q) / N            (ST passes w straight through)
+      dcodebook = sum over positions n with idx = k of 2 (z_q - z)_n / N
+    with N = z.size.  Returns a dict of float32 / float64 arrays."""
+    z = np.asarray(z, np.float32)
+    c = np.asarray(codebook, np.float32)
+    idx = np.asarray(idx, np.int64)
+    zq = np.transpose(c[idx], (0, 2, 1)).astype(np.float32)      # (B, Dv, T)
+    zq_st = (z + (zq - z)).astype(np.float32)
+    d = (z.astype(np.float64) - zq.astype(np.float64))
+    n = z.size
+    commit = beta * (d ** 2).mean()
+    cb_loss = (d ** 2).mean()
+    return {"z_q": zq, "z_q_st": zq_st, "commit": commit, "codebook": cb_loss,
+            "dz_extra": beta * 2.0 * d / n,
+            "dcodebook": np.stack([(-2.0 * d / n).transpose(1, 0, 2)[:, idx == k].sum(axis=1)
+                                   for k in range(c.shape[0])])}
+
+
 # ------------------------------------------------------------------- Viterbi
 def viterbi_f32(log_pi, log_A, em, lengths):
     """fp32 max-plus Viterbi with the exact op order of the contract above.

@@ -54,10 +54,18 @@ def param_shapes(input_dim, hidden_dim, K, hidden_dim2, u_dim, trans_hidden=128)
     }
 
 
-def encoder_logits(p, x):
-    """(B,D,T) -> logits (B,K,T).  Reference: Encoder.forward :38-41."""
-    a = F.relu(F.conv1d(x, p["encoder.conv1.weight"], p["encoder.conv1.bias"], padding=1))
-    a = F.relu(F.conv1d(a, p["encoder.conv2.weight"], p["encoder.conv2.bias"], padding=1))
+def _relu(z, mask=None):
+    """F.relu, or — with `mask` — the same piecewise-linear branch fixed by a given
+    pattern (z * mask): the gradient of a forward whose ReLU decisions are `mask`."""
+    return F.relu(z) if mask is None else z * mask.to(z.dtype)
+
+
+def encoder_logits(p, x, masks=None):
+    """(B,D,T) -> logits (B,K,T).  Reference: Encoder.forward :38-41.
+    masks: None, or the ReLU patterns (h1, h2, ...) to use (see _relu)."""
+    m = masks or (None, None)
+    a = _relu(F.conv1d(x, p["encoder.conv1.weight"], p["encoder.conv1.bias"], padding=1), m[0])
+    a = _relu(F.conv1d(a, p["encoder.conv2.weight"], p["encoder.conv2.bias"], padding=1), m[1])
     return F.conv1d(a, p["encoder.to_logits.weight"], p["encoder.to_logits.bias"])
 
 
@@ -79,30 +87,37 @@ def prior_tables(p, u, K, u_dim):
     return F.log_softmax(p["prior.log_prior"], dim=-1), log_A
 
 
-def decoder_params(p, q):
-    """q (B,K,T) -> (mu, logvar) each (B,D,T).  Reference: Decoder.forward :81-90."""
+def decoder_params(p, q, masks=None):
+    """q (B,K,T) -> (mu, logvar) each (B,D,T).  Reference: Decoder.forward :81-90.
+    masks: None, or the ReLU patterns (g1, g2) to use (see _relu)."""
+    m = masks or (None, None)
     emb = torch.matmul(q.transpose(1, 2), p["decoder.embeddings.weight"]).transpose(1, 2)
-    a = F.relu(F.conv1d(emb, p["decoder.conv1.weight"], p["decoder.conv1.bias"], padding=1))
-    a = F.relu(F.conv1d(a, p["decoder.conv2.weight"], p["decoder.conv2.bias"], padding=1))
+    a = _relu(F.conv1d(emb, p["decoder.conv1.weight"], p["decoder.conv1.bias"], padding=1), m[0])
+    a = _relu(F.conv1d(a, p["decoder.conv2.weight"], p["decoder.conv2.bias"], padding=1), m[1])
     out = F.conv1d(a, p["decoder.to_params.weight"], p["decoder.to_params.bias"])
     half = out.shape[1] // 2
     return out[:, :half, :], out[:, half:, :]
 
 
-def elbo_terms(p, x, u, lengths, K, u_dim, norm=None):
+def elbo_terms(p, x, u, lengths, K, u_dim, norm=None, relu_masks=None):
     """Returns the named pieces of the mean-field ELBO (reference :106-135).
 
     norm=(valid_count, batch) replaces the batch's own normalisers mask.sum()
     (:120) and B (:131 .mean(), :135) by a global batch's (data-parallel shard
-    of it; the product's `norm` argument, include/vqhmm.h).  None = reference."""
+    of it; the product's `norm` argument, include/vqhmm.h).  None = reference.
+    relu_masks=(h1, h2, g1, g2) fixes the four conv ReLU decisions (see _relu):
+    run in fp64 with a device forward's own patterns, this is the exact gradient of
+    the branch that forward took, free of the fp32 ReLU-boundary flips that make two
+    correct fp32 computations differ by ~1e-5 (tests/test_gpu_configs.py)."""
     nb, nc, nt = x.shape
     if lengths is None:
         raise ValueError("lengths required")
     valid = torch.arange(nt, device=x.device)[None, :] < lengths[:, None].to(x.device)
     log_pi, log_A = prior_tables(p, u, K, u_dim)
-    logits = encoder_logits(p, x)
+    rm = relu_masks or (None, None, None, None)
+    logits = encoder_logits(p, x, rm[0:2])
     q = F.softmax(logits, dim=1)
-    mu, logvar = decoder_params(p, q)
+    mu, logvar = decoder_params(p, q, rm[2:4])
 
     var = logvar.exp().clamp(min=1e-8)
     nll = 0.5 * (torch.log(2 * math.pi * var) + (mu - x) ** 2 / var)
@@ -125,9 +140,9 @@ def elbo_terms(p, x, u, lengths, K, u_dim, norm=None):
                 mu=mu, logvar=logvar, log_pi=log_pi, log_A=log_A)
 
 
-def elbo(p, x, u, lengths, beta, K, u_dim, norm=None):
+def elbo(p, x, u, lengths, beta, K, u_dim, norm=None, relu_masks=None):
     """Scalar loss = recon + beta*(prior - entropy).  Reference :137."""
-    t = elbo_terms(p, x, u, lengths, K, u_dim, norm)
+    t = elbo_terms(p, x, u, lengths, K, u_dim, norm, relu_masks)
     return t["recon"] + beta * (t["prior"] - t["entropy"])
 
 

@@ -92,3 +92,45 @@ def test_train_state_resume_bit_identical(tmp_path):
     vqhmm.load_checkpoint(mr, opt, path)
     for name, p in mr.named_parameters():
         assert int(opt.state[p]["step"]) == 2, name
+
+
+def test_encoder_only_checkpoint_format(tmp_path):
+    """VQ_VAE+HMM.ipynb:774 writes {'model_state_dict': trained.encoder.state_dict(),
+    'config': {input_dim, hidden_dim, hidden_dim2, K}} and :818 / visualize.ipynb:62 rebuild
+    Encoder(input_dim, hidden_dim, hidden_dim2, K) from it."""
+    torch.manual_seed(3)
+    m = vqhmm.VAE_HMM(5, 64, 3, 32, u_dim=4, trans_hidden=128)
+    path = tmp_path / "encoder_saved.pth"
+    vqhmm.save_encoder(m, path)
+    ck = torch.load(path, map_location="cpu", weights_only=True)
+    assert set(ck) == {"model_state_dict", "config"}
+    assert ck["config"] == {"input_dim": 5, "hidden_dim": 64, "hidden_dim2": 32, "K": 3}
+    assert list(ck["model_state_dict"]) == list(m.encoder.state_dict())
+    # the notebook's own reading code, on the file we wrote
+    cfg = ck.get("config", {})
+    enc = vqhmm.Encoder(cfg.get("input_dim"), cfg.get("hidden_dim", 32), cfg.get("hidden_dim2", cfg["hidden_dim"]),
+                        cfg.get("K"))
+    enc.load_state_dict(ck["model_state_dict"])
+    enc2 = vqhmm.load_encoder(path)
+    for (k, a), (k2, b) in zip(m.encoder.state_dict().items(), enc2.state_dict().items()):
+        assert k == k2 and torch.equal(a, b)
+    # a file without hidden_dim2 falls back to hidden_dim (the notebook's .get default)
+    torch.save({"model_state_dict": vqhmm.Encoder(5, 16, 16, 4).state_dict(),
+                "config": {"input_dim": 5, "hidden_dim": 16, "K": 4}}, tmp_path / "e2.pth")
+    e3 = vqhmm.load_encoder(tmp_path / "e2.pth")
+    assert e3.conv2.weight.shape == (16, 16, 3) and e3.to_logits.weight.shape == (4, 16, 1)
+
+
+@pytest.mark.gpu
+def test_encoder_only_checkpoint_round_trip_on_device(tmp_path):
+    """A reloaded encoder gives bit-identical logits and hard regimes to the trained model's."""
+    torch.manual_seed(4)
+    m = vqhmm.VAE_HMM(5, 64, 3, 32, u_dim=4, trans_hidden=128).cuda()
+    vqhmm.save_encoder(m, tmp_path / "enc.pth")
+    enc = vqhmm.load_encoder(tmp_path / "enc.pth").cuda().eval()
+    x = torch.randn(3, 5, 100, device="cuda")
+    with torch.no_grad():
+        assert torch.equal(enc(x), m.encode(x))
+    r1, q1 = vqhmm.hard_regimes(m, x)
+    r2, q2 = vqhmm.hard_regimes(enc, x)
+    assert torch.equal(r1, r2) and torch.equal(q1, q2)

@@ -80,3 +80,44 @@ def test_device_loader_bit_identical(batch_size, drop_last):
         assert x.is_cuda and u.is_cuda and not L.is_cuda and L.dtype == torch.int64
         assert torch.equal(L, Lr)
         assert torch.equal(x.cpu(), xr) and torch.equal(u.cpu(), ur)
+
+
+def golden_collate_dataset():
+    """The sequences tests/golden/make_golden.py:make_collate_case fed the REFERENCE's
+    RandomChunkDataset (torch generator seed 99; lengths 230 / 180 / 260)."""
+    g = torch.Generator().manual_seed(99)
+    xs = [torch.randn(5, n, generator=g) for n in (230, 180, 260)]
+    us = [torch.randn(4, n, generator=g) for n in (230, 180, 260)]
+    return RandomChunkDataset(xs, us, min_len=20, max_len=200)
+
+
+def test_dataset_and_collate_match_reference_fixture():
+    """vqhmm.RandomChunkDataset items under random.seed(7) and vqhmm.collate_fn reproduce
+    the reference's (VQ_VAE_HMM_fixed.py:10-29, 164-179) captured in collate.npz bit for bit."""
+    from conftest import load_golden
+    gold = load_golden("collate")
+    ds = golden_collate_dataset()
+    assert len(ds) == int(gold["len_ds"])
+    random.seed(7)
+    items = [ds[i] for i in range(6)]
+    for i, (xi, ui, L) in enumerate(items):
+        assert L == int(gold[f"item{i}/L"])
+        assert np.array_equal(xi.numpy(), gold[f"item{i}/x"]) and np.array_equal(ui.numpy(), gold[f"item{i}/u"])
+    x, u, lengths = collate_fn(items, device="cpu")
+    assert lengths.dtype == torch.int64 and np.array_equal(lengths.numpy(), gold["lengths"])
+    assert np.array_equal(x.numpy(), gold["x"]) and np.array_equal(u.numpy(), gold["u"])
+
+
+@pytest.mark.gpu
+def test_device_loader_matches_reference_fixture():
+    """DeviceChunkLoader's first batch (batch_size 6, random.seed(7)) equals the reference's
+    collate_fn output in collate.npz bit for bit."""
+    from conftest import load_golden
+    gold = load_golden("collate")
+    ds = golden_collate_dataset()
+    ld = DeviceChunkLoader(ds, 6, device="cuda")
+    random.seed(7)
+    x, u, lengths = next(iter(ld))
+    assert x.is_cuda and u.is_cuda and not lengths.is_cuda
+    assert np.array_equal(lengths.numpy(), gold["lengths"])
+    assert np.array_equal(x.cpu().numpy(), gold["x"]) and np.array_equal(u.cpu().numpy(), gold["u"])

@@ -28,7 +28,9 @@ def gpu(*arrs):
     return [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in arrs]
 
 
-CASES = [(2, 3, 50), (3, 7, 41), (4, 5, 200), (5, 9, 64), (8, 6, 300), (8, 3, 1), (1, 4, 17), (3, 70, 33)]
+CASES = [(2, 3, 50), (3, 7, 41), (4, 5, 200), (5, 9, 64), (8, 6, 300), (8, 3, 1), (1, 4, 17), (3, 70, 33),
+         # K > 8: one sequence per wave (hmm_wide.hip), both half widths
+         (9, 5, 77), (12, 4, 130), (16, 6, 64), (17, 3, 45), (24, 5, 99), (32, 6, 200), (32, 3, 1), (32, 2, 1500)]
 
 
 @pytest.mark.parametrize("K,B,T", CASES)
@@ -98,7 +100,7 @@ def test_forward_backward_long_T_precision():
     assert np.all(np.abs(logZ.cpu().numpy() - rz) <= 1e-5 * np.abs(rz))
 
 
-@pytest.mark.parametrize("K", [3, 8])
+@pytest.mark.parametrize("K", [3, 8, 13, 32])
 def test_forward_backward_extreme_tables(K):
     """Tables that push the fast base-2 step out of range, so chunks take the exact
     max-shifted recomputation: left-to-right transitions (log 0 = -inf), emissions of
@@ -142,3 +144,27 @@ def test_gamma_sums_to_one_and_viterbi_on_model_tables():
     path, score = vqhmm.viterbi(log_pi, log_A, em)
     rp, rs = c_oracle.viterbi(log_pi.cpu().numpy(), log_A.cpu().numpy(), em.cpu().numpy(), np.full(8, 200))
     assert np.array_equal(path.cpu().numpy(), rp)
+
+
+def test_viterbi_wide_ties():
+    """K = 32 with all-equal tables: every step ties across all i; lowest index wins."""
+    import vqhmm
+    K, B, T = 32, 3, 40
+    log_pi = np.zeros(K, np.float32)
+    log_A = np.zeros((B, T, K, K), np.float32)
+    em = np.zeros((B, T, K), np.float32)
+    em[1, ::3, 20] = 1.0
+    em[2, :, 17:] = 0.5  # ties inside the upper half only
+    L = np.array([T, T, 7])
+    path, score = vqhmm.viterbi(*gpu(log_pi, log_A, em), torch.from_numpy(L))
+    rp, rs = c_oracle.viterbi(log_pi, log_A, em, L)
+    assert np.array_equal(path.cpu().numpy(), rp)
+    assert np.array_equal(score.cpu().numpy(), rs)
+
+
+def test_hmm_k_over_32_rejected():
+    import vqhmm
+    K, B, T = 33, 1, 4
+    log_pi, log_A, em = random_hmm(1, B, T, K)
+    with pytest.raises(RuntimeError, match="unsupported"):
+        vqhmm.viterbi(*gpu(log_pi, log_A, em))

@@ -162,26 +162,11 @@ def test_train_model_lines(case):
 
 
 def test_cfg2_full_size_vs_oracle():
-    """BASELINE cfg2 (B=1024, T=200, K=3, D=5, H=64): loss and all gradients vs the CPU
-    oracle on the same seeded inputs, with variable lengths."""
-    import vqhmm
-    torch.manual_seed(0)
-    m = vqhmm.VAE_HMM(5, 64, 3, 32, u_dim=4, trans_hidden=128)
-    gen = torch.Generator().manual_seed(1234)
-    B, T = 1024, 200
-    x = torch.randn(B, 5, T, generator=gen)
-    u = torch.randn(B, 4, T, generator=gen)
-    L = torch.randint(20, T + 1, (B,), generator=gen)
-    L[:512] = T
-    p = {k: v.detach().clone().requires_grad_(True) for k, v in m.state_dict().items()}
-    ref = RM.elbo(p, x, u, L, 1.0, 3, 4)
-    ref.backward()
-    mg = m.cuda()
-    loss = mg.compute_loss(x.cuda(), u.cuda(), L, 1.0)
-    loss.backward()
-    assert abs(loss.item() - ref.item()) <= LOSS_RTOL * abs(ref.item())
-    for name, prm in mg.named_parameters():
-        assert_grad_close(prm.grad.cpu().numpy(), p[name].grad.numpy(), name)
+    """BASELINE cfg2 (B=1024, T=200, K=3, D=5, H=64): loss vs the fp32 CPU oracle and all
+    gradients vs the fp64 oracle on the device forward's ReLU branch, variable lengths
+    (tests/test_gpu_configs.py:check_step_vs_oracle)."""
+    from test_gpu_configs import check_step_vs_oracle
+    check_step_vs_oracle((5, 64, 3, 32, 4, 128), 1024, 200, seed=1234)
 
 
 def test_cpu_input_rejected():

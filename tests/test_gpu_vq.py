@@ -68,3 +68,30 @@ def test_vq_cfg3_size_property():
     assert torch.equal(idx[:, ::7].long(), lab[:, ::7])
     sl = z[:64].cpu().numpy()
     assert np.array_equal(idx[:64].cpu().numpy(), c_oracle.vq_argmin(sl, cb.cpu().numpy(), want_dmin=False))
+
+
+@pytest.mark.parametrize("B,Dv,T,K,beta", [(3, 5, 200, 3, 0.25), (2, 64, 50, 32, 1.0), (4, 16, 77, 8, 0.5)])
+def test_quantize_vs_pseudocode(B, Dv, T, K, beta):
+    """vqhmm.quantize (pseudocode.txt:11-18): z_q, straight-through value, commit and
+    codebook losses, and their autograd gradients vs the fp32 numpy restatement
+    (oracle/hmm_ref.quantize_f32) on the C oracle's indices."""
+    import vqhmm
+    from oracle import hmm_ref
+    rng = np.random.default_rng(K * 31 + Dv)
+    z = rng.standard_normal((B, Dv, T)).astype(np.float32)
+    cb = rng.standard_normal((K, Dv)).astype(np.float32)
+    w = rng.standard_normal((B, Dv, T)).astype(np.float32)
+    zt = torch.from_numpy(z).cuda().requires_grad_(True)
+    ct = torch.from_numpy(cb).cuda().requires_grad_(True)
+    zq_st, idx, commit, cb_loss = vqhmm.quantize(zt, ct, beta=beta)
+    ridx = c_oracle.vq_argmin(z, cb, want_dmin=False)
+    assert np.array_equal(idx.cpu().numpy(), ridx)
+    ref = hmm_ref.quantize_f32(z, cb, ridx, beta)
+    assert np.array_equal(zq_st.detach().cpu().numpy(), ref["z_q_st"])
+    assert abs(commit.item() - ref["commit"]) <= 1e-5 * ref["commit"]
+    assert abs(cb_loss.item() - ref["codebook"]) <= 1e-5 * ref["codebook"]
+    (zq_st * torch.from_numpy(w).cuda()).sum().add(commit).add(cb_loss).backward()
+    dz = zt.grad.cpu().numpy().astype(np.float64)
+    assert np.abs(dz - (w + ref["dz_extra"])).max() <= 1e-6 * np.abs(w).max()
+    dc = ct.grad.cpu().numpy().astype(np.float64)
+    assert np.abs(dc - ref["dcodebook"]).max() <= 1e-5 * max(np.abs(ref["dcodebook"]).max(), 1e-12)

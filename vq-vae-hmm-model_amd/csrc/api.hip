@@ -145,7 +145,7 @@ ConvArgs conv_base(const ElboPlan& p) {
 
 extern "C" {
 
-int32_t vqhmm_abi_version(void) { return 2; }
+int32_t vqhmm_abi_version(void) { return 3; }
 
 int vqhmm_param_layout(const vqhmm_dims_t* d, int64_t off[VQHMM_NPARAMS + 1]) {
   if (!dims_ok(d) || !off) return VQHMM_EINVAL;
@@ -548,6 +548,15 @@ int vqhmm_elbo_pieces(const vqhmm_dims_t* d, int64_t B, int64_t T, const void* w
   return VQHMM_OK;
 }
 
+int vqhmm_elbo_debug_buffers(const vqhmm_dims_t* d, int64_t B, int64_t T, const void* ws, const float** out) {
+  if (!dims_ok(d) || !ws || !out) return VQHMM_EINVAL;
+  ElboPlan p = plan_elbo(d, B, T, const_cast<void*>(ws));
+  const float* v[16] = {p.xp, p.h1e, p.h2e, p.logits, p.q, p.g1, p.g2, p.par,
+                        p.dpar, p.dg2, p.dg1, p.dqd, p.dlog, p.dh2, p.dh1, p.dqx};
+  for (int i = 0; i < 16; ++i) out[i] = v[i];
+  return VQHMM_OK;
+}
+
 int vqhmm_adam_f32(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, double lr,
                    double beta1, double beta2, double eps, int64_t* step, float grad_scale, void* stream) {
   if (n < 0 || !step || (n > 0 && (!param || !grad || !exp_avg || !exp_avg_sq))) return VQHMM_EINVAL;
@@ -586,7 +595,7 @@ int vqhmm_infer_workspace_size(const vqhmm_dims_t* d, int64_t B, int64_t T, size
 // x is CF (B, D, T); it is first copied into the padded PCL buffer xin.
 static int encode_impl(const vqhmm_dims_t* d, const float* const* w, const float* x, int64_t B, int64_t T,
                        float* logits_cf, float* q_cf, float* q_pcl, float* xin, float* bufA, float* bufB,
-                       hipStream_t s) {
+                       hipStream_t s, int32_t* regimes = nullptr) {
   const int64_t R = B * (T + 2);
   int rc;
   if ((rc = launch_to_pcl(x, d->input_dim, B, (int)T, T, 1, xin, s))) return rc;
@@ -603,7 +612,8 @@ static int encode_impl(const vqhmm_dims_t* d, const float* const* w, const float
   if (logits_cf) { a.t_cf0 = logits_cf; a.t_split = d->K; }
   a.q_out = q_pcl;
   a.q_cf = q_cf;
-  if (logits_cf && q_cf) return VQHMM_EINVAL;
+  a.reg_out = regimes;
+  if (logits_cf && (q_cf || regimes)) return VQHMM_EINVAL;
   return launch_conv(a, s);
 }
 
@@ -678,6 +688,22 @@ int vqhmm_forward_f32(const vqhmm_dims_t* d, const float* const* w, const float*
   int rc;
   if ((rc = encode_impl(d, w, x, B, T, nullptr, q, b.q, b.in, b.A, b.B, s))) return rc;
   return decode_impl(d, w, b.q, 0, B, T, mu, logvar, b.q, b.A, b.B, b.Wc, s);
+}
+
+int vqhmm_regimes_f32(const vqhmm_dims_t* d, const float* const* w, const float* x, int64_t B, int64_t T, float* q,
+                      int32_t* regimes, void* ws, size_t ws_bytes, void* stream) {
+  if (!dims_ok(d) || !w || !x || !regimes || !ws || B < 0 || T < 0) return VQHMM_EINVAL;
+  if (B * T == 0) return VQHMM_OK;
+  size_t need;
+  vqhmm_infer_workspace_size(d, B, T, &need);
+  if (ws_bytes < need) return VQHMM_EWORKSPACE;
+  InferBufs b = carve_infer(d, B, T, ws);
+  return encode_impl(d, w, x, B, T, nullptr, q, nullptr, b.in, b.A, b.B, (hipStream_t)stream, regimes);
+}
+
+int vqhmm_argmax_f32(const float* q, int64_t B, int64_t K, int64_t T, int32_t* idx, void* stream) {
+  if (B < 0 || K < 1 || T < 0 || K > INT32_MAX || (B * T > 0 && (!q || !idx))) return VQHMM_EINVAL;
+  return launch_argmax_cf(q, B, K, T, idx, (hipStream_t)stream);
 }
 
 int vqhmm_prior_f32(const vqhmm_dims_t* d, const float* const* w, const float* u, int u_layout, int64_t B, int64_t T,

@@ -82,6 +82,15 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// torch.argmax's order on (value, index) pairs: NaN is the maximum, and among equal
+// values (or NaNs) the lowest index wins.  True when (v, i) beats (bv, bi).
+__device__ __forceinline__ bool argmax_beats(float v, int i, float bv, int bi) {
+  const bool vn = v != v, bn = bv != bv;
+  if (vn) return !bn || i < bi;
+  if (bn) return false;
+  return v > bv || (v == bv && i < bi);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);

@@ -189,14 +189,18 @@ __global__ __launch_bounds__(256) void conv_mm_kernel(ConvArgs a) {
       if (a.t_out && r < a.R) a.t_out[r * ld4(a.C2) + c2] = 0.f;
       if (a.q_out && r < a.R) a.q_out[r * ld4(a.C2) + c2] = 0.f;
     }
-    if (a.q_out || a.q_cf) {
+    if (a.q_out || a.q_cf || a.reg_out) {
       float s = 0.f;
       for (int c2 = 0; c2 < a.C2; ++c2) s += __expf(Zs[row * LDZ + c2] - mx);
+      float bq = -__builtin_inff();
+      int bi = 0x7fffffff;
       for (int c2 = 0; c2 < a.C2; ++c2) {
         const float q = valid ? __expf(Zs[row * LDZ + c2] - mx) / s : 0.f;
         if (a.q_out && r < a.R) a.q_out[r * ld4(a.C2) + c2] = q;
         if (a.q_cf) Zs[row * LDZ + c2] = q;
+        if (argmax_beats(q, c2, bq, bi)) { bq = q; bi = c2; }
       }
+      if (a.reg_out && valid) a.reg_out[b * a.T + t] = bi;  // hard regime (backtesting.py:154-155)
     }
   }
   if (a.t_cf0 || a.q_cf) {

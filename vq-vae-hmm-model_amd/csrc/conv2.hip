@@ -158,7 +158,7 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a, int64_t m0, in
             else if (c2 < a.C2) a.t_cf1[(b * (a.C2 - a.t_split) + c2 - a.t_split) * a.T + t] = z[v];
           }
         }
-        if (a.q_out || a.q_cf) {
+        if (a.q_out || a.q_cf || a.reg_out) {
           float m = -__builtin_inff();
 #pragma unroll
           for (int v = 0; v < 4; ++v)
@@ -181,6 +181,20 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a, int64_t m0, in
 #pragma unroll
             for (int v = 0; v < 4; ++v)
               if (c0 + v < a.C2) a.q_cf[(b * a.C2 + c0 + v) * a.T + t] = qv[v];
+          }
+          if (a.reg_out) {  // hard regime: first argmax of the row's q (backtesting.py:154-155)
+            float bq = -__builtin_inff();
+            int bi = 0x7fffffff;
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+              if (c0 + v < a.C2 && argmax_beats(qv[v], c0 + v, bq, bi)) { bq = qv[v]; bi = c0 + v; }
+#pragma unroll
+            for (int o = 16; o <= 32; o <<= 1) {
+              const float pq = __shfl_xor(bq, o);
+              const int pi = __shfl_xor(bi, o);
+              if (argmax_beats(pq, pi, bq, bi)) { bq = pq; bi = pi; }
+            }
+            if (valid && lg4 == 0) a.reg_out[b * a.T + t] = bi;
           }
         }
       }

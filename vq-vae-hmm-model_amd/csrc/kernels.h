@@ -32,6 +32,7 @@ struct ConvArgs {
   int t_split;
   float* q_out;      // PCL softmax of the tail
   float* q_cf;       // CF softmax of the tail
+  int32_t* reg_out;  // (B, T) first-index argmax over channels of that softmax (torch.argmax rule)
   // act == 3 (conv2 only, N <= 4): the output y = dL/dq of the decoder path is also
   // pushed through the softmax backward (logits_bwd_kernel's formula):
   // lb_dlog = q * (dq - <q, dq>) + scale * lb_dlx,  dq = y + scale * lb_dqx
@@ -220,7 +221,14 @@ int launch_prologue(PrologueArgs a, hipStream_t s);
 int launch_gather_chunks(const float* src, const int64_t* meta, int64_t B, int64_t C, int64_t Tm, float* out,
                          hipStream_t s);
 int launch_log_softmax_vec(const float* x, int K, float* out, hipStream_t s);
+int launch_argmax_cf(const float* q, int64_t B, int64_t K, int64_t T, int32_t* idx, hipStream_t s);
 size_t viterbi_ws_bytes(int64_t B, int64_t T, int64_t K);
+// K in (8, 32]: one sequence per wave (hmm_wide.hip)
+size_t viterbi_wide_ws_bytes(int64_t B, int64_t T);
+int launch_viterbi_wide(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths, int64_t B,
+                        int64_t T, int64_t K, int32_t* path, float* score, void* ws, hipStream_t s);
+int launch_fwdbwd_wide(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths, int64_t B,
+                       int64_t T, int64_t K, float* gamma, float* logZ, float* ws, hipStream_t s);
 size_t fwdbwd_ws_bytes(int64_t B, int64_t T, int64_t K);
 int launch_viterbi(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths, int64_t B,
                    int64_t T, int64_t K, int32_t* path, float* score, void* ws, size_t ws_bytes, hipStream_t s);

@@ -433,4 +433,31 @@ int launch_gather_chunks(const float* src, const int64_t* meta, int64_t B, int64
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
 }
+
+// ------------------------------------------------------------ hard regimes
+// idx[b, t] = first argmax_k q[b, k, t] of a CF (B, K, T) tensor, torch.argmax's rule
+// (NaN counts as the maximum, lowest index on ties): regime_probs.argmax(dim=1) of
+// backtesting.py:154-155 / VQ_VAE+HMM.ipynb:830.  Consecutive threads walk t (coalesced).
+__global__ __launch_bounds__(256) void argmax_cf_kernel(const float* __restrict__ q, int64_t B, int K, int64_t T,
+                                                        int32_t* __restrict__ idx) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= B * T) return;
+  const int64_t b = i / T, t = i - b * T;
+  const float* col = q + b * K * T + t;
+  float bq = col[0];
+  int bi = 0;
+  for (int k = 1; k < K; ++k) {
+    const float v = col[(int64_t)k * T];
+    if (argmax_beats(v, k, bq, bi)) { bq = v; bi = k; }
+  }
+  idx[i] = bi;
+}
+
+int launch_argmax_cf(const float* q, int64_t B, int64_t K, int64_t T, int32_t* idx, hipStream_t s) {
+  const int64_t n = B * T;
+  if (n == 0) return VQHMM_OK;
+  argmax_cf_kernel<<<(unsigned)cdiv(n, 256), 256, 0, s>>>(q, B, (int)K, T, idx);
+  VQHMM_LAUNCH_CHECK();
+  return VQHMM_OK;
+}
 }  // namespace vqhmm

@@ -206,9 +206,20 @@ static int64_t big_chunks() {
   return n;
 }
 
+// chunks for every output size (experiment override VQHMM_WGRAD_CHUNKS, read once; 0 = default)
+static int64_t all_chunks() {
+  static const int64_t n = [] {
+    const char* e = getenv("VQHMM_WGRAD_CHUNKS");
+    const long v = e ? atol(e) : 0;
+    return (int64_t)(v >= 64 && v <= 65536 ? v : 0);
+  }();
+  return n;
+}
+
 int64_t wgrad2_rows(int64_t R, int N, int C, int ks) {
   // 2 chunks per CU (measured: 63.5 vs 66.2 us on dec_conv2_wgrad at cfg2, 2 waves/SIMD)
-  const int64_t chunks = ((int64_t)N * C * ks >= 4096) ? big_chunks() : 512;
+  int64_t chunks = ((int64_t)N * C * ks >= 4096) ? big_chunks() : 512;
+  if (all_chunks()) chunks = all_chunks();
   int64_t rows = cdiv(R, chunks);
   return cdiv(rows, RT) * RT;
 }

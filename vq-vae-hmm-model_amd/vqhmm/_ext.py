@@ -12,7 +12,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libvqhmm.so")
 NPARAMS = 18
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 _ERRORS = {-1: "invalid argument", -2: "kernel launch failed", -3: "workspace too small",
            -4: "unsupported shape"}
@@ -68,6 +68,10 @@ _SIGS = {
                                          c_vp, c_vp, c_vp, c_sz, c_vp]),
     "vqhmm_prior_f32": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(c_vp), c_vp, ctypes.c_int, c_i64,
                                        c_i64, c_vp, c_vp, c_vp]),
+    "vqhmm_regimes_f32": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(c_vp), c_vp, c_i64, c_i64, c_vp,
+                                         c_vp, c_vp, c_sz, c_vp]),
+    "vqhmm_argmax_f32": (ctypes.c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp]),
+    "vqhmm_elbo_debug_buffers": (ctypes.c_int, [ctypes.POINTER(Dims), c_i64, c_i64, c_vp, ctypes.POINTER(c_vp)]),
 }
 
 

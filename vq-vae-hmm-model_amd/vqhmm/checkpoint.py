@@ -59,6 +59,38 @@ def load_adam_state_dict(state, sd):
     state.lr, state.betas, state.eps = float(g["lr"]), tuple(float(b) for b in g["betas"]), float(g["eps"])
 
 
+def encoder_config(model):
+    """The 'config' dict of the encoder-only checkpoint (VQ_VAE+HMM.ipynb:774-781)."""
+    enc = model.encoder if hasattr(model, "encoder") else model
+    H, D, _ = enc.conv1.weight.shape
+    return {"input_dim": int(D), "hidden_dim": int(H), "hidden_dim2": int(enc.conv2.weight.shape[0]),
+            "K": int(enc.to_logits.weight.shape[0])}
+
+
+def save_encoder(model, path, config=None):
+    """Encoder-only checkpoint as the notebook writes it (VQ_VAE+HMM.ipynb:774):
+    {'model_state_dict': trained.encoder.state_dict(), 'config': {input_dim, hidden_dim,
+    hidden_dim2, K}}.  `model` is a VAE_HMM or an Encoder; config defaults to its dims."""
+    enc = model.encoder if hasattr(model, "encoder") else model
+    cfg = encoder_config(enc) if config is None else dict(config)
+    torch.save({"model_state_dict": enc.state_dict(), "config": cfg}, path)
+
+
+def load_encoder(path, map_location="cpu", defaults=None):
+    """Rebuild the Encoder from an encoder-only checkpoint (VQ_VAE+HMM.ipynb:818-827,
+    visualize.ipynb:62): dims from ckpt['config'] (missing keys from `defaults`, and
+    hidden_dim2 falling back to hidden_dim as the notebook does), weights from
+    ckpt['model_state_dict'].  Read with weights_only=True."""
+    from .model import Encoder
+    ck = torch.load(path, map_location=map_location, weights_only=True)
+    cfg = dict(defaults or {})
+    cfg.update(ck.get("config", {}))
+    hidden = cfg["hidden_dim"]
+    enc = Encoder(cfg["input_dim"], hidden, cfg.get("hidden_dim2", hidden), cfg["K"])
+    enc.load_state_dict(ck["model_state_dict"])
+    return enc
+
+
 def save_checkpoint(model, optimizer, epoch, loss, path):
     """src/utils/data.py:47-53."""
     from .train import TrainState

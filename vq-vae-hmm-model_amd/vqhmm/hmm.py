@@ -32,6 +32,20 @@ def vq_argmin(z, codebook, return_dist=False):
     return (idx, dmin) if return_dist else idx
 
 
+def regime_argmax(q):
+    """q (B, K, T) -> (B, T) int64: q.argmax(dim=1) by torch.argmax's rule (first index on
+    ties, NaN is the maximum), the hard regimes of backtesting.py:154-155 on given probabilities."""
+    _ext.require_device(q)
+    if q.dim() != 3:
+        raise ValueError(f"regime_argmax: expected q (B, K, T), got {tuple(q.shape)}")
+    q = q.contiguous().float()
+    B, K, T = q.shape
+    idx = torch.empty((B, T), dtype=torch.int32, device=q.device)
+    _ext.check(_ext.load().vqhmm_argmax_f32(_ext.ptr(q), B, K, T, _ext.ptr(idx), _ext.stream_ptr(q.device)),
+               "regime_argmax")
+    return idx.long()
+
+
 def quantize(z, codebook, beta=0.25):
     """VQ-VAE quantizer of pseudocode.txt:11-18 on channels-first z (B, Dv, T).
 

@@ -4,15 +4,18 @@
                             web server: x [C][T] -> {'mu', 'logvar', 'regime_probs'}
                             lists, through the fused forward (vqhmm_forward_f32:
                             encode -> softmax -> decode, one call).
-  hard_regimes(model, x)    backtesting.py:154-155: argmax_k softmax(encode(x))_k,
-                            as the VQ argmin kernel over the one-hot codebook
-                            (argmin_k ||q - e_k||^2 = argmax_k q, first index on ties).
+  hard_regimes(model, x)    backtesting.py:154-155: softmax(encode(x)).argmax(dim=1),
+                            one fused pass (vqhmm_regimes_f32: the to_logits epilogue
+                            computes q and its first argmax, torch.argmax's rule).
   viterbi_regimes(...)      MAP state path under the Prior's tables with the encoder
                             posterior as emission (log_softmax(logits)).
 """
+import ctypes
+
 import torch
 
-from .hmm import viterbi, vq_argmin
+from . import _ext
+from .hmm import viterbi
 
 
 def _device(model):
@@ -31,12 +34,32 @@ def infer(model, x):
 def hard_regimes(model, x):
     """x (B, C, T) on the device -> (regimes (B, T) int64, q (B, K, T)).
 
-    Exact for q_max >= 1/4 (1 - 2q is then exact in fp32); below that, two
-    probabilities within one ulp of 1 - 2q can tie where torch.argmax would not."""
-    with torch.no_grad():
-        q = torch.softmax(model.encode(x), dim=1)
-        eye = torch.eye(q.shape[1], device=q.device)
-        return vq_argmin(q, eye).long(), q
+    regimes == q.argmax(dim=1) bit for bit (first index on ties, NaN counts as the
+    maximum), computed in the same epilogue that produces q."""
+    _ext.require_device(x)
+    enc = model.encoder if hasattr(model, "encoder") else model
+    if x.dim() != 3 or x.shape[1] != enc.conv1.weight.shape[1]:
+        raise RuntimeError(f"hard_regimes: expected x (B, {enc.conv1.weight.shape[1]}, T), got {tuple(x.shape)}")
+    x = x.contiguous().float()
+    B, _, T = x.shape
+    d = enc._dims()
+    q = torch.empty((B, d.K, T), device=x.device)
+    reg = torch.empty((B, T), dtype=torch.int32, device=x.device)
+    if B * T:
+        from .model import _ptr_array
+        lib = _ext.load()
+        nb = ctypes.c_size_t()
+        _ext.check(lib.vqhmm_infer_workspace_size(ctypes.byref(d), B, T, ctypes.byref(nb)), "workspace")
+        ws = torch.empty(nb.value, dtype=torch.uint8, device=x.device)
+        w = [None] * _ext.NPARAMS
+        w[0:6] = [enc.conv1.weight, enc.conv1.bias, enc.conv2.weight, enc.conv2.bias, enc.to_logits.weight,
+                  enc.to_logits.bias]
+        with torch.no_grad():
+            _ext.check(lib.vqhmm_regimes_f32(ctypes.byref(d), _ptr_array([t.detach() if t is not None else None
+                                                                           for t in w]),
+                                             _ext.ptr(x), B, T, _ext.ptr(q), _ext.ptr(reg), _ext.ptr(ws), nb.value,
+                                             _ext.stream_ptr(x.device)), "hard_regimes")
+    return reg.long(), q
 
 
 def viterbi_regimes(model, x, u, lengths=None):
