@@ -1,17 +1,25 @@
 #!/usr/bin/env python3
 """Headline benchmark: VAE_HMM train-step sequences/sec on MI355X.
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W --scaling strong|weak]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
         bench.py --gpus N --steps K --warmup W
 
 Workload (BASELINE.json configs[1], "cfg2"): VAE_HMM(K=3, input_dim=5,
-hidden_dim=64, hidden_dim2=32, u_dim=4, trans_hidden=128), batch 1024 x T=200
-per GPU, synthetic x/u ~ N(0,1) already resident in HBM, lengths = T, beta=1,
-Adam lr=1e-3.  A step = zero_grad + compute_loss + backward + [RCCL
-all-reduce of the flat gradient] + Adam, exactly the reference's train_model
-inner loop (VQ_VAE_HMM_fixed.py:154-157).  N ranks each process 1024
-sequences (weak scaling); `value` = N*1024*K / max-over-ranks wall time.
+hidden_dim=64, hidden_dim2=32, u_dim=4, trans_hidden=128), T=200, synthetic
+x/u ~ N(0,1) already resident in HBM, lengths = T, beta=1, Adam lr=1e-3.  A
+step = zero_grad + compute_loss + backward + [RCCL all-reduce of the flat
+gradient] + Adam, exactly the reference's train_model inner loop
+(VQ_VAE_HMM_fixed.py:154-157).
+
+Scaling: "strong" (default) keeps the GLOBAL batch at the
+config's 1024 sequences (cfg4: 4096) and splits it over the N ranks (128 per
+GPU at N=8); "weak" gives every rank the full batch.  `value` = sequences of
+all ranks per step * K / max-over-ranks wall time of K steps.
+
+Multi-GPU: one process per GPU over RCCL.  Under torchrun the world comes from
+its env (it must equal --gpus); a bare `python bench.py --gpus N` spawns the N
+rank processes itself (fresh interpreters; the parent never touches the GPU).
 
 Also reported (rank 0):
   roofline      dominant kernel of the step, timed live with HIP events on the
@@ -38,9 +46,9 @@ sys.path.insert(0, os.path.join(ROOT, "vq-vae-hmm-model_amd"))
 sys.path.insert(0, ROOT)
 
 CONFIGS = {
-    # name: (B per GPU, T, D, H, H2, K, U, TH)
+    # name: (global B, T, D, H, H2, K, U, TH)
     "cfg2": (1024, 200, 5, 64, 32, 3, 4, 128),
-    "cfg4": (512, 512, 16, 64, 32, 8, 4, 128),
+    "cfg4": (4096, 512, 16, 64, 32, 8, 4, 128),
 }
 MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense FP32 (matrix = vector peak)
 HBM_PEAK_GBPS = 8000.0         # MI355X_MICROARCH.md: HBM3E spec peak
@@ -52,6 +60,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
+    ap.add_argument("--scaling", default="strong", choices=("strong", "weak"),
+                    help="strong: the config's global batch split over the ranks; weak: the full batch per rank")
+    ap.add_argument("--batch", type=int, default=0, help="override the global batch (strong) / per-rank batch (weak)")
     ap.add_argument("--no-graph", action="store_true", help="run the N=1 step eagerly instead of a HIP graph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -181,11 +192,31 @@ def hmm_kernels(lib):
     return out
 
 
-def cpu_baseline(cfg, seconds):
-    """CPU oracle (oracle/ref_model.py) train step on the same shape, this host's cores."""
+def host_threads():
+    """Threads for the CPU baseline: the CPUs this process may run on
+    (len(os.sched_getaffinity(0))), capped by the cgroup CPU quota and OMP_NUM_THREADS when
+    those are set (a GPU box's affinity mask can list the whole machine while its share is
+    smaller).  Returns (threads, affinity_cpus)."""
+    n_aff = len(os.sched_getaffinity(0))
+    n = n_aff
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return n, n_aff
+
+
+def _oracle_step_times(cfg, B, threads, seconds, min_steps, warmup):
     from oracle import ref_model as RM
     import vqhmm
-    B, T, D, H, H2, K, U, TH = cfg
+    _, T, D, H, H2, K, U, TH = cfg
+    torch.set_num_threads(threads)
     torch.manual_seed(0)
     m = vqhmm.VAE_HMM(D, H, K, H2, u_dim=U, trans_hidden=TH)  # same init as the GPU run (CPU tensors)
     p = {k: v.detach().clone().requires_grad_(True) for k, v in m.state_dict().items()}
@@ -200,27 +231,71 @@ def cpu_baseline(cfg, seconds):
         RM.elbo(p, x, u, L, 1.0, K, U).backward()
         opt.step()
 
-    step()
+    for _ in range(warmup):
+        step()
     times = []
     t_end = time.perf_counter() + seconds
-    while time.perf_counter() < t_end or len(times) < 3:
+    while time.perf_counter() < t_end or len(times) < min_steps:
         t0 = time.perf_counter()
         step()
         times.append(time.perf_counter() - t0)
-    med = statistics.median(times)
-    return {"value": round(B / med, 1), "unit": "sequences/s", "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"{len(times)} full train steps (B={B}, T={T}, cfg2 shape) of the torch-CPU oracle, "
-                      f"median {med*1e3:.1f} ms/step"}
+    return statistics.median(times), len(times)
+
+
+def cpu_baseline(cfg, B, seconds):
+    """CPU oracle (oracle/ref_model.py, pinned bit-exact to the reference) train step on the
+    same shape: all the host threads this process may use (>= 3 warm-up steps, ~`seconds`
+    of timed steps), plus a 1-thread figure on a 256-sequence sample of the same workload."""
+    nthr, n_aff = host_threads()
+    saved = torch.get_num_threads()
+    try:
+        med, n = _oracle_step_times(cfg, B, nthr, seconds, 3, 3)
+        B1 = min(B, 256)
+        med1, n1 = _oracle_step_times(cfg, B1, 1, 0.0, 3, 1)
+    finally:
+        torch.set_num_threads(saved)
+    _, T = cfg[0], cfg[1]
+    return {"value": round(B / med, 1), "unit": "sequences/s", "cores": nthr, "kind": "port",
+            "sample": f"{n} full train steps (B={B}, T={T}) of the torch-CPU oracle after 3 warm-up steps, "
+                      f"median {med*1e3:.1f} ms/step, {nthr} threads ({n_aff} CPUs in the affinity mask, "
+                      f"capped by the cgroup quota / OMP_NUM_THREADS)",
+            "one_thread": {"value": round(B1 / med1, 1), "unit": "sequences/s", "cores": 1,
+                           "sample": f"{n1} train steps of B={B1}, T={T} after 1 warm-up, "
+                                     f"median {med1*1e3:.1f} ms/step"}}
+
+
+def spawn_ranks(n):
+    """`python bench.py --gpus N` without torchrun: start N fresh rank processes (this
+    parent never touches the GPU) on 127.0.0.1 and return the worst exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    return max(abs(p.wait()) for p in procs)
 
 
 def main():
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = int(os.environ.get("WORLD_SIZE", "0"))
+    if world == 0:
+        if a.gpus > 1:
+            sys.exit(spawn_ranks(a.gpus))
+        world = 1
+    if world != a.gpus:
+        sys.exit(f"bench.py: --gpus {a.gpus} but the launcher's WORLD_SIZE is {world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         torch.cuda.set_device(local)
         torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if torch.distributed.get_world_size() != world:
+            sys.exit("bench.py: process group size disagrees with WORLD_SIZE")
     else:
         torch.cuda.set_device(0)
     import vqhmm
@@ -228,7 +303,16 @@ def main():
     lib = _ext.load()
 
     cfg = CONFIGS[a.config]
-    B, T, D, H, H2, K, U, TH = cfg
+    Bglob, T, D, H, H2, K, U, TH = cfg
+    if a.batch:
+        Bglob = a.batch
+    if a.scaling == "strong":
+        if Bglob % world:
+            sys.exit(f"bench.py: global batch {Bglob} does not split over {world} ranks")
+        B = Bglob // world
+    else:
+        B = Bglob
+        Bglob = B * world
     torch.manual_seed(0)
     model = vqhmm.VAE_HMM(D, H, K, H2, u_dim=U, trans_hidden=TH).cuda()
     st = vqhmm.TrainState(model, lr=1e-3)
@@ -261,7 +345,7 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = t.item()
     ms_per_step = elapsed / a.steps * 1e3
-    value = world * B * a.steps / elapsed
+    value = Bglob * a.steps / elapsed
 
     roof = None
     kernels = None
@@ -280,23 +364,24 @@ def main():
         roof.update({"traffic": traffic_for(dom["name"], a.config), "kernel": dom["name"],
                      "avg_us": round(dom["us"], 2)})
         kernels = {s["name"]: round(s["us"], 2) for s in stages}
-    vq = vq_cfg3(lib) if rank == 0 else None
-    hmm = hmm_kernels(lib) if rank == 0 and not a.no_hmm else {}
+    vq = vq_cfg3(lib) if rank == 0 and world == 1 else None
+    hmm = hmm_kernels(lib) if rank == 0 and world == 1 and not a.no_hmm else {}
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(cfg, a.cpu_seconds)
+        cpu = cpu_baseline(cfg, B, a.cpu_seconds)
 
     if rank == 0:
         line = {
             "metric": "VAE_HMM train-step sequences/sec (K=3, T=200, D=5) at 1/2/4/8 MI355X",
             "value": round(value, 1), "unit": "sequences/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "scaling": a.scaling, "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": f"{a.config}: VAE_HMM train step (compute_loss+backward+Adam)",
-                       "global_batch": world * B, "seq_len": T, "K": K, "input_dim": D, "hidden_dim": H,
-                       "hidden_dim2": H2, "u_dim": U, "trans_hidden": TH,
-                       "parallelism": f"dp{world}" if world > 1 else "single", "hip_graph": use_graph},
+                       "global_batch": Bglob, "per_gpu_batch": B, "seq_len": T, "K": K, "input_dim": D,
+                       "hidden_dim": H, "hidden_dim2": H2, "u_dim": U, "trans_hidden": TH,
+                       "parallelism": f"dp{world}" if world > 1 else "single", "hip_graph": use_graph,
+                       "rccl_ranks": torch.distributed.get_world_size() if world > 1 else 0},
             "roofline": roof, "cpu_baseline": cpu,
             "step_kernels_us": kernels, "vq_cfg3": vq, **hmm,
         }

@@ -63,8 +63,11 @@ struct ElboPlan {
   float *dg2, *dg1, *dqd, *dlog, *dh2, *dh1, *dWc, *q0sum;
   int nwl;
   WLayer wl[8];  // 0 to_params, 1 dec2, 2 dec1', 3 to_logits, 4 enc2, 5 enc1, [6 Prior W1, 7 Prior W2]
+  float* img[32];  // per stage: packed conv2_kernel weight image (WImgJob), built by the prologue, or null
   size_t bytes;
 };
+
+void plan_images(ElboPlan& p, Carver& c);
 
 ElboPlan plan_elbo(const vqhmm_dims_t* d, int64_t B, int64_t T, void* ws) {
   ElboPlan p{};
@@ -131,6 +134,7 @@ ElboPlan plan_elbo(const vqhmm_dims_t* d, int64_t B, int64_t T, void* ws) {
     w.slab = c.take<float>((size_t)w.nchunks * w.N * w.C * w.ks);
     w.bslab = c.take<float>((size_t)w.nchunks * w.N);
   }
+  plan_images(p, c);
   p.bytes = c.off + 256;
   return p;
 }
@@ -249,6 +253,7 @@ ConvArgs conv_of(const ElboPlan& p, const float* const* wp, int st) {
   static const float* const kNull[VQHMM_NPARAMS] = {};
   const float* const* w = wp ? wp : kNull;  // stage_work() only needs the shapes
   ConvArgs a = conv_base(p);
+  a.Wimg = p.img[st];
   switch (st) {
     case S_ENC1:
       a.src = p.xp; a.Kc = p.D; a.ks = 3; a.W = w[ENC1_W]; a.bias = w[ENC1_B]; a.N = p.H; a.act = 1; a.out = p.h1e;
@@ -285,6 +290,35 @@ ConvArgs conv_of(const ElboPlan& p, const float* const* wp, int st) {
       break;
   }
   return a;
+}
+
+// Convolutions whose conv2_kernel launches take a packed weight image (built once per step in
+// the prologue, misc.hip wimg_slice) instead of re-packing W in every workgroup.
+const int kImgStages[] = {S_ENC1, S_ENC2, S_DEC1, S_DEC2, S_PAR_DG, S_DEC2_DG, S_DEC1_DG, S_LOGIT_DG, S_ENC2_DG};
+
+void plan_images(ElboPlan& p, Carver& c) {
+  for (int st : kImgStages) {
+    p.img[st] = nullptr;
+    const ConvArgs a = conv_of(p, nullptr, st);
+    if (conv2_supported(a)) p.img[st] = c.take<float>((size_t)c2_image_floats(a.N, a.Kc, a.ks));
+  }
+}
+
+// The prologue's image jobs: each conv's effective weight, the composed decoder conv1
+// (W' = W E^T, stages S_DEC1 / S_DEC1_DG) computed straight from W and E.
+int image_jobs(const ElboPlan& p, const float* const* w, WImgJob* jobs) {
+  int n = 0;
+  for (int st : kImgStages) {
+    if (!p.img[st]) continue;
+    const ConvArgs a = conv_of(p, w, st);
+    WImgJob j{};
+    j.W = a.W; j.w_dgrad = a.w_dgrad; j.N = a.N; j.Kc = a.Kc; j.ks = a.ks; j.img = p.img[st];
+    if (st == S_DEC1 || st == S_DEC1_DG) {
+      j.composed = 1; j.W = w[DEC1_W]; j.E = w[EMB]; j.H = p.H;
+    }
+    jobs[n++] = j;
+  }
+  return n;
 }
 
 // Staged head: Prior MLP as 1x1 convs over PCL rows, L1/L2 row kernels, then the
@@ -337,6 +371,9 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       a.u = c.u; a.U = p.U; a.usc = c.u_layout == 0 ? p.T : 1; a.ust = c.u_layout == 0 ? 1 : p.U; a.up = p.up;
       a.B = p.B; a.T = p.T;
       a.W = w[DEC1_W]; a.E = w[EMB]; a.H = p.H; a.K = p.K; a.Wc = p.Wc;
+      a.nimg = image_jobs(p, w, a.img);
+      a.wc_img_f = p.img[S_DEC1];
+      a.wc_img_d = p.img[S_DEC1_DG];
       return launch_prologue(a, s);
     }
     case S_COMPOSE:  // runs inside S_TOPCL's launch

@@ -220,12 +220,17 @@ __global__ __launch_bounds__(256, (C2Occ<NB, KCP, TAIL>::W)) void conv2_kernel(C
   const int lg4 = lane >> 4, l16 = lane & 15;
 
   // ---- weights once: Ws[tap][n][c] = Weff(n, c, tap)
-  for (int i = tid; i < KS * C::NW * C::KCW; i += 256) {
-    const int c = i % C::KCW, n = (i / C::KCW) % C::NW, tap = i / (C::KCW * C::NW);
-    float v = 0.f;
-    if (n < a.N && c < a.Kc)
-      v = a.w_dgrad ? a.W[((int64_t)c * a.N + n) * KS + (KS - 1 - tap)] : a.W[((int64_t)n * a.Kc + c) * KS + tap];
-    Ws[(tap * C::NW + n) * C::LDX + c] = v;
+  if (a.Wimg) {  // the step's prologue packed them in exactly this layout: float4 copy
+    const float4* src = reinterpret_cast<const float4*>(a.Wimg);
+    for (int i = tid; i < (int)(C::W_FLOATS / 4); i += 256) smem4[i] = src[i];
+  } else {
+    for (int i = tid; i < KS * C::NW * C::KCW; i += 256) {
+      const int c = i % C::KCW, n = (i / C::KCW) % C::NW, tap = i / (C::KCW * C::NW);
+      float v = 0.f;
+      if (n < a.N && c < a.Kc)
+        v = a.w_dgrad ? a.W[((int64_t)c * a.N + n) * KS + (KS - 1 - tap)] : a.W[((int64_t)n * a.Kc + c) * KS + tap];
+      Ws[(tap * C::NW + n) * C::LDX + c] = v;
+    }
   }
   // ---- per-lane epilogue constants
   float bias_r[NB][4];

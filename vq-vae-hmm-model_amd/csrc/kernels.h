@@ -15,6 +15,7 @@ struct ConvArgs {
   int ks;            // 1 or 3
   const float* W;
   int w_dgrad;       // 0: W is (N, Kc, ks); 1: W is (Kc, N, ks) used transposed + flipped
+  const float* Wimg; // conv2_kernel only: W already packed in its LDS layout (WImgJob), or null
   const float* bias; // (N) or null
   const float* scale;// device scalar multiplying the accumulator, or null
   int N;             // output channels
@@ -155,6 +156,24 @@ int launch_vq_argmin(const float* z, int64_t B, int64_t Dv, int64_t T, const flo
                      float* dmin, hipStream_t s);
 int launch_conv(const ConvArgs& a, hipStream_t s);
 bool conv2_supported(const ConvArgs& a);
+// Packed weight image of a conv2_kernel launch: img[(tap*NW + n)*LDX + c] = Weff(n, c, tap)
+// (zero past N / Kc), NW = 16*NB and LDX = 16*KCP + 4 for the launch's (NB, KCP) (c2_nb / c2_kcp).
+// Built once per step (prologue), so every workgroup stages its weights with float4 copies.
+// composed = 1: the logical weight is the decoder's folded conv1, Wc[o][k][tap] =
+// sum_h W[o][h][tap] E[k][h] (W (H,H,3), E (K,H)); the job writes only the image's zero
+// padding, the prologue's compose blocks write the Wc entries (PrologueArgs::wc_img_*).
+struct WImgJob {
+  const float* W;
+  const float* E;  // composed only
+  int composed, H; // composed only: H = reduction length of the fold
+  int w_dgrad, N, Kc, ks;
+  float* img;
+};
+__host__ __device__ inline int c2_nb(int N) { return N <= 16 ? 1 : N <= 32 ? 2 : 4; }
+__host__ __device__ inline int c2_kcp(int Kc) { return Kc <= 16 ? 1 : Kc <= 32 ? 2 : 4; }
+__host__ __device__ inline int64_t c2_image_floats(int N, int Kc, int ks) {
+  return (int64_t)ks * 16 * c2_nb(N) * (16 * c2_kcp(Kc) + 4);
+}
 int launch_conv2(const ConvArgs& a, hipStream_t s);
 int launch_wgrad(const WgradArgs& a, hipStream_t s);
 int64_t wgrad_chunks(int64_t R, int64_t tiles);
@@ -210,12 +229,18 @@ int launch_logits_bwd(const float* q, const float* dq_dec, const float* dqx, con
 // CF / (B,T,C) tensor -> PCL (R, ld4(C)) with zero pad rows / channels:
 // dst[b*(T+2)+1+t][c] = src[b*C*T + c*sc + t*st]
 int launch_to_pcl(const float* src, int C, int64_t B, int T, int64_t sc, int64_t st, float* dst, hipStream_t s);
-struct PrologueArgs {  // step prologue: x, u -> PCL and the composed decoder conv1 weight (misc.hip)
+constexpr int MAX_WIMG = 12;
+struct PrologueArgs {  // step prologue: x, u -> PCL, the composed decoder conv1 weight and the conv weight images
   const float* x; int D; int64_t xsc, xst; float* xp;
   const float* u; int U; int64_t usc, ust; float* up;
   int64_t B; int T;
   const float* W; const float* E; int H, K; float* Wc;
-  unsigned nbx, nbu;  // set by launch_prologue
+  WImgJob img[MAX_WIMG];
+  int nimg;
+  float* wc_img_f;  // images of the composed decoder conv1 (forward / data gradient), or null
+  float* wc_img_d;
+  unsigned nbx, nbu;                // set by launch_prologue
+  unsigned img_blk0[MAX_WIMG + 1];  // set by launch_prologue: first block of each image
 };
 int launch_prologue(PrologueArgs a, hipStream_t s);
 int launch_gather_chunks(const float* src, const int64_t* meta, int64_t B, int64_t C, int64_t Tm, float* out,

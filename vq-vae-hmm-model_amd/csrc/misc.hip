@@ -128,8 +128,11 @@ int launch_finalize_loss(const double* part, int nblk, const int64_t* lengths, c
 // ------------------------------------------------------------ composed decoder conv1
 // Wc[o][k][tap] = sum_h W[o][h][tap] * E[k][h];  W (H,H,3), E (K,H), Wc (H,K,3).
 // One block per output channel o; W[o] and E staged in LDS.
+// img_f / img_d (nullable): the packed conv2_kernel images of Wc for the forward (N = H, Kc = K)
+// and the data gradient (N = K, Kc = H) — this block writes their entries of channel o; the
+// image jobs (wimg_slice, composed) write the zero padding around them.
 __device__ __forceinline__ void compose_fwd_block(const float* W, const float* E, int H, int K, float* Wc, int o,
-                                                  float* cs) {
+                                                  float* cs, float* img_f = nullptr, float* img_d = nullptr) {
   float* wo = cs;          // [H*3]
   float* es = cs + H * 3;  // [K*H]
   for (int i = threadIdx.x; i < H * 3; i += 256) wo[i] = W[(int64_t)o * H * 3 + i];
@@ -140,6 +143,8 @@ __device__ __forceinline__ void compose_fwd_block(const float* W, const float* E
     float s = 0.f;
     for (int h = 0; h < H; ++h) s = fmaf(wo[h * 3 + tap], es[k * H + h], s);
     Wc[(int64_t)o * K * 3 + i] = s;
+    if (img_f) img_f[((int64_t)tap * 16 * c2_nb(H) + o) * (16 * c2_kcp(K) + 4) + k] = s;
+    if (img_d) img_d[((int64_t)(2 - tap) * 16 * c2_nb(K) + k) * (16 * c2_kcp(H) + 4) + o] = s;
   }
 }
 __global__ __launch_bounds__(256) void compose_fwd_kernel(const float* W, const float* E, int H, int K, float* Wc) {
@@ -373,9 +378,32 @@ __global__ __launch_bounds__(256) void to_pcl_kernel(const float* __restrict__ s
                                                      int64_t sc, int64_t st, float* __restrict__ dst) {
   to_pcl_slot(src, C, B, T, sc, st, dst, (int64_t)blockIdx.x * 256 + threadIdx.x);
 }
-// Step prologue in ONE launch (the step's first three tiny pieces of work): blocks
-// [0, nbx) convert x and [nbx, nbx + nbu) convert u to PCL (to_pcl_kernel), the last H
-// blocks compose the decoder conv1 weight (compose_fwd_kernel).
+// One 256-entry slice of a packed conv weight image (WImgJob, kernels.h).
+__device__ __forceinline__ void wimg_slice(const WImgJob& j, int64_t i0) {
+  const int NW = 16 * c2_nb(j.N), LDX = 16 * c2_kcp(j.Kc) + 4;
+  const int64_t n_img = (int64_t)j.ks * NW * LDX;
+  const int64_t i = i0 + threadIdx.x;
+  if (i >= n_img) return;
+  const int tap = (int)(i / (NW * LDX));
+  const int rem = (int)(i - (int64_t)tap * NW * LDX);
+  const int n = rem / LDX, c = rem - n * LDX;
+  float v = 0.f;
+  if (n < j.N && c < j.Kc) {
+    // stored (a, b, tw): forward W[n][c][tap]; data gradient W[c][n][ks - 1 - tap]
+    const int a = j.w_dgrad ? c : n, b = j.w_dgrad ? n : c, tw = j.w_dgrad ? j.ks - 1 - tap : tap;
+    if (j.composed) return;  // Wc entries: written by the compose block of output channel a
+    {
+      const int inner = j.w_dgrad ? j.N : j.Kc;
+      v = j.W[((int64_t)a * inner + b) * j.ks + tw];
+    }
+  }
+  j.img[i] = v;
+}
+
+// Step prologue in ONE launch (the step's first tiny pieces of work): blocks
+// [0, nbx) convert x and [nbx, nbx + nbu) convert u to PCL (to_pcl_kernel), the next H
+// blocks compose the decoder conv1 weight (compose_fwd_kernel), the rest pack the conv
+// weight images (wimg_slice).
 __global__ __launch_bounds__(256) void prologue_kernel(PrologueArgs a) {
   extern __shared__ float cs[];
   const unsigned bx = blockIdx.x;
@@ -383,16 +411,25 @@ __global__ __launch_bounds__(256) void prologue_kernel(PrologueArgs a) {
     to_pcl_slot(a.x, a.D, a.B, a.T, a.xsc, a.xst, a.xp, (int64_t)bx * 256 + threadIdx.x);
   } else if (bx < a.nbx + a.nbu) {
     to_pcl_slot(a.u, a.U, a.B, a.T, a.usc, a.ust, a.up, (int64_t)(bx - a.nbx) * 256 + threadIdx.x);
+  } else if (bx < a.nbx + a.nbu + (unsigned)a.H) {
+    compose_fwd_block(a.W, a.E, a.H, a.K, a.Wc, (int)(bx - a.nbx - a.nbu), cs, a.wc_img_f, a.wc_img_d);
   } else {
-    compose_fwd_block(a.W, a.E, a.H, a.K, a.Wc, (int)(bx - a.nbx - a.nbu), cs);
+    const unsigned ib = bx - a.nbx - a.nbu - (unsigned)a.H;
+    int j = 0;
+    while (j + 1 < a.nimg && ib >= a.img_blk0[j + 1]) ++j;
+    wimg_slice(a.img[j], (int64_t)(ib - a.img_blk0[j]) * 256);
   }
 }
 int launch_prologue(PrologueArgs a, hipStream_t s) {
   const int64_t R = a.B * (int64_t)(a.T + 2);
   a.nbx = (unsigned)cdiv(R * (ld4(a.D) / 4), 256);
   a.nbu = (unsigned)cdiv(R * (ld4(a.U) / 4), 256);
+  if (a.nimg < 0 || a.nimg > MAX_WIMG) return VQHMM_EINVAL;
+  a.img_blk0[0] = 0;
+  for (int j = 0; j < a.nimg; ++j)
+    a.img_blk0[j + 1] = a.img_blk0[j] + (unsigned)cdiv(c2_image_floats(a.img[j].N, a.img[j].Kc, a.img[j].ks), 256);
   const size_t lds = (size_t)(a.H * 3 + a.K * a.H) * 4;
-  prologue_kernel<<<a.nbx + a.nbu + (unsigned)a.H, 256, lds, s>>>(a);
+  prologue_kernel<<<a.nbx + a.nbu + (unsigned)a.H + a.img_blk0[a.nimg], 256, lds, s>>>(a);
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
 }
