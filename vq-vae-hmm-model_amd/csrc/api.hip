@@ -5,6 +5,7 @@
 #include "vqhmm.h"
 
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "kernels.h"
@@ -30,6 +31,15 @@ struct Carver {
     return p;
   }
 };
+
+// A/B switch to the previous tile-barrier MFMA head (VQHMM_HEAD=tile), read once.
+bool head_legacy() {
+  static const bool v = [] {
+    const char* e = getenv("VQHMM_HEAD");
+    return e && strcmp(e, "tile") == 0;
+  }();
+  return v;
+}
 
 bool dims_ok(const vqhmm_dims_t* d) {
   return d && d->input_dim > 0 && d->hidden_dim > 0 && d->K > 0 && d->hidden_dim2 > 0 && d->u_dim > 0 &&
@@ -58,6 +68,7 @@ struct ElboPlan {
   float *loss, *pieces;
   // staged head (shapes the fused heads do not cover): Prior MLP as 1x1 convs
   bool staged;
+  bool wave_head;  // head_wave.hip (else head_mfma / head.hip)
   float *hid, *lgA, *dhid, *nx, *dqc, *trw, *logpi;
   // backward
   float *dg2, *dg1, *dqd, *dlog, *dh2, *dh1, *dWc, *q0sum;
@@ -86,7 +97,12 @@ ElboPlan plan_elbo(const vqhmm_dims_t* d, int64_t B, int64_t T, void* ws) {
   p.g2 = c.take<float>(R * ld4(H));
   p.par = c.take<float>(R * ld4(2 * D));
   p.Wc = c.take<float>((size_t)H * K * 3);
-  p.hgrid = head_grid(R);
+  {
+    HeadArgs hc{};
+    hc.K = K; hc.U = p.U; hc.TH = p.TH; hc.D = D;
+    p.wave_head = head_mfma_supported(hc) && p.U <= 4 && !head_legacy();
+  }
+  p.hgrid = p.wave_head ? head_wave_grid(R) : head_grid(R);
   p.dpar = c.take<float>(R * ld4(2 * D));
   p.dqx = c.take<float>(R * ld4(K));
   p.dlx = c.take<float>(R * ld4(K));
@@ -409,6 +425,7 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       h.beta = c.beta; h.norm = c.norm; h.need_grad = c.need_grad;
       h.dpar = p.dpar; h.dqx = p.dqx; h.dlx = p.dlx; h.part = p.part;
       h.slab_W1 = p.sW1; h.slab_b1 = p.sb1; h.slab_W2 = p.sW2; h.slab_b2 = p.sb2; h.slab_q0 = p.sq0;
+      if (p.wave_head) return launch_head_wave(h, p.hgrid, s);
       return launch_head(h, p.hgrid, s);
     }
     case S_FINAL:

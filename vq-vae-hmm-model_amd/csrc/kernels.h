@@ -204,6 +204,9 @@ bool fused_head_supported(const HeadArgs& a);
 int launch_staged_head(const StagedHeadArgs& a, int l2grid, hipStream_t s);
 
 int head_grid(int64_t R);
+// wave-window head (head_wave.hip), same support as head_mfma; its grid / slab count
+int head_wave_grid(int64_t R);
+int launch_head_wave(const HeadArgs& a, int grid, hipStream_t s);
 bool head_mfma_supported(const HeadArgs& a);
 int launch_head_mfma(const HeadArgs& a, int grid, hipStream_t s);
 int launch_head(const HeadArgs& a, int grid, hipStream_t s);
