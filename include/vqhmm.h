@@ -128,6 +128,17 @@ int vqhmm_elbo_fwd_f32(const vqhmm_dims_t* dims, const float* const* params, con
 int vqhmm_elbo_bwd_f32(const vqhmm_dims_t* dims, const float* const* params, const float* x,
                        const int64_t* norm, int64_t B, int64_t T, float beta, const float* grad_scale,
                        void* workspace, size_t ws_bytes, float* grad, void* stream);
+/* Backward + torch.optim.Adam step (the single-process train_model step,
+ * VQ_VAE_HMM_fixed.py:155-157): vqhmm_elbo_bwd_f32 (grad_scale NULL) whose last launch
+ * also applies vqhmm_adam_f32's update to every parameter element (same formula, same
+ * device step counter and ticket), saving the separate update launch; grad still receives
+ * the full gradient.  params[i] must be param + offset[i] of vqhmm_param_layout (the flat
+ * buffer Adam updates in place).  adam_grad_scale multiplies the gradient inside Adam only. */
+int vqhmm_elbo_bwd_adam_f32(const vqhmm_dims_t* dims, const float* const* params, const float* x,
+                            const int64_t* norm, int64_t B, int64_t T, float beta, void* workspace,
+                            size_t ws_bytes, float* grad, float* param, float* exp_avg, float* exp_avg_sq,
+                            double lr, double beta1, double beta2, double eps, int64_t* step,
+                            float adam_grad_scale, void* stream);
 /* Device addresses (inside the workspace) of the last forward's loss and of its
  * pieces [recon, prior, entropy] (for tests).  Host-only, no GPU access. */
 int vqhmm_elbo_pieces(const vqhmm_dims_t* dims, int64_t B, int64_t T, const void* workspace,

@@ -71,7 +71,8 @@ struct ElboPlan {
   bool wave_head;  // head_wave.hip (else head_mfma / head.hip)
   float *hid, *lgA, *dhid, *nx, *dqc, *trw, *logpi;
   // backward
-  float *dg2, *dg1, *dqd, *dlog, *dh2, *dh1, *dWc, *q0sum;
+  float *dg2, *dg1, *dqd, *dlog, *dh2, *dh1, *dWc;
+  float *Ecopy, *Wcopy;  // the prologue's copies of decoder.embeddings / decoder.conv1 weights (compose_adam)
   int nwl;
   WLayer wl[8];  // 0 to_params, 1 dec2, 2 dec1', 3 to_logits, 4 enc2, 5 enc1, [6 Prior W1, 7 Prior W2]
   float* img[32];  // per stage: packed conv2_kernel weight image (WImgJob), built by the prologue, or null
@@ -137,7 +138,8 @@ ElboPlan plan_elbo(const vqhmm_dims_t* d, int64_t B, int64_t T, void* ws) {
   p.dh2 = c.take<float>(R * ld4(H2));
   p.dh1 = c.take<float>(R * ld4(H));
   p.dWc = c.take<float>((size_t)H * K * 3);
-  p.q0sum = c.take<float>(K);
+  p.Ecopy = c.take<float>((size_t)K * H);
+  p.Wcopy = c.take<float>((size_t)H * H * 3);
   const int shapes[8][3] = {{2 * D, H, 1}, {H, H, 3}, {H, K, 3}, {K, H2, 1}, {H2, H, 3}, {H, D, 3},
                             {p.TH, p.U, 1}, {K * K, p.TH, 1}};
   p.nwl = p.staged ? 8 : 6;
@@ -165,7 +167,7 @@ ConvArgs conv_base(const ElboPlan& p) {
 
 extern "C" {
 
-int32_t vqhmm_abi_version(void) { return 3; }
+int32_t vqhmm_abi_version(void) { return 4; }
 
 int vqhmm_param_layout(const vqhmm_dims_t* d, int64_t off[VQHMM_NPARAMS + 1]) {
   if (!dims_ok(d) || !off) return VQHMM_EINVAL;
@@ -247,8 +249,8 @@ const char* kStageNames[S_COUNT] = {
     "elbo_head", "finalize_loss", "to_params_dgrad", "dec_conv2_dgrad", "dec_conv1_dgrad(+logits_bwd, to_logits_dgrad if K<=4)",
     "logits_bwd(K>4)",
     "to_logits_dgrad(K>4)", "enc_conv2_dgrad", "to_params_wgrad", "dec_conv2_wgrad", "dec_conv1_wgrad",
-    "to_logits_wgrad", "enc_conv2_wgrad", "enc_conv1_wgrad", "reduce_slabs", "compose_bwd+log_prior_grad",
-    "(log_prior_grad: in compose_bwd)"};
+    "to_logits_wgrad", "enc_conv2_wgrad", "enc_conv1_wgrad", "grad_tail(reduce_slabs+log_prior_grad)",
+    "compose_bwd[+adam]", "(log_prior_grad: in grad_tail)"};
 
 struct StepCtx {
   const float* const* w;
@@ -263,6 +265,7 @@ struct StepCtx {
   double* loss_accum;
   const float* gscale;
   float* g;
+  const AdamArgs* adam;  // non-null: Adam fused into the step's last launch (S_COMPOSE_BWD)
 };
 
 ConvArgs conv_of(const ElboPlan& p, const float* const* wp, int st) {
@@ -390,6 +393,8 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       a.nimg = image_jobs(p, w, a.img);
       a.wc_img_f = p.img[S_DEC1];
       a.wc_img_d = p.img[S_DEC1_DG];
+      a.Ecopy = p.Ecopy;
+      a.Wcopy = p.Wcopy;
       return launch_prologue(a, s);
     }
     case S_COMPOSE:  // runs inside S_TOPCL's launch
@@ -450,10 +455,10 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       vqhmm_param_layout(&d, off);
       float* g = c.g;
       const float* gs = c.gscale;
-      SlabSeg segs[18];
+      TailArgs ta{};
       int n = 0;
       auto seg = [&](const float* slab, int64_t nch, int64_t len, float* out, const float* scale) {
-        segs[n++] = SlabSeg{slab, out, scale, nch, len};
+        ta.s[n++] = SlabSeg{slab, out, scale, nch, len};
       };
       const WLayer* wl = p.wl;
       seg(wl[0].slab, wl[0].nchunks, (int64_t)wl[0].N * wl[0].C, g + off[PAR_W], gs);  // dpar is unscaled
@@ -473,21 +478,30 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
         seg(wl[6].bslab, wl[6].nchunks, p.TH, g + off[TN0_B], gs);
         seg(wl[7].slab, wl[7].nchunks, (int64_t)p.K * p.K * p.TH, g + off[TN2_W], gs);
         seg(wl[7].bslab, wl[7].nchunks, (int64_t)p.K * p.K, g + off[TN2_B], gs);
-        seg(p.sq0, 1, p.K, p.q0sum, nullptr);
       } else {
         seg(p.sW1, p.hgrid, (int64_t)p.TH * p.U, g + off[TN0_W], gs);
         seg(p.sb1, p.hgrid, p.TH, g + off[TN0_B], gs);
         seg(p.sW2, p.hgrid, (int64_t)p.K * p.K * p.TH, g + off[TN2_W], gs);
         seg(p.sb2, p.hgrid, (int64_t)p.K * p.K, g + off[TN2_B], gs);
-        seg(p.sq0, p.hgrid, p.K, p.q0sum, nullptr);
       }
-      return launch_reduce_slabs(segs, n, s);
+      ta.nseg = n;
+      ta.q0slab = p.sq0;
+      ta.q0chunks = p.staged ? 1 : p.hgrid;
+      ta.lp = LogPriorGradArgs{nullptr, w[LOG_PRIOR], p.K, c.beta, c.norm, p.B, c.gscale, g + off[LOG_PRIOR]};
+      return launch_grad_tail(ta, s);
     }
     case S_COMPOSE_BWD: {
       int64_t off[VQHMM_NPARAMS + 1];
       vqhmm_dims_t d{p.D, p.H, p.K, p.H2, p.U, p.TH};
       vqhmm_param_layout(&d, off);
-      const LogPriorGradArgs lp{p.q0sum, w[LOG_PRIOR], p.K, c.beta, c.norm, p.B, c.gscale, c.g + off[LOG_PRIOR]};
+      if (c.adam) {  // + Adam on every element: the step's last launch
+        ComposeAdamArgs ca{};
+        ca.dWc = p.dWc; ca.Ecopy = p.Ecopy; ca.Wcopy = p.Wcopy; ca.H = p.H; ca.K = p.K;
+        ca.g = c.g; ca.n = off[VQHMM_NPARAMS]; ca.off_w = off[DEC1_W]; ca.off_e = off[EMB];
+        ca.adam = *c.adam;
+        return launch_compose_adam(ca, s);
+      }
+      const LogPriorGradArgs lp{nullptr, nullptr, p.K, c.beta, c.norm, p.B, c.gscale, nullptr};  // in S_REDUCE
       return launch_compose_bwd(p.dWc, w[DEC1_W], w[EMB], p.H, p.K, c.g + off[DEC1_W], c.g + off[EMB], lp, s);
     }
     case S_LOGPRIOR:  // runs inside S_COMPOSE_BWD's launch
@@ -546,7 +560,7 @@ int vqhmm_elbo_fwd_f32(const vqhmm_dims_t* d, const float* const* w, const float
     if (!w[i]) return VQHMM_EINVAL;
   ElboPlan p = plan_elbo(d, B, T, ws);
   if (ws_bytes < p.bytes) return VQHMM_EWORKSPACE;
-  StepCtx c{w, x, u, u_layout, lengths, norm, beta, need_grad, loss, loss_accum, nullptr, nullptr};
+  StepCtx c{w, x, u, u_layout, lengths, norm, beta, need_grad, loss, loss_accum, nullptr, nullptr, nullptr};
   for (int st = FWD_FIRST; st <= FWD_LAST; ++st)
     if (int rc = run_stage(p, c, st, (hipStream_t)stream)) return rc;
   return VQHMM_OK;
@@ -558,7 +572,26 @@ int vqhmm_elbo_bwd_f32(const vqhmm_dims_t* d, const float* const* w, const float
   if (!dims_ok(d) || !w || B <= 0 || T <= 0 || !x || !ws || !g) return VQHMM_EINVAL;
   ElboPlan p = plan_elbo(d, B, T, ws);
   if (ws_bytes < p.bytes) return VQHMM_EWORKSPACE;
-  StepCtx c{w, x, nullptr, 0, nullptr, norm, beta, 1, nullptr, nullptr, grad_scale, g};
+  StepCtx c{w, x, nullptr, 0, nullptr, norm, beta, 1, nullptr, nullptr, grad_scale, g, nullptr};
+  for (int st = BWD_FIRST; st <= BWD_LAST; ++st)
+    if (int rc = run_stage(p, c, st, (hipStream_t)stream)) return rc;
+  return VQHMM_OK;
+}
+
+int vqhmm_elbo_bwd_adam_f32(const vqhmm_dims_t* d, const float* const* w, const float* x, const int64_t* norm,
+                            int64_t B, int64_t T, float beta, void* ws, size_t ws_bytes, float* g, float* param,
+                            float* exp_avg, float* exp_avg_sq, double lr, double beta1, double beta2, double eps,
+                            int64_t* step, float grad_scale, void* stream) {
+  if (!dims_ok(d) || !w || B <= 0 || T <= 0 || !x || !ws || !g || !param || !exp_avg || !exp_avg_sq || !step)
+    return VQHMM_EINVAL;
+  ElboPlan p = plan_elbo(d, B, T, ws);
+  if (ws_bytes < p.bytes) return VQHMM_EWORKSPACE;
+  int64_t off[VQHMM_NPARAMS + 1];
+  vqhmm_param_layout(d, off);
+  for (int i = 0; i < VQHMM_NPARAMS; ++i)  // the last launch updates param in place: w must be its views
+    if (w[i] != param + off[i]) return VQHMM_EINVAL;
+  AdamArgs ad{param, exp_avg, exp_avg_sq, step, lr, beta1, beta2, eps, grad_scale};
+  StepCtx c{w, x, nullptr, 0, nullptr, norm, beta, 1, nullptr, nullptr, nullptr, g, &ad};
   for (int st = BWD_FIRST; st <= BWD_LAST; ++st)
     if (int rc = run_stage(p, c, st, (hipStream_t)stream)) return rc;
   return VQHMM_OK;
@@ -589,7 +622,7 @@ int vqhmm_elbo_stage_f32(const vqhmm_dims_t* d, const float* const* w, const flo
   if (!dims_ok(d) || !w || !ws || stage < 0 || stage >= S_COUNT) return VQHMM_EINVAL;
   ElboPlan p = plan_elbo(d, B, T, ws);
   if (ws_bytes < p.bytes) return VQHMM_EWORKSPACE;
-  StepCtx c{w, x, u, u_layout, lengths, norm, beta, 1, p.loss, nullptr, nullptr, grad};
+  StepCtx c{w, x, u, u_layout, lengths, norm, beta, 1, p.loss, nullptr, nullptr, grad, nullptr};
   return run_stage(p, c, stage, (hipStream_t)stream);
 }
 

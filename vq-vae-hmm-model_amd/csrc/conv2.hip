@@ -24,7 +24,7 @@ template <int NB, int KCP, int KS, int PB>
 struct C2Cfg {
   static constexpr int BM = 4 * PB * 16;       // rows per tile
   static constexpr int KCW = KCP * 16;         // padded input channels
-  static constexpr int LDX = KCW + 4;          // LDS row stride (conflict-free float4 reads)
+  static constexpr int LDX = KCW + 8;          // LDS row stride = c2_ldx: conflict-free b128 reads
   static constexpr int NW = NB * 16;           // padded output channels
   static constexpr int XROWS = BM + 2;
   static constexpr int XF4 = XROWS * KCW / 4;  // float4 slots of one X tile

@@ -145,6 +145,16 @@ struct PriorArgs {
   float* log_A;  // (B, T, K, K)
 };
 
+struct LogPriorGradArgs {  // log_prior gradient (misc.hip log_prior_grad_body); out == null: skipped
+  const float* q0sum;
+  const float* log_prior;
+  int K;
+  float beta;
+  const int64_t* norm;
+  int64_t B;
+  const float* scale;
+  float* out;
+};
 struct SlabSeg {
   const float* slab;   // [nchunks][len]
   float* out;          // [len]
@@ -171,8 +181,11 @@ struct WImgJob {
 };
 __host__ __device__ inline int c2_nb(int N) { return N <= 16 ? 1 : N <= 32 ? 2 : 4; }
 __host__ __device__ inline int c2_kcp(int Kc) { return Kc <= 16 ? 1 : Kc <= 32 ? 2 : 4; }
+// LDS row stride of conv2_kernel's W / X tiles: 16*KCP + 8 floats makes the ds_read_b128 operand reads
+// (lane (lg4, l16) -> row l16, float4 lg4) bank-conflict free in all four 16-lane groups (+4 was 2-way)
+__host__ __device__ inline int c2_ldx(int Kc) { return 16 * c2_kcp(Kc) + 8; }
 __host__ __device__ inline int64_t c2_image_floats(int N, int Kc, int ks) {
-  return (int64_t)ks * 16 * c2_nb(N) * (16 * c2_kcp(Kc) + 4);
+  return (int64_t)ks * 16 * c2_nb(N) * c2_ldx(Kc);
 }
 int launch_conv2(const ConvArgs& a, hipStream_t s);
 int launch_wgrad(const WgradArgs& a, hipStream_t s);
@@ -211,20 +224,46 @@ bool head_mfma_supported(const HeadArgs& a);
 int launch_head_mfma(const HeadArgs& a, int grid, hipStream_t s);
 int launch_head(const HeadArgs& a, int grid, hipStream_t s);
 int launch_prior_fwd(const PriorArgs& p, hipStream_t s);
-int launch_reduce_slabs(const SlabSeg* segs, int n, hipStream_t s);
+// Backward tail (misc.hip grad_tail_kernel), ONE launch: every gradient segment's slabs summed in a
+// fixed chunk order (deterministic, no atomics) and scaled; one extra workgroup reduces the q0 slab
+// and writes the log_prior gradient.
+constexpr int MAX_SEGS = 24;
+struct TailArgs {
+  SlabSeg s[MAX_SEGS];
+  int64_t blk_start[MAX_SEGS + 1];  // set by launch_grad_tail
+  int nseg;
+  const float* q0slab;   // [q0chunks][K]: sum_b q[b, :, 0] partials (log_prior gradient), or null
+  int64_t q0chunks;
+  LogPriorGradArgs lp;   // q0sum unused (the tail block reduces q0slab itself)
+};
+// torch.optim.Adam over the flat buffers (misc.hip adam_kernel / compose_adam_kernel)
+struct AdamArgs {
+  float* p;
+  float* m;
+  float* v;
+  int64_t* step;         // device step counter (+ completion ticket in the upper 32 bits)
+  double lr, b1, b2, eps;
+  float gmul;
+};
+// The step's last launch when Adam is fused (single process): the composed decoder conv1's
+// dW[o][h][tap] = sum_k dWc[o][k][tap] E[k][h] and dE[k][h] = sum_{o,tap} dWc[o][k][tap] W[o][h][tap]
+// written into g (E, W: the prologue's copies, since this launch updates the parameters), then
+// every element's Adam update.
+struct ComposeAdamArgs {
+  const float* dWc;      // (H, K, 3) reduced
+  const float* Ecopy;    // (K, H)
+  const float* Wcopy;    // (H, H, 3)
+  int H, K;
+  float* g;              // flat gradient
+  int64_t n;             // elements
+  int64_t off_w, off_e;  // element offsets of decoder.conv1.weight and decoder.embeddings.weight
+  AdamArgs adam;
+};
+int launch_compose_adam(const ComposeAdamArgs& a, hipStream_t s);
+int launch_grad_tail(TailArgs& a, hipStream_t s);
 int launch_finalize_loss(const double* part, int nblk, const int64_t* lengths, const int64_t* norm, int64_t B, int T,
                          int D, float beta, float* loss, double* accum, float* pieces, hipStream_t s);
 int launch_compose_fwd(const float* W, const float* E, int H, int K, float* Wc, hipStream_t s);
-struct LogPriorGradArgs {  // log_prior gradient (misc.hip log_prior_grad_body); out == null: skipped
-  const float* q0sum;
-  const float* log_prior;
-  int K;
-  float beta;
-  const int64_t* norm;
-  int64_t B;
-  const float* scale;
-  float* out;
-};
 int launch_compose_bwd(const float* dWc, const float* W, const float* E, int H, int K, float* dW, float* dE,
                        const LogPriorGradArgs& lp, hipStream_t s);
 int launch_logits_bwd(const float* q, const float* dq_dec, const float* dqx, const float* dlx, const float* scale,
@@ -242,6 +281,8 @@ struct PrologueArgs {  // step prologue: x, u -> PCL, the composed decoder conv1
   int nimg;
   float* wc_img_f;  // images of the composed decoder conv1 (forward / data gradient), or null
   float* wc_img_d;
+  float* Ecopy;     // (K, H) / (H, H, 3) copies of the embedding and decoder.conv1's weight for the
+  float* Wcopy;     // fused compose + Adam launch, or null
   unsigned nbx, nbu;                // set by launch_prologue
   unsigned img_blk0[MAX_WIMG + 1];  // set by launch_prologue: first block of each image
 };

@@ -1,10 +1,12 @@
 // Small kernels of the training step:
-//   reduce_slabs     deterministic split-K reduction of per-workgroup gradient partials
-//                    into the flat gradient buffer (fixed chunk order, no atomics)
+//   grad_tail        deterministic split-K reduction of the per-workgroup gradient slabs into
+//                    the flat gradient (fixed chunk order, no atomics) + the log_prior gradient
+//   compose_adam     (single process) the composed decoder conv1's dW / dE and every element's
+//                    Adam update in the step's last launch
 //   finalize_loss    loss = recon + beta*(prior - entropy)  (VQ_VAE_HMM_fixed.py:137)
 //   compose_fwd/bwd  decoder embedding folded into decoder.conv1:
 //                    conv1(q^T E) == conv1'(q) with W'[o,k,tap] = sum_h W[o,h,tap] E[k,h];
-//                    compose_bwd's extra workgroup also does the log_prior gradient
+//                    (compose_bwd: the generic path's dW / dE when the tail cannot take them)
 //   prologue         x, u -> PCL + compose_fwd in one launch (the step's first stage)
 //   logits_bwd       softmax backward of q = softmax(logits) (:114) + entropy's direct term
 //   adam             torch.optim.Adam update (defaults of train_model, :146)
@@ -12,36 +14,125 @@
 
 namespace vqhmm {
 
-// ------------------------------------------------------------ slab reduction
-constexpr int MAX_SEGS = 24;
-struct SlabSegs {
-  SlabSeg s[MAX_SEGS];
-  int64_t blk_start[MAX_SEGS + 1];  // prefix of column-blocks per segment
-  int nseg;
+// ------------------------------------------------------------ backward tail
+// torch.optim.Adam's update of element i (adam_kernel below has the derivation and the device
+// step counter; tn = this step's count).  Split so a caller can load the element's state early
+// (adam_load) and apply it once the gradient is known (adam_apply).  misc.hip is built with
+// -ffp-contract=off, so every launch that applies it rounds identically.
+struct AdamElem {
+  float step_size, bc2s, m, v, p;
 };
+__device__ __forceinline__ AdamElem adam_load(const AdamArgs& a, int64_t i, int64_t tn) {
+  const double t = (double)tn;
+  AdamElem e;
+  e.step_size = (float)(a.lr / (1.0 - pow(a.b1, t)));
+  e.bc2s = (float)sqrt(1.0 - pow(a.b2, t));
+  e.m = a.m[i];
+  e.v = a.v[i];
+  e.p = a.p[i];
+  return e;
+}
+__device__ __forceinline__ void adam_apply(const AdamArgs& a, int64_t i, float g, const AdamElem& e) {
+  const float gi = g * a.gmul;
+  const float mi = e.m + (float)(1.0 - a.b1) * (gi - e.m);
+  const float vi = e.v * (float)a.b2 + (float)(1.0 - a.b2) * gi * gi;
+  a.m[i] = mi;
+  a.v[i] = vi;
+  const float denom = sqrtf(vi) / e.bc2s + (float)a.eps;
+  a.p[i] = e.p + (-e.step_size) * (mi / denom);
+}
+// The step counter advances inside the update's own launch: every workgroup read
+// t = (*step & 0xffffffff) + 1 at its start, then takes a ticket in the upper 32 bits here; the
+// last one to do so (all reads are behind it) stores t with a zero ticket.  No fence: the ticket
+// orders only the reads of *step, not this workgroup's parameter writes.
+__device__ __forceinline__ void adam_ticket(int64_t* step, int64_t tn) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    auto* st = reinterpret_cast<unsigned long long*>(step);
+    const unsigned long long old = atomicAdd(st, 1ull << 32);
+    if ((old >> 32) == gridDim.x - 1) atomicExch(st, (unsigned long long)tn);
+  }
+}
 
-// One workgroup = 64 consecutive columns x all chunks.  Where a segment's rows are
-// float4-aligned (len % 4 == 0, 16-B slab base), 16 lanes x float4 cover the 64
-// columns and 16 chunk phases keep 16 x 8 wide loads in flight per column group;
-// otherwise 64 lanes x 4 phases of scalar loads.  Phases combine in a fixed order
-// (deterministic, no atomics).
-__global__ __launch_bounds__(256) void reduce_slabs_kernel(SlabSegs segs) {
+// Columns [v0, v0 + nv) of a [nch][ld] slab summed over its chunks into red[0, nv) (LDS), by the
+// whole workgroup: value v is split over P = 256 / nv chunk phases (16 interleaved partials each),
+// combined in a fixed order.  Ends with a barrier.
+__device__ void block_reduce_cols(const float* slab, int64_t nch, int64_t ld, int64_t v0, int nv, float* red,
+                                  float* scratch) {
+  const int tid = threadIdx.x;
+  for (int base = 0; base < nv; base += 256) {
+    const int n = min(256, nv - base);
+    const int P = 256 / n;
+    const int v = tid % n, ph = tid / n;
+    if (ph < P) {  // 16 loads in flight per round: the chunk loop is latency-bound
+      float acc[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+      const float* col = slab + v0 + base + v;
+      int64_t c = ph;
+      for (; c + 15 * P < nch; c += 16 * P)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[j] += col[(c + j * P) * ld];
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (c + j * P < nch) acc[j] += col[(c + j * P) * ld];
+#pragma unroll
+      for (int w = 8; w >= 1; w >>= 1)
+#pragma unroll
+        for (int j = 0; j < w; ++j) acc[j] += acc[j + w];
+      scratch[ph * n + v] = acc[0];
+    }
+    __syncthreads();
+    if (tid < n) {
+      float r = 0.f;
+      for (int h = 0; h < P; ++h) r += scratch[h * n + tid];
+      red[base + tid] = r;
+    }
+    __syncthreads();
+  }
+}
+
+// One workgroup = 64 consecutive columns of one segment x all its chunks (where a segment's rows
+// are float4-aligned, 16 lanes x float4 cover the 64 columns and 16 chunk phases keep 16 x 8 wide
+// loads in flight per column group; otherwise 64 lanes x 4 phases of scalar loads), or (last
+// block, q0slab set) the log_prior gradient.  Phases combine in a fixed order.
+__global__ __launch_bounds__(256) void grad_tail_kernel(TailArgs ta) {
   __shared__ float part[16][64];
+  __shared__ float red[256];
+  __shared__ float scratch[256];
+  const int64_t nblk = ta.blk_start[ta.nseg];
+  if ((int64_t)blockIdx.x >= nblk) {  // ---- log_prior gradient (VQ_VAE_HMM_fixed.py:71,:123,:131)
+    const LogPriorGradArgs& lp = ta.lp;
+    const int K = lp.K;
+    block_reduce_cols(ta.q0slab, ta.q0chunks, K, 0, K, red, scratch);
+    if (threadIdx.x == 0) {
+      const float c = -lp.beta / loss_norm_batch(lp.norm, lp.B);
+      const float sc = lp.scale ? *lp.scale : 1.f;
+      float m = -__builtin_inff();
+      for (int k = 0; k < K; ++k) m = fmaxf(m, lp.log_prior[k]);
+      float se = 0.f;
+      for (int k = 0; k < K; ++k) se += __expf(lp.log_prior[k] - m);
+      float tot = 0.f;
+      for (int k = 0; k < K; ++k) tot += c * red[k];
+      for (int k = 0; k < K; ++k) lp.out[k] = sc * (c * red[k] - __expf(lp.log_prior[k] - m) / se * tot);
+    }
+    return;
+  }
   int si = 0;
-  while (si + 1 < segs.nseg && (int64_t)blockIdx.x >= segs.blk_start[si + 1]) ++si;
-  const SlabSeg& sg = segs.s[si];
-  const int64_t col0 = ((int64_t)blockIdx.x - segs.blk_start[si]) * 64;
+  while (si + 1 < ta.nseg && (int64_t)blockIdx.x >= ta.blk_start[si + 1]) ++si;
+  const SlabSeg& sg = ta.s[si];
+  const int64_t col0 = ((int64_t)blockIdx.x - ta.blk_start[si]) * 64;
   const bool vec = (sg.len % 4 == 0) && ((reinterpret_cast<uintptr_t>(sg.slab) & 15) == 0);
   int nph;
   if (vec) {
     nph = 16;
     const int ph = threadIdx.x >> 4, cg = (threadIdx.x & 15) * 4;
-    const int64_t col = col0 + cg;
+    const int64_t c4 = col0 + cg;
     float4 p8[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) p8[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (col < sg.len) {  // len % 4 == 0: the whole float4 is in range
-      const float4* sl = reinterpret_cast<const float4*>(sg.slab + col);
+    if (c4 < sg.len) {  // len % 4 == 0: the whole float4 is in range
+      const float4* sl = reinterpret_cast<const float4*>(sg.slab + c4);
       const int64_t ld = sg.len / 4;
       int64_t c = ph;
       for (; c + 112 < sg.nchunks; c += 128) {
@@ -69,18 +160,18 @@ __global__ __launch_bounds__(256) void reduce_slabs_kernel(SlabSegs segs) {
     for (int e = 0; e < 4; ++e) part[ph][cg + e] = acc[e];
   } else {
     nph = 4;
-    const int64_t col = col0 + (threadIdx.x & 63);
+    const int64_t cs = col0 + (threadIdx.x & 63);
     const int ph = threadIdx.x >> 6;
     float p8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (col < sg.len) {
+    if (cs < sg.len) {
       int64_t c = ph;
       for (; c + 28 < sg.nchunks; c += 32) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) p8[k] += sg.slab[(c + 4 * k) * sg.len + col];
+        for (int k = 0; k < 8; ++k) p8[k] += sg.slab[(c + 4 * k) * sg.len + cs];
       }
 #pragma unroll
       for (int k = 0; k < 8; ++k)  // < 8 rows left per phase
-        if (c + 4 * k < sg.nchunks) p8[k] += sg.slab[(c + 4 * k) * sg.len + col];
+        if (c + 4 * k < sg.nchunks) p8[k] += sg.slab[(c + 4 * k) * sg.len + cs];
     }
     part[ph][threadIdx.x & 63] = ((p8[0] + p8[1]) + (p8[2] + p8[3])) + ((p8[4] + p8[5]) + (p8[6] + p8[7]));
   }
@@ -95,17 +186,73 @@ __global__ __launch_bounds__(256) void reduce_slabs_kernel(SlabSegs segs) {
   }
 }
 
-int launch_reduce_slabs(const SlabSeg* segs, int n, hipStream_t s) {
-  if (n > MAX_SEGS) return VQHMM_EINVAL;
-  SlabSegs ss{};
-  ss.nseg = n;
-  ss.blk_start[0] = 0;
-  for (int i = 0; i < n; ++i) {
-    ss.s[i] = segs[i];
-    ss.blk_start[i + 1] = ss.blk_start[i] + cdiv(segs[i].len, 64);
+int launch_grad_tail(TailArgs& a, hipStream_t s) {
+  if (a.nseg > MAX_SEGS || (a.q0slab && a.lp.K > 256)) return VQHMM_EINVAL;
+  a.blk_start[0] = 0;
+  for (int i = 0; i < a.nseg; ++i) a.blk_start[i + 1] = a.blk_start[i] + cdiv(a.s[i].len, 64);
+  const int64_t nb = a.blk_start[a.nseg] + (a.q0slab ? 1 : 0);
+  if (nb == 0) return VQHMM_OK;
+  grad_tail_kernel<<<(unsigned)nb, 256, 0, s>>>(a);
+  VQHMM_LAUNCH_CHECK();
+  return VQHMM_OK;
+}
+
+// Blocks [0, nb): 256 consecutive elements each: gradient (decoder.conv1 weight from dWc and the
+// embedding copy; every other element as reduced) then Adam.  Blocks nb .. nb+K-1: one embedding
+// row k each, dE[k][h] with 4 thread groups splitting o (combined in a fixed order), then Adam.
+__global__ __launch_bounds__(256) void compose_adam_kernel(ComposeAdamArgs a) {
+  __shared__ float part[4][256];
+  const AdamArgs& ad = a.adam;
+  const int64_t tn = (*ad.step & 0xffffffffll) + 1;
+  const int H = a.H, K = a.K;
+  const int64_t nb = cdiv(a.n, 256);
+  if ((int64_t)blockIdx.x < nb) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const bool live = i < a.n && !(i >= a.off_e && i < a.off_e + (int64_t)K * H);
+    if (live) {
+      const AdamElem e = adam_load(ad, i, tn);
+      float gv;
+      if (i >= a.off_w && i < a.off_w + (int64_t)H * H * 3) {
+        const int64_t j = i - a.off_w;
+        const int o = (int)(j / (3 * H)), rem = (int)(j - (int64_t)o * 3 * H), h = rem / 3, tap = rem - 3 * h;
+        float sacc = 0.f;
+        for (int k = 0; k < K; ++k) sacc = fmaf(a.dWc[((int64_t)o * K + k) * 3 + tap], a.Ecopy[(int64_t)k * H + h], sacc);
+        gv = sacc;
+        a.g[i] = gv;
+      } else {
+        gv = a.g[i];
+      }
+      adam_apply(ad, i, gv, e);
+    }
+  } else {
+    const int k = (int)(blockIdx.x - nb);
+    const int grp = threadIdx.x >> 6;
+    for (int h0 = 0; h0 < H; h0 += 64) {
+      const int h = h0 + (threadIdx.x & 63);
+      float sacc = 0.f;
+      if (h < H)
+        for (int o = grp; o < H; o += 4)
+#pragma unroll
+          for (int tap = 0; tap < 3; ++tap)
+            sacc = fmaf(a.dWc[((int64_t)o * K + k) * 3 + tap], a.Wcopy[((int64_t)o * H + h) * 3 + tap], sacc);
+      part[grp][threadIdx.x & 63] = sacc;
+      __syncthreads();
+      if (threadIdx.x < 64 && h < H) {
+        const int64_t i = a.off_e + (int64_t)k * H + h;
+        const AdamElem e = adam_load(ad, i, tn);
+        const float gv = ((part[0][threadIdx.x] + part[1][threadIdx.x]) + part[2][threadIdx.x]) + part[3][threadIdx.x];
+        a.g[i] = gv;
+        adam_apply(ad, i, gv, e);
+      }
+      __syncthreads();
+    }
   }
-  if (ss.blk_start[n] == 0) return VQHMM_OK;
-  reduce_slabs_kernel<<<(unsigned)ss.blk_start[n], 256, 0, s>>>(ss);
+  adam_ticket(ad.step, tn);
+}
+
+int launch_compose_adam(const ComposeAdamArgs& a, hipStream_t s) {
+  const int64_t nb = cdiv(a.n, 256) + a.K;
+  compose_adam_kernel<<<(unsigned)nb, 256, 0, s>>>(a);
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
 }
@@ -132,19 +279,26 @@ int launch_finalize_loss(const double* part, int nblk, const int64_t* lengths, c
 // and the data gradient (N = K, Kc = H) — this block writes their entries of channel o; the
 // image jobs (wimg_slice, composed) write the zero padding around them.
 __device__ __forceinline__ void compose_fwd_block(const float* W, const float* E, int H, int K, float* Wc, int o,
-                                                  float* cs, float* img_f = nullptr, float* img_d = nullptr) {
+                                                  float* cs, float* img_f = nullptr, float* img_d = nullptr,
+                                                  float* Ecopy = nullptr, float* Wcopy = nullptr) {
   float* wo = cs;          // [H*3]
   float* es = cs + H * 3;  // [K*H]
-  for (int i = threadIdx.x; i < H * 3; i += 256) wo[i] = W[(int64_t)o * H * 3 + i];
-  for (int i = threadIdx.x; i < K * H; i += 256) es[i] = E[i];
+  for (int i = threadIdx.x; i < H * 3; i += 256) {
+    wo[i] = W[(int64_t)o * H * 3 + i];
+    if (Wcopy) Wcopy[(int64_t)o * H * 3 + i] = wo[i];
+  }
+  for (int i = threadIdx.x; i < K * H; i += 256) {
+    es[i] = E[i];
+    if (Ecopy && o == 0) Ecopy[i] = es[i];
+  }
   __syncthreads();
   for (int i = threadIdx.x; i < K * 3; i += 256) {
     const int k = i / 3, tap = i % 3;
     float s = 0.f;
     for (int h = 0; h < H; ++h) s = fmaf(wo[h * 3 + tap], es[k * H + h], s);
     Wc[(int64_t)o * K * 3 + i] = s;
-    if (img_f) img_f[((int64_t)tap * 16 * c2_nb(H) + o) * (16 * c2_kcp(K) + 4) + k] = s;
-    if (img_d) img_d[((int64_t)(2 - tap) * 16 * c2_nb(K) + k) * (16 * c2_kcp(H) + 4) + o] = s;
+    if (img_f) img_f[((int64_t)tap * 16 * c2_nb(H) + o) * c2_ldx(K) + k] = s;
+    if (img_d) img_d[((int64_t)(2 - tap) * 16 * c2_nb(K) + k) * c2_ldx(H) + o] = s;
   }
 }
 __global__ __launch_bounds__(256) void compose_fwd_kernel(const float* W, const float* E, int H, int K, float* Wc) {
@@ -270,26 +424,9 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
                                                    float gmul) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t tn = (*step & 0xffffffffll) + 1;
-  if (i < n) {
-    const double t = (double)tn;
-    const float step_size = (float)(lr / (1.0 - pow(b1, t)));
-    const float bc2s = (float)sqrt(1.0 - pow(b2, t));
-    const float gi = g[i] * gmul;
-    const float mi = m[i] + (float)(1.0 - b1) * (gi - m[i]);
-    const float vi = v[i] * (float)b2 + (float)(1.0 - b2) * gi * gi;
-    m[i] = mi;
-    v[i] = vi;
-    const float denom = sqrtf(vi) / bc2s + (float)eps;
-    p[i] = p[i] + (-step_size) * (mi / denom);
-  }
-  // No fence: the ticket orders only the reads of *step (all returned before the
-  // barrier), not this workgroup's parameter writes.
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    auto* st = reinterpret_cast<unsigned long long*>(step);
-    const unsigned long long old = atomicAdd(st, 1ull << 32);
-    if ((old >> 32) == gridDim.x - 1) atomicExch(st, (unsigned long long)tn);
-  }
+  const AdamArgs a{p, m, v, step, lr, b1, b2, eps, gmul};
+  if (i < n) adam_apply(a, i, g[i], adam_load(a, i, tn));
+  adam_ticket(step, tn);
 }
 
 // ------------------------------------------------------------ gradient clipping
@@ -380,7 +517,7 @@ __global__ __launch_bounds__(256) void to_pcl_kernel(const float* __restrict__ s
 }
 // One 256-entry slice of a packed conv weight image (WImgJob, kernels.h).
 __device__ __forceinline__ void wimg_slice(const WImgJob& j, int64_t i0) {
-  const int NW = 16 * c2_nb(j.N), LDX = 16 * c2_kcp(j.Kc) + 4;
+  const int NW = 16 * c2_nb(j.N), LDX = c2_ldx(j.Kc);
   const int64_t n_img = (int64_t)j.ks * NW * LDX;
   const int64_t i = i0 + threadIdx.x;
   if (i >= n_img) return;
@@ -412,7 +549,7 @@ __global__ __launch_bounds__(256) void prologue_kernel(PrologueArgs a) {
   } else if (bx < a.nbx + a.nbu) {
     to_pcl_slot(a.u, a.U, a.B, a.T, a.usc, a.ust, a.up, (int64_t)(bx - a.nbx) * 256 + threadIdx.x);
   } else if (bx < a.nbx + a.nbu + (unsigned)a.H) {
-    compose_fwd_block(a.W, a.E, a.H, a.K, a.Wc, (int)(bx - a.nbx - a.nbu), cs, a.wc_img_f, a.wc_img_d);
+    compose_fwd_block(a.W, a.E, a.H, a.K, a.Wc, (int)(bx - a.nbx - a.nbu), cs, a.wc_img_f, a.wc_img_d, a.Ecopy, a.Wcopy);
   } else {
     const unsigned ib = bx - a.nbx - a.nbu - (unsigned)a.H;
     int j = 0;

@@ -14,7 +14,8 @@ TrainState owns, per model:
 
 One step = elbo forward (+loss accumulate) -> elbo backward -> [RCCL
 all-reduce of the flat gradient when torch.distributed is initialised] ->
-fused Adam.  Everything in the step is HIP kernels from libvqhmm.so plus the
+fused Adam.  In a single process without clipping, Adam rides in the
+backward's last launch (vqhmm_elbo_bwd_adam_f32).  Everything in the step is HIP kernels from libvqhmm.so plus the
 collective; nothing syncs the host, so a fixed-shape step can be captured in a
 HIP graph (`capture()`).  Optionally (overlap_bwd / VQHMM_BWD_OVERLAP=1) the
 backward's weight gradients run on a side stream beside the data-gradient
@@ -160,6 +161,41 @@ class TrainState:
         for stage in (S_REDUCE, S_COMPOSE_BWD, S_LOGPRIOR):
             run(stage, main)
 
+    def forward_backward_adam(self, x, u, lengths, beta, norm=None):
+        """forward_backward + apply_adam with Adam fused into the backward's last launch
+        (vqhmm_elbo_bwd_adam_f32): single process, no clipping."""
+        B, _, T = x.shape
+        lay = self.model.prior.u_layout(u)
+        ws = self.workspace(B, T)
+        st = _ext.stream_ptr(self.device)
+        d = ctypes.byref(self.dims)
+        _ext.check(self.lib.vqhmm_elbo_fwd_f32(d, self.ptrs, _ext.ptr(x), _ext.ptr(u), lay, _ext.ptr(lengths),
+                                               _ext.ptr(norm), B, T, float(beta), 1, _ext.ptr(ws), ws.numel(),
+                                               _ext.ptr(self.loss), _ext.ptr(self.epoch_acc), st), "elbo forward")
+        b1, b2 = self.betas
+        rc = self.lib.vqhmm_elbo_bwd_adam_f32(d, self.ptrs, _ext.ptr(x), _ext.ptr(norm), B, T, float(beta),
+                                              _ext.ptr(ws), ws.numel(), _ext.ptr(self.grad), _ext.ptr(self.flat),
+                                              _ext.ptr(self.exp_avg), _ext.ptr(self.exp_avg_sq), self.lr, b1, b2,
+                                              self.eps, _ext.ptr(self.step_dev), self.grad_scale(norm is not None),
+                                              st)
+        _ext.check(rc, "elbo backward + adam")
+
+    def _fused_adam_ok(self, max_norm=None):
+        return not (self.distributed and self.world > 1) and max_norm is None and not self.overlap_bwd
+
+    def _step_device(self, x, u, lengths, beta, norm=None, max_norm=None):
+        """One step on device tensors (no host sync)."""
+        if self._fused_adam_ok(max_norm):
+            self.forward_backward_adam(x, u, lengths, beta, norm)
+            return
+        self.forward_backward(x, u, lengths, beta, norm)
+        self.reduce_gradients()
+        if max_norm is None:
+            self.apply_adam(global_norm=norm is not None)
+        else:
+            self.clip_grad_norm(max_norm, global_norm=norm is not None)
+            self.apply_adam(scale=1.0)
+
     def reduce_gradients(self):
         if self.distributed and self.world > 1:
             torch.distributed.all_reduce(self.grad, op=torch.distributed.ReduceOp.SUM, group=self.pg)
@@ -198,13 +234,7 @@ class TrainState:
         norm (device int64 {valid_count, batch} of the global batch, or None): see
         forward_backward.  With it, the ranks' summed gradient IS the global batch's."""
         x, u, lengths = self.prepare(x, u, lengths)
-        self.forward_backward(x, u, lengths, beta, norm)
-        self.reduce_gradients()
-        if max_norm is None:
-            self.apply_adam(global_norm=norm is not None)
-        else:
-            self.clip_grad_norm(max_norm, global_norm=norm is not None)
-            self.apply_adam(scale=1.0)
+        self._step_device(x, u, lengths, beta, norm, max_norm)
         return self.loss
 
     def publish_grads(self):
@@ -225,15 +255,12 @@ class TrainState:
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
             for _ in range(warmup):  # warm-up steps are real steps (identical to eager ones)
-                self.forward_backward(x, u, lengths, beta, norm)
-                self.reduce_gradients()
-                self.apply_adam(norm is not None)
+                self._step_device(x, u, lengths, beta, norm)
         torch.cuda.current_stream(self.device).wait_stream(s)
         if not split:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                self.forward_backward(x, u, lengths, beta, norm)
-                self.apply_adam(norm is not None)
+                self._step_device(x, u, lengths, beta, norm)
             return g.replay
         g_fb, g_adam = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         with torch.cuda.graph(g_fb):
