@@ -56,6 +56,73 @@ __device__ __forceinline__ float4 x_mask(const ConvArgs& a, int64_t m0, int s, i
 
 }  // namespace
 
+// The tile's MFMAs: acc[nb][pb] (16 n x 16 rows) += W_tap (n x c) @ X(rows + tap - 1, c)^T over the
+// KS * KCP 16-wide k-steps.  Operands of step s + 1 are read from LDS while the 16*PB MFMAs of step
+// s run (two register sets; sched_barrier keeps the reads ahead of the MFMAs), and the MFMAs are
+// issued component-major so consecutive ones use different accumulators (the accumulator chain
+// of every block is still x, y, z, w per step: the same k-ordered fma chain as before).
+// Xw = row 0 of the wave's first 16-row block in the X tile (tile row 0 = PCL row m0 - 1).
+template <int NB, int PB, int KCP, int KS, int LDX, int NW>
+__device__ __forceinline__ void c2_mfma_tile(const float* Ws, const float* Xw, int lg4, int l16,
+                                             f32x4 (&acc)[NB][PB], bool pipe) {
+  constexpr int NSTEP = KS * KCP;
+  if (!pipe) {  // A/B reference: operands read per step, accumulator-major issue
+#pragma unroll
+    for (int st = 0; st < NSTEP; ++st) {
+      const int tap = st / KCP, kk = st - tap * KCP;
+      const int rowoff = (KS == 3) ? tap : 1;
+      const int col = kk * 16 + 4 * lg4;
+      float4 a[NB], b[PB];
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb)
+        a[nb] = *reinterpret_cast<const float4*>(Ws + (tap * NW + nb * 16 + l16) * LDX + col);
+#pragma unroll
+      for (int pb = 0; pb < PB; ++pb)
+        b[pb] = *reinterpret_cast<const float4*>(Xw + (pb * 16 + l16 + rowoff) * LDX + col);
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+        for (int pb = 0; pb < PB; ++pb) {
+          acc[nb][pb] = mfma16x16x4(a[nb].x, b[pb].x, acc[nb][pb]);
+          acc[nb][pb] = mfma16x16x4(a[nb].y, b[pb].y, acc[nb][pb]);
+          acc[nb][pb] = mfma16x16x4(a[nb].z, b[pb].z, acc[nb][pb]);
+          acc[nb][pb] = mfma16x16x4(a[nb].w, b[pb].w, acc[nb][pb]);
+        }
+    }
+    return;
+  }
+  float4 av[2][NB], bv[2][PB];
+  auto load = [&](int st, float4 (&a)[NB], float4 (&b)[PB]) {
+    const int tap = st / KCP, kk = st - tap * KCP;
+    const int rowoff = (KS == 3) ? tap : 1;
+    const int col = kk * 16 + 4 * lg4;
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+      a[nb] = *reinterpret_cast<const float4*>(Ws + (tap * NW + nb * 16 + l16) * LDX + col);
+#pragma unroll
+    for (int pb = 0; pb < PB; ++pb)
+      b[pb] = *reinterpret_cast<const float4*>(Xw + (pb * 16 + l16 + rowoff) * LDX + col);
+  };
+  load(0, av[0], bv[0]);
+#pragma unroll
+  for (int st = 0; st < NSTEP; ++st) {
+    const int cb = st & 1;
+    if (st + 1 < NSTEP) load(st + 1, av[cb ^ 1], bv[cb ^ 1]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+        for (int pb = 0; pb < PB; ++pb) {
+          const float x = e == 0 ? av[cb][nb].x : e == 1 ? av[cb][nb].y : e == 2 ? av[cb][nb].z : av[cb][nb].w;
+          const float y = e == 0 ? bv[cb][pb].x : e == 1 ? bv[cb][pb].y : e == 2 ? bv[cb][pb].z : bv[cb][pb].w;
+          acc[nb][pb] = mfma16x16x4(x, y, acc[nb][pb]);
+        }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 // Epilogue of one tile (ACT: 0 none, 1 ReLU, 2 ReLU-backward mask by aux, 3 none + the softmax
 // backward of the row, see ConvArgs::lb_*).
 template <int NB, int PB, int ACT>
@@ -303,33 +370,174 @@ __global__ __launch_bounds__(256, (C2Occ<NB, KCP, TAIL>::W)) void conv2_kernel(C
     for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
       for (int pb = 0; pb < PB; ++pb) acc[nb][pb] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int tap = 0; tap < KS; ++tap) {
-      const int rowoff = (KS == 3) ? tap : 1;
-#pragma unroll
-      for (int kk = 0; kk < KCP; ++kk) {
-        const int col = kk * 16 + 4 * lg4;
-        float4 av[NB], bv[PB];
-#pragma unroll
-        for (int nb = 0; nb < NB; ++nb)
-          av[nb] = *reinterpret_cast<const float4*>(Ws + (tap * C::NW + nb * 16 + l16) * C::LDX + col);
-#pragma unroll
-        for (int pb = 0; pb < PB; ++pb)
-          bv[pb] = *reinterpret_cast<const float4*>(Xs + ((wave * PB + pb) * 16 + l16 + rowoff) * C::LDX + col);
-#pragma unroll
-        for (int nb = 0; nb < NB; ++nb)
-#pragma unroll
-          for (int pb = 0; pb < PB; ++pb) {
-            acc[nb][pb] = mfma16x16x4(av[nb].x, bv[pb].x, acc[nb][pb]);
-            acc[nb][pb] = mfma16x16x4(av[nb].y, bv[pb].y, acc[nb][pb]);
-            acc[nb][pb] = mfma16x16x4(av[nb].z, bv[pb].z, acc[nb][pb]);
-            acc[nb][pb] = mfma16x16x4(av[nb].w, bv[pb].w, acc[nb][pb]);
-          }
-      }
-    }
+    c2_mfma_tile<NB, PB, KCP, KS, C::LDX, C::NW>(Ws, Xs + (wave * PB) * 16 * C::LDX, lg4, l16, acc, a.pipe);
     conv2_epilogue<NB, PB, ACT>(a, m0, wave, lg4, l16, acc, auxv, bias_r, tw, tb0, sc, tail);
     tile = next;
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Wave-independent variant: the workgroup (up to 16 waves, one per CU) stages the weight image in
+// LDS once; after that single barrier every wave works alone on 16-row tiles dealt round-robin
+// over the grid, with its own 18-row X slot in LDS (written and read by that wave only, so no
+// further workgroup barrier) and its own register prefetch of the next tile.  Up to 4 waves per
+// SIMD keep the MFMA pipe fed while the others run their epilogues, stores and loads.
+template <int NB, int KCP, int KS>
+struct C2wCfg {
+  static constexpr int KCW = KCP * 16;
+  static constexpr int LDX = KCW + 8;          // = c2_ldx: conflict-free b128 operand reads
+  static constexpr int NW = NB * 16;
+  static constexpr int XROWS = 18;             // 16 rows + the k = 3 halo
+  static constexpr int XF4 = XROWS * KCW / 4;  // float4 slots of one X slot
+  static constexpr int PF = (XF4 + 63) / 64;   // float4 slots per lane
+  static constexpr size_t W_FLOATS = (size_t)KS * NW * LDX;
+  static constexpr size_t X_FLOATS = (size_t)XROWS * LDX;
+  static constexpr size_t E_FLOATS = (size_t)NW + 16 * NW + 16;  // bias, tail weight (16 x NW), tail bias
+  static constexpr size_t lds(int wpg) { return (W_FLOATS + E_FLOATS + (size_t)wpg * X_FLOATS) * 4; }
+};
+
+// waves per workgroup the register budget is sized for: 4 per SIMD (128 VGPRs) where that fits
+// without spills, 3 (170) for the wide layers
+template <int NB, int KCP>
+struct C2wOcc {
+  static constexpr int MAXW = NB * KCP >= 8 ? 12 : 16;
+};
+
+template <int NB, int KCP, int KS, int ACT, bool TAIL>
+__global__ __launch_bounds__((64 * C2wOcc<NB, KCP>::MAXW)) void conv2w_kernel(ConvArgs a, int64_t ntiles) {
+  using C = C2wCfg<NB, KCP, KS>;
+  extern __shared__ float4 smem4[];
+  float* Ws = reinterpret_cast<float*>(smem4);  // [KS][NW][LDX]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nwv = blockDim.x >> 6;
+  float* Es = Ws + C::W_FLOATS;                       // bias [NW], tail weight [16][NW], tail bias [16]
+  float* Xs = Es + C::E_FLOATS + wave * C::X_FLOATS;  // this wave's [XROWS][LDX]
+  const int lg4 = lane >> 4, l16 = lane & 15;
+
+  if (a.Wimg) {
+    const float4* src = reinterpret_cast<const float4*>(a.Wimg);
+    for (int i = tid; i < (int)(C::W_FLOATS / 4); i += blockDim.x) smem4[i] = src[i];
+  } else {
+    for (int i = tid; i < KS * C::NW * C::KCW; i += blockDim.x) {
+      const int c = i % C::KCW, n = (i / C::KCW) % C::NW, tap = i / (C::KCW * C::NW);
+      float v = 0.f;
+      if (n < a.N && c < a.Kc)
+        v = a.w_dgrad ? a.W[((int64_t)c * a.N + n) * KS + (KS - 1 - tap)] : a.W[((int64_t)n * a.Kc + c) * KS + tap];
+      Ws[(tap * C::NW + n) * C::LDX + c] = v;
+    }
+  }
+  // epilogue constants in LDS (read back per tile: registers go to the MFMA loop's prefetch)
+  for (int i = tid; i < (int)C::E_FLOATS; i += blockDim.x) {
+    float v = 0.f;
+    if (i < C::NW) {
+      v = (a.bias && i < a.N) ? a.bias[i] : 0.f;
+    } else if (i < 17 * C::NW) {
+      const int j = i - C::NW, c2 = j / C::NW, n = j - c2 * C::NW;
+      v = (TAIL && c2 < a.C2 && n < a.N) ? a.tW[(int64_t)c2 * a.N + n] : 0.f;
+    } else {
+      const int c2 = i - 17 * C::NW;
+      v = (TAIL && a.tb && c2 < a.C2) ? a.tb[c2] : 0.f;
+    }
+    Es[i] = v;
+  }
+  const float sc = a.scale ? *a.scale : 1.0f;
+
+  const int64_t stride = (int64_t)gridDim.x * nwv;
+  int64_t tile = (int64_t)blockIdx.x * nwv + wave;
+  float4 pf[C::PF];
+#pragma unroll
+  for (int k = 0; k < C::PF; ++k) {
+    const int s = lane + k * 64;
+    pf[k] = x_raw(a, tile * 16, s < C::XF4 ? s : 0, C::KCW);
+  }
+  __syncthreads();  // the weights; from here on the waves never wait for each other
+  while (tile < ntiles) {
+    const int64_t m0 = tile * 16;
+#pragma unroll
+    for (int k = 0; k < C::PF; ++k) {
+      const int s = lane + k * 64;
+      if (s < C::XF4) {
+        const int row = s / (C::KCW / 4), c = (s - row * (C::KCW / 4)) * 4;
+        *reinterpret_cast<float4*>(Xs + row * C::LDX + c) = x_mask(a, m0, s, C::KCW, pf[k]);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // LDS ops of a wave run in order; keep the compiler from hoisting reads
+    float4 auxv[NB][1] = {};
+    if constexpr (ACT == 2) {
+      const int64_t r = m0 + l16;
+      const int ldn = ld4(a.N);
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb)
+        auxv[nb][0] = *reinterpret_cast<const float4*>(a.aux + (r < a.R ? r : a.R - 1) * ldn + min(nb * 16 + 4 * lg4, ldn - 4));
+    }
+    const int64_t next = tile + stride;
+    if (next < ntiles) {
+#pragma unroll
+      for (int k = 0; k < C::PF; ++k) {
+        const int s = lane + k * 64;
+        pf[k] = x_raw(a, next * 16, s < C::XF4 ? s : 0, C::KCW);
+      }
+    }
+    f32x4 acc[NB][1];
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) acc[nb][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+    c2_mfma_tile<NB, 1, KCP, KS, C::LDX, C::NW>(Ws, Xs, lg4, l16, acc, a.pipe);
+    __builtin_amdgcn_wave_barrier();  // the slot's reads are done before the next tile overwrites it
+    float bias_r[NB][4], tw[NB][4];
+    f32x4 tb0 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      const float4 b4 = *reinterpret_cast<const float4*>(Es + nb * 16 + 4 * lg4);
+      bias_r[nb][0] = b4.x; bias_r[nb][1] = b4.y; bias_r[nb][2] = b4.z; bias_r[nb][3] = b4.w;
+      if constexpr (TAIL) {
+        const float4 t4 = *reinterpret_cast<const float4*>(Es + C::NW + l16 * C::NW + nb * 16 + 4 * lg4);
+        tw[nb][0] = t4.x; tw[nb][1] = t4.y; tw[nb][2] = t4.z; tw[nb][3] = t4.w;
+      }
+    }
+    if constexpr (TAIL) {
+      const float4 t4 = *reinterpret_cast<const float4*>(Es + 17 * C::NW + 4 * lg4);
+      tb0 = f32x4{t4.x, t4.y, t4.z, t4.w};
+    }
+    conv2_epilogue<NB, 1, ACT>(a, m0, 0, lg4, l16, acc, auxv, bias_r, tw, tb0, sc, TAIL);
+    tile = next;
+  }
+}
+
+// Kernel choice: VQHMM_CONV=wg | wave forces one (A/B), else the wave kernel below
+// VQHMM_CONV_WAVE_ROWS rows (default: always; it measured equal or faster at B = 128 .. 1024)
+// and the workgroup-tile kernel above; VQHMM_CONV_PIPE=0
+// turns the operand pipelining off (A/B).  Read once.
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+static bool conv2_wave_mode(int64_t R) {
+  static const int force = [] {
+    const char* e = getenv("VQHMM_CONV");
+    return !e ? 0 : (e[0] == 'w' && e[1] == 'g') ? 1 : (e[0] == 'w' && e[1] == 'a') ? 2 : 0;
+  }();
+  static const int64_t rows = env_int("VQHMM_CONV_WAVE_ROWS", 1 << 30);
+  return force == 2 || (force == 0 && R < rows);
+}
+static bool conv2_pipe() {
+  static const bool v = env_int("VQHMM_CONV_PIPE", 1) != 0;
+  return v;
+}
+
+template <int NB, int KCP, int KS, int ACT, bool TAIL>
+static int launch_c2w(const ConvArgs& a, hipStream_t s) {
+  using C = C2wCfg<NB, KCP, KS>;
+  const int64_t ntiles = cdiv(a.R, 16);
+  int wmax = C2wOcc<NB, KCP>::MAXW;
+  while (wmax > 1 && C::lds(wmax) > 160 * 1024) --wmax;
+  if (C::lds(wmax) > 160 * 1024) return VQHMM_EUNSUPPORTED;
+  // one workgroup per CU: as many waves as it takes to give every CU work, up to wmax
+  const int64_t want = cdiv(ntiles, 256);
+  const int wpg = (int)(want < wmax ? (want > 0 ? want : 1) : wmax);
+  const int64_t grid = cdiv(ntiles, wpg) < 256 ? cdiv(ntiles, wpg) : 256;
+  conv2w_kernel<NB, KCP, KS, ACT, TAIL><<<(unsigned)grid, 64 * wpg, C::lds(wpg), s>>>(a, ntiles);
+  VQHMM_LAUNCH_CHECK();
+  return VQHMM_OK;
 }
 
 bool conv2_supported(const ConvArgs& a) {
@@ -338,13 +546,16 @@ bool conv2_supported(const ConvArgs& a) {
 
 template <int NB, int KCP, int KS, int PB, int ACT, bool TAIL>
 static int launch_c2v(const ConvArgs& a, hipStream_t s) {
+  ConvArgs ap = a;
+  ap.pipe = conv2_pipe();
+  if (conv2_wave_mode(a.R)) return launch_c2w<NB, KCP, KS, ACT, TAIL>(ap, s);
   using C = C2Cfg<NB, KCP, KS, PB>;
   const int64_t ntiles = cdiv(a.R, C::BM);
   int per_cu = (int)((160 * 1024) / C::LDS);
   if (per_cu < 1) return VQHMM_EUNSUPPORTED;
   if (per_cu > 4) per_cu = 4;
   const int64_t grid = ntiles < 256LL * per_cu ? ntiles : 256LL * per_cu;
-  conv2_kernel<NB, KCP, KS, PB, ACT, TAIL><<<(unsigned)grid, 256, C::LDS, s>>>(a, ntiles);
+  conv2_kernel<NB, KCP, KS, PB, ACT, TAIL><<<(unsigned)grid, 256, C::LDS, s>>>(ap, ntiles);
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
 }

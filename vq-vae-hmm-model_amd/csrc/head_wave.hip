@@ -142,6 +142,9 @@ __global__ __launch_bounds__(256, 2) void elbo_head_wave_kernel(HeadArgs a) {
   for (int ij = 0; ij < KK; ++ij) db2v[ij] = 0.f;
 
   // ---- phase A on the window's NBW row blocks at once: lg^T -> lgS (NBW independent chains).
+  // Software-pipelined over the hidden blocks: hb + 1's weight operands are read from LDS and its
+  // hidden MFMAs issued behind hb's 16 output MFMAs (sched_barrier pins that order, so the
+  // compiler cannot hoist every block's loads up front and spill); lg's chain order is unchanged.
   auto phase_a = [&]() {
     float ub0[NBW];
     f32x4 lg[NBW];
@@ -150,27 +153,39 @@ __global__ __launch_bounds__(256, 2) void elbo_head_wave_kernel(HeadArgs a) {
       ub0[i] = W.uS[(i * 16 + l16) * 8 + lg4];
       lg[i] = b2f;
     }
-    auto hid = [&](int hb, f32x4 (&h)[NBW]) {  // u' = [u, 1]: the bias column is the accumulator's start
-      const float w1a = sh.W1S[(hb * 16 + l16) * 8 + lg4];
-      f32x4 b;
-#pragma unroll
-      for (int v = 0; v < 4; ++v) b[v] = sh.W1S[(hb * 16 + 4 * lg4 + v) * 8 + U];
-#pragma unroll
-      for (int i = 0; i < NBW; ++i) h[i] = mfma16x16x4(w1a, ub0[i], b);
+    struct AW {
+      float w1a;
+      f32x4 b, w2v;
     };
+    auto ldw = [&](int hb, AW& w) {  // u' = [u, 1]: the bias column is the accumulator's start
+      w.w1a = sh.W1S[(hb * 16 + l16) * 8 + lg4];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) w.b[v] = sh.W1S[(hb * 16 + 4 * lg4 + v) * 8 + U];
+      w.w2v = *reinterpret_cast<const f32x4*>(&sh.W2S[l16 * S::LDW2 + hb * 16 + 4 * lg4]);
+    };
+    auto hid = [&](const AW& w, f32x4 (&h)[NBW]) {
+#pragma unroll
+      for (int i = 0; i < NBW; ++i) h[i] = mfma16x16x4(w.w1a, ub0[i], w.b);
+    };
+    AW wv[2];
+    f32x4 hc[2][NBW];
+    ldw(0, wv[0]);
+    hid(wv[0], hc[0]);
 #pragma unroll
     for (int hb = 0; hb < HB; ++hb) {
-      f32x4 hc[NBW];
-      hid(hb, hc);
-      const f32x4 w2v = *reinterpret_cast<const f32x4*>(&sh.W2S[l16 * S::LDW2 + hb * 16 + 4 * lg4]);
+      const int cb = hb & 1;
+      if (hb + 1 < HB) ldw(hb + 1, wv[cb ^ 1]);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < NBW; ++i)
 #pragma unroll
-        for (int v = 0; v < 4; ++v) hc[i][v] = fmaxf(hc[i][v], 0.f);
+        for (int v = 0; v < 4; ++v) hc[cb][i][v] = fmaxf(hc[cb][i][v], 0.f);
 #pragma unroll
       for (int v = 0; v < 4; ++v)
 #pragma unroll
-        for (int i = 0; i < NBW; ++i) lg[i] = mfma16x16x4(w2v[v], hc[i][v], lg[i]);
+        for (int i = 0; i < NBW; ++i) lg[i] = mfma16x16x4(wv[cb].w2v[v], hc[cb][i][v], lg[i]);
+      if (hb + 1 < HB) hid(wv[cb ^ 1], hc[cb ^ 1]);
+      __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int i = 0; i < NBW; ++i) *reinterpret_cast<f32x4*>(&W.lgS[(i * 16 + l16) * LGS + 4 * lg4]) = lg[i];
@@ -181,6 +196,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_wave_kernel(HeadArgs a) {
   // layout, lane (lg4, l16) holding rows 4*lg4 + v of hidden unit hb*16 + l16; the
   // contractions over rows then map row 4*lg4 + s to MFMA step s, so register v = s of those
   // fragments IS the operand (no transposes).  db2 is summed in phase B instead.
+  // Pipelined like phase A: hb + 1's hid / dhid MFMAs are issued behind hb's 8*NBW gradient MFMAs.
   auto phase_c = [&]() {
     constexpr int SD = (KK + 3) / 4;  // 4-wide contraction steps over ij that hold nonzero dlg
     float ua[NBW], dla[NBW][SD], dlt[NBW][4], ub[NBW][4];
@@ -196,30 +212,42 @@ __global__ __launch_bounds__(256, 2) void elbo_head_wave_kernel(HeadArgs a) {
         ub[i][s] = l16 < 8 ? uv : 0.f;                                                               // u'[row 4lg4+s][c' l16]
       }
     }
+    struct CW {
+      float w1, bb, w2b[SD];
+    };
+    auto ldw = [&](int hb, CW& w) {
+      w.w1 = sh.W1S[(hb * 16 + l16) * 8 + lg4];                                                     // W1'[h][c lg4]
+      w.bb = sh.W1S[(hb * 16 + l16) * 8 + U];                                                       // b1[h]
 #pragma unroll
-    for (int hb = 0; hb < HB; ++hb) {
-      float w2b[SD];
-      const float w1 = sh.W1S[(hb * 16 + l16) * 8 + lg4];                                           // W1'[h][c lg4]
-      const float bb = sh.W1S[(hb * 16 + l16) * 8 + U];                                             // b1[h]
-#pragma unroll
-      for (int s = 0; s < SD; ++s) w2b[s] = sh.W2S[(4 * s + lg4) * S::LDW2 + hb * 16 + l16];      // W2[ij 4s+lg4][h]
-      f32x4 h[NBW], dh[NBW];
+      for (int s = 0; s < SD; ++s) w.w2b[s] = sh.W2S[(4 * s + lg4) * S::LDW2 + hb * 16 + l16];    // W2[ij 4s+lg4][h]
+    };
+    auto fwd = [&](const CW& w, f32x4 (&h)[NBW], f32x4 (&dh)[NBW]) {
 #pragma unroll
       for (int i = 0; i < NBW; ++i) {  // bias as the accumulator's start (u' = [u, 1], U <= 4)
-        h[i] = mfma16x16x4(ua[i], w1, f32x4{bb, bb, bb, bb});
-        dh[i] = mfma16x16x4(dla[i][0], w2b[0], f32x4{0.f, 0.f, 0.f, 0.f});
+        h[i] = mfma16x16x4(ua[i], w.w1, f32x4{w.bb, w.bb, w.bb, w.bb});
+        dh[i] = mfma16x16x4(dla[i][0], w.w2b[0], f32x4{0.f, 0.f, 0.f, 0.f});
       }
 #pragma unroll
       for (int s = 1; s < SD; ++s)  // ij >= K*K are zero: the steps past them are skipped
 #pragma unroll
-        for (int i = 0; i < NBW; ++i) dh[i] = mfma16x16x4(dla[i][s], w2b[s], dh[i]);
+        for (int i = 0; i < NBW; ++i) dh[i] = mfma16x16x4(dla[i][s], w.w2b[s], dh[i]);
+    };
+    CW wv[2];
+    f32x4 h[2][NBW], dh[2][NBW];
+    ldw(0, wv[0]);
+    fwd(wv[0], h[0], dh[0]);
+#pragma unroll
+    for (int hb = 0; hb < HB; ++hb) {
+      const int cb = hb & 1;
+      if (hb + 1 < HB) ldw(hb + 1, wv[cb ^ 1]);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < NBW; ++i) {
         f32x4 hr, dm;
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-          hr[v] = fmaxf(h[i][v], 0.f);
-          dm[v] = h[i][v] > 0.f ? dh[i][v] : 0.f;
+          hr[v] = fmaxf(h[cb][i][v], 0.f);
+          dm[v] = h[cb][i][v] > 0.f ? dh[cb][i][v] : 0.f;
         }
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
@@ -227,6 +255,8 @@ __global__ __launch_bounds__(256, 2) void elbo_head_wave_kernel(HeadArgs a) {
           gW1[hb] = mfma16x16x4(dm[s], ub[i][s], gW1[hb]);    // (h x c') += dhid^T . u'
         }
       }
+      if (hb + 1 < HB) fwd(wv[cb ^ 1], h[cb ^ 1], dh[cb ^ 1]);
+      __builtin_amdgcn_sched_barrier(0);
     }
   };
 
@@ -461,7 +491,8 @@ __global__ __launch_bounds__(256, 2) void elbo_head_wave_kernel(HeadArgs a) {
   if (lane < K) a.slab_q0[blockIdx.x * K + lane] = ((qw[lane] + qw[4 + lane]) + qw[8 + lane]) + qw[12 + lane];
   if (lane < KK)
     a.slab_b2[(int64_t)blockIdx.x * KK + lane] = ((bw[lane] + bw[16 + lane]) + bw[32 + lane]) + bw[48 + lane];
-  for (int ww = 0; ww < 3; ++ww) {
+#pragma unroll 1
+  for (int ww = 0; ww < 3; ++ww) {  // one wave's 8*HB partials at a time (registers)
     const float* xb = xbuf + ww * NV * 64;
 #pragma unroll
     for (int hb = 0; hb < HB; ++hb) {
@@ -499,7 +530,7 @@ static int head_wave_nbw(int64_t R) {
     const char* e = getenv("VQHMM_HEAD_NBW");
     return e ? atoi(e) : 0;
   }();
-  if (force == 1 || force == 4) return force;
+  if (force == 1 || force == 2 || force == 4) return force;
   return cdiv(R, 63) >= 512 ? 4 : 1;
 }
 
@@ -524,6 +555,10 @@ int launch_head_wave(const HeadArgs& a, int grid, hipStream_t s) {
       const size_t lds = head_wave_lds<4>(HBV);                                                        \
       if (a.D <= 8) elbo_head_wave_kernel<KV, HBV, 8, 4><<<grid, 256, lds, s>>>(a);                   \
       else elbo_head_wave_kernel<KV, HBV, 16, 4><<<grid, 256, lds, s>>>(a);                           \
+    } else if (nbw == 2) {                                                                             \
+      const size_t lds = head_wave_lds<2>(HBV);                                                        \
+      if (a.D <= 8) elbo_head_wave_kernel<KV, HBV, 8, 2><<<grid, 256, lds, s>>>(a);                   \
+      else elbo_head_wave_kernel<KV, HBV, 16, 2><<<grid, 256, lds, s>>>(a);                           \
     } else {                                                                                           \
       const size_t lds = head_wave_lds<1>(HBV);                                                        \
       if (a.D <= 8) elbo_head_wave_kernel<KV, HBV, 8, 1><<<grid, 256, lds, s>>>(a);                   \

@@ -48,6 +48,7 @@ struct ConvArgs {
   const float* lb_h;
   float* lb_dh;
   int lb_C;
+  int pipe;          // conv2 kernels: software-pipelined operand reads (set by the launcher)
 };
 
 // Loss normalisers of compute_loss (VQ_VAE_HMM_fixed.py:120 mask.sum()*C, :131/:135 B).
@@ -103,6 +104,7 @@ struct WgradArgs {
   int64_t rows_per_chunk;  // multiple of 64
   float* slab;       // [nchunks][N][C][ks]
   float* bias_slab;  // [nchunks][N] or null
+  int pipe;          // wgrad2: software-pipelined operand reads (set by the launcher; VQHMM_WGRAD_PIPE=0 A/B)
 };
 
 struct HeadArgs {

@@ -22,8 +22,8 @@ namespace {
 constexpr int RT = 64;  // rows per stage
 }
 
-template <int NBW, int CBW, int KS, int NPAD, int CPAD>
-__global__ __launch_bounds__(256) void wgrad2_kernel(WgradArgs a, int WN, int WC, int WR) {
+template <int NBW, int CBW, int KS, int NPAD, int CPAD, int WR>
+__global__ __launch_bounds__(256) void wgrad2_kernel(WgradArgs a, int WN, int WC) {
   constexpr int LDA = NPAD + 4, LDB = CPAD + 4;  // 4*LD = 16 (mod 32): conflict-free b32 column reads
   constexpr int DY4 = RT * NPAD / 4;             // float4 slots of the dY stage
   constexpr int X4 = (RT + 2) * CPAD / 4;        // float4 slots of the X stage
@@ -116,24 +116,48 @@ __global__ __launch_bounds__(256) void wgrad2_kernel(WgradArgs a, int WN, int WC
     if (a.bias_slab) {
       for (int row = brow0; row < RT; row += bstep) bacc += dys[row * LDA + bcol];
     }
-    // this wave's 16-row slices of the stage
-    for (int sl = wr; sl < RT / 16; sl += WR) {
+    // this wave's 16-row slices of the stage, as 4 * (4 / WR) MFMA steps (one row per lane group
+    // each): the operands of step s + 1 are read from LDS while the MFMAs of step s run (two
+    // register sets, sched_barrier keeps the reads ahead); each accumulator's chain is unchanged
+    constexpr int NST = 4 * (4 / WR);
+    float av[2][NBW], bv[2][KS][CBW];
+    auto load = [&](int st, float (&a_)[NBW], float (&b_)[KS][CBW]) {
+      const int sl = wr + (st >> 2) * WR, e = st & 3;
+      const int rr = sl * 16 + 4 * lg4 + e;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int rr = sl * 16 + 4 * lg4 + e;
-        float av[NBW];
+      for (int i = 0; i < NBW; ++i) a_[i] = dys[rr * LDA + (wn + i * WN) * 16 + l16];
 #pragma unroll
-        for (int i = 0; i < NBW; ++i) av[i] = dys[rr * LDA + (wn + i * WN) * 16 + l16];
+      for (int tp = 0; tp < KS; ++tp) {
+        const int xrow = rr + (KS == 3 ? tp : 1);
 #pragma unroll
-        for (int tp = 0; tp < KS; ++tp) {
-          const int xrow = rr + (KS == 3 ? tp : 1);
+        for (int j = 0; j < CBW; ++j) b_[tp][j] = xs[xrow * LDB + (wc + j * WC) * 16 + l16];
+      }
+    };
+    if (a.pipe) {
+      load(0, av[0], bv[0]);
 #pragma unroll
-          for (int j = 0; j < CBW; ++j) {
-            const float bv = xs[xrow * LDB + (wc + j * WC) * 16 + l16];
+      for (int st = 0; st < NST; ++st) {
+        const int cb = st & 1;
+        if (st + 1 < NST) load(st + 1, av[cb ^ 1], bv[cb ^ 1]);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int i = 0; i < NBW; ++i) acc[tp][i][j] = mfma16x16x4(av[i], bv, acc[tp][i][j]);
-          }
-        }
+        for (int tp = 0; tp < KS; ++tp)
+#pragma unroll
+          for (int j = 0; j < CBW; ++j)
+#pragma unroll
+            for (int i = 0; i < NBW; ++i) acc[tp][i][j] = mfma16x16x4(av[cb][i], bv[cb][tp][j], acc[tp][i][j]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {  // A/B reference: the compiler's own schedule
+#pragma unroll
+      for (int st = 0; st < NST; ++st) {
+        load(st, av[0], bv[0]);
+#pragma unroll
+        for (int tp = 0; tp < KS; ++tp)
+#pragma unroll
+          for (int j = 0; j < CBW; ++j)
+#pragma unroll
+            for (int i = 0; i < NBW; ++i) acc[tp][i][j] = mfma16x16x4(av[0][i], bv[0][tp][j], acc[tp][i][j]);
       }
     }
   }
@@ -224,11 +248,18 @@ int64_t wgrad2_rows(int64_t R, int N, int C, int ks) {
   return cdiv(rows, RT) * RT;
 }
 
-template <int NBW, int CBW, int KS, int NPAD, int CPAD>
-static int launch_w2(const WgradArgs& a, int WN, int WC, int WR, hipStream_t s) {
+template <int NBW, int CBW, int KS, int NPAD, int CPAD, int WR>
+static int launch_w2(const WgradArgs& a, int WN, int WC, hipStream_t s) {
   const int64_t nchunks = cdiv(a.R, a.rows_per_chunk);
   if (WR > 1 && (NBW * CBW != 1 || KS * 4 * 64 * (4 / WR) > 1536)) return VQHMM_EUNSUPPORTED;
-  wgrad2_kernel<NBW, CBW, KS, NPAD, CPAD><<<(unsigned)nchunks, 256, 0, s>>>(a, WN, WC, WR);
+  if (WN * WC * WR != 4) return VQHMM_EINVAL;
+  static const bool pipe = [] {
+    const char* e = getenv("VQHMM_WGRAD_PIPE");
+    return !(e && e[0] == '0');
+  }();
+  WgradArgs ap = a;
+  ap.pipe = pipe;
+  wgrad2_kernel<NBW, CBW, KS, NPAD, CPAD, WR><<<(unsigned)nchunks, 256, 0, s>>>(ap, WN, WC);
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
 }
@@ -237,16 +268,16 @@ template <int KS>
 static int launch_w2_ks(const WgradArgs& a, hipStream_t s) {
   const int nbn = (int)cdiv(a.N, 16), nbc = (int)cdiv(a.C, 16);
   // choose the wave split: prefer output blocks, then rows
-  if (nbn == 4 && nbc == 4) return launch_w2<4, 1, KS, 64, 64>(a, 1, 4, 1, s);
-  if (nbn == 2 && nbc == 4) return launch_w2<2, 1, KS, 32, 64>(a, 1, 4, 1, s);
-  if (nbn == 4 && nbc == 2) return launch_w2<1, 2, KS, 64, 32>(a, 4, 1, 1, s);
-  if (nbn == 1 && nbc == 4) return launch_w2<1, 1, KS, 16, 64>(a, 1, 4, 1, s);
-  if (nbn == 4 && nbc == 1) return launch_w2<1, 1, KS, 64, 16>(a, 4, 1, 1, s);
-  if (nbn == 1 && nbc == 2) return launch_w2<1, 1, KS, 16, 32>(a, 1, 2, 2, s);
-  if (nbn == 2 && nbc == 1) return launch_w2<1, 1, KS, 32, 16>(a, 2, 1, 2, s);
-  if (nbn == 2 && nbc == 2) return launch_w2<1, 1, KS, 32, 32>(a, 2, 2, 1, s);
-  if (nbn == 1 && nbc == 1) return launch_w2<1, 1, KS, 16, 16>(a, 1, 1, 4, s);
-  if (nbn <= 4 && nbc <= 4) return launch_w2<4, 1, KS, 64, 64>(a, 1, 4, 1, s);
+  if (nbn == 4 && nbc == 4) return launch_w2<4, 1, KS, 64, 64, 1>(a, 1, 4, s);
+  if (nbn == 2 && nbc == 4) return launch_w2<2, 1, KS, 32, 64, 1>(a, 1, 4, s);
+  if (nbn == 4 && nbc == 2) return launch_w2<1, 2, KS, 64, 32, 1>(a, 4, 1, s);
+  if (nbn == 1 && nbc == 4) return launch_w2<1, 1, KS, 16, 64, 1>(a, 1, 4, s);
+  if (nbn == 4 && nbc == 1) return launch_w2<1, 1, KS, 64, 16, 1>(a, 4, 1, s);
+  if (nbn == 1 && nbc == 2) return launch_w2<1, 1, KS, 16, 32, 2>(a, 1, 2, s);
+  if (nbn == 2 && nbc == 1) return launch_w2<1, 1, KS, 32, 16, 2>(a, 2, 1, s);
+  if (nbn == 2 && nbc == 2) return launch_w2<1, 1, KS, 32, 32, 1>(a, 2, 2, s);
+  if (nbn == 1 && nbc == 1) return launch_w2<1, 1, KS, 16, 16, 4>(a, 1, 1, s);
+  if (nbn <= 4 && nbc <= 4) return launch_w2<4, 1, KS, 64, 64, 1>(a, 1, 4, s);
   return VQHMM_EUNSUPPORTED;
 }
 
