@@ -8,6 +8,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+
 #include "kernels.h"
 
 
@@ -37,6 +39,24 @@ bool head_legacy() {
   static const bool v = [] {
     const char* e = getenv("VQHMM_HEAD");
     return e && strcmp(e, "tile") == 0;
+  }();
+  return v;
+}
+
+// A/B switches, read once: VQHMM_WGROUP=0 launches the six weight gradients separately;
+// VQHMM_WGRAD_MINROWS = the grouped launch's minimum rows per chunk (multiple of 64).
+bool wgroup_enabled() {
+  static const bool v = [] {
+    const char* e = getenv("VQHMM_WGROUP");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+int64_t wgroup_min_rows() {
+  static const int64_t v = [] {
+    const char* e = getenv("VQHMM_WGRAD_MINROWS");
+    const long r = e ? atol(e) : 128;  // 2 stages: fewer, fuller slabs at small batches (B = 128: 0.165 -> 0.158 ms)
+    return (int64_t)(r >= 64 && r <= 65536 && r % 64 == 0 ? r : 128);
   }();
   return v;
 }
@@ -73,6 +93,7 @@ struct ElboPlan {
   // backward
   float *dg2, *dg1, *dqd, *dlog, *dh2, *dh1, *dWc;
   float *Ecopy, *Wcopy;  // the prologue's copies of decoder.embeddings / decoder.conv1 weights (compose_adam)
+  bool wgroup;           // the six weight gradients run as one grouped launch (wgrad2_group)
   int nwl;
   WLayer wl[8];  // 0 to_params, 1 dec2, 2 dec1', 3 to_logits, 4 enc2, 5 enc1, [6 Prior W1, 7 Prior W2]
   float* img[32];  // per stage: packed conv2_kernel weight image (WImgJob), built by the prologue, or null
@@ -143,11 +164,18 @@ ElboPlan plan_elbo(const vqhmm_dims_t* d, int64_t B, int64_t T, void* ws) {
   const int shapes[8][3] = {{2 * D, H, 1}, {H, H, 3}, {H, K, 3}, {K, H2, 1}, {H2, H, 3}, {H, D, 3},
                             {p.TH, p.U, 1}, {K * K, p.TH, 1}};
   p.nwl = p.staged ? 8 : 6;
+  p.wgroup = wgroup_enabled();
+  for (int i = 0; i < 6; ++i) {
+    WgradArgs t{};
+    t.N = shapes[i][0]; t.C = shapes[i][1]; t.ks = shapes[i][2];
+    p.wgroup = p.wgroup && wgrad2_group_supported(t);
+  }
   for (int i = 0; i < p.nwl; ++i) {
     WLayer& w = p.wl[i];
     w.N = shapes[i][0]; w.C = shapes[i][1]; w.ks = shapes[i][2];
     const int64_t tiles = cdiv(w.N, 64) * cdiv(w.C, 64);
     w.rows = (w.N <= 64 && w.C <= 64) ? wgrad2_rows(R, w.N, w.C, w.ks) : wgrad_chunks(R, tiles);
+    if (i < 6 && p.wgroup) w.rows = std::max<int64_t>(w.rows, wgroup_min_rows());
     w.nchunks = cdiv(R, w.rows);
     w.slab = c.take<float>((size_t)w.nchunks * w.N * w.C * w.ks);
     w.bslab = c.take<float>((size_t)w.nchunks * w.N);
@@ -381,6 +409,19 @@ bool logits_bwd_fused(const ElboPlan& p) { return p.K <= 4 && conv2_supported(co
 // ... and to_logits' dgrad too when the encoder conv2 width splits into float4s over the 4 lane groups.
 bool logits_dg_fused(const ElboPlan& p) { return logits_bwd_fused(p) && ld4(p.H2) % 16 == 0 && p.H2 <= 64; }
 
+// The six convolutions' weight-gradient problems, in S_W_PAR .. S_W_ENC1 order.
+void wgrad_jobs(const ElboPlan& p, WgradArgs* wa) {
+  const float* dys[6] = {p.dpar, p.dg2, p.dg1, p.dlog, p.dh2, p.dh1};
+  const float* xs[6] = {p.g2, p.g1, p.q, p.h2e, p.h1e, p.xp};
+  for (int i = 0; i < 6; ++i) {
+    const WLayer& L = p.wl[i];
+    wa[i] = WgradArgs{};
+    wa[i].dy = dys[i]; wa[i].x = xs[i]; wa[i].x_cf = 0; wa[i].R = p.R; wa[i].T = p.T;
+    wa[i].N = L.N; wa[i].C = L.C; wa[i].ks = L.ks; wa[i].rows_per_chunk = L.rows; wa[i].slab = L.slab;
+    wa[i].bias_slab = L.bslab;
+  }
+}
+
 int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
   const float* const* w = c.w;
   switch (st) {
@@ -440,14 +481,13 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       if (logits_bwd_fused(p)) return VQHMM_OK;  // ran in S_DEC1_DG's epilogue
       return launch_logits_bwd(p.q, p.dqd, p.dqx, p.dlx, c.gscale, p.R, p.K, p.dlog, s);
     case S_W_PAR: case S_W_DEC2: case S_W_DEC1: case S_W_LOGIT: case S_W_ENC2: case S_W_ENC1: {
-      const int i = st - S_W_PAR;
-      const float* dys[6] = {p.dpar, p.dg2, p.dg1, p.dlog, p.dh2, p.dh1};
-      const float* xs[6] = {p.g2, p.g1, p.q, p.h2e, p.h1e, p.xp};
-      const WLayer& L = p.wl[i];
-      WgradArgs wa{};
-      wa.dy = dys[i]; wa.x = xs[i]; wa.x_cf = 0; wa.R = p.R; wa.T = p.T;
-      wa.N = L.N; wa.C = L.C; wa.ks = L.ks; wa.rows_per_chunk = L.rows; wa.slab = L.slab; wa.bias_slab = L.bslab;
-      return launch_wgrad(wa, s);
+      WgradArgs wa[6];
+      wgrad_jobs(p, wa);
+      if (p.wgroup) {  // all six in S_W_ENC1's launch (every dY is ready by then, in any stage order)
+        if (st != S_W_ENC1) return VQHMM_OK;
+        return launch_wgrad2_group(wa, 6, s);
+      }
+      return launch_wgrad(wa[st - S_W_PAR], s);
     }
     case S_REDUCE: {
       int64_t off[VQHMM_NPARAMS + 1];
@@ -522,9 +562,12 @@ void stage_work(const ElboPlan& p, int st, double* flops, double* bytes, int* mf
     *bytes = 4.0 * (R * a.Kc + R * a.N + (a.act == 2 ? R * a.N : 0) + (a.tW ? R * a.C2 * (a.q_out ? 2 : 1) : 0));
     *mfma = 1;
   } else if (st >= S_W_PAR && st <= S_W_ENC1) {
-    const WLayer& L = p.wl[st - S_W_PAR];
-    *flops = 2.0 * N * L.N * L.C * L.ks;
-    *bytes = 4.0 * (R * L.N + R * L.C + (double)L.nchunks * (L.N * L.C * L.ks + L.N));
+    const int i0 = p.wgroup ? 0 : st - S_W_PAR, i1 = p.wgroup ? (st == S_W_ENC1 ? 6 : 0) : i0 + 1;
+    for (int i = i0; i < i1; ++i) {  // grouped: S_W_ENC1's launch does all six
+      const WLayer& L = p.wl[i];
+      *flops += 2.0 * N * L.N * L.C * L.ks;
+      *bytes += 4.0 * (R * L.N + R * L.C + (double)L.nchunks * (L.N * L.C * L.ks + L.N));
+    }
     *mfma = 1;
   } else if (st == S_HEAD) {
     const double KK = (double)p.K * p.K;
@@ -604,7 +647,10 @@ int vqhmm_elbo_stage_info(const vqhmm_dims_t* d, int64_t B, int64_t T, int stage
   if (!dims_ok(d) || stage < 0 || stage >= S_COUNT || B <= 0 || T <= 0) return VQHMM_EINVAL;
   ElboPlan p = plan_elbo(d, B, T, nullptr);
   if (name && name_len) {
-    strncpy(name, kStageNames[stage], name_len - 1);
+    const char* nm = kStageNames[stage];
+    if (p.wgroup && stage == S_W_ENC1) nm = "wgrad_group(all 6 weight gradients)";
+    else if (p.wgroup && stage >= S_W_PAR && stage < S_W_ENC1) nm = "(wgrad: in wgrad_group)";
+    strncpy(name, nm, name_len - 1);
     name[name_len - 1] = 0;
   }
   double f, b;

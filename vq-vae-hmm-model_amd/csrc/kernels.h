@@ -195,6 +195,17 @@ int64_t wgrad_chunks(int64_t R, int64_t tiles);
 bool wgrad2_supported(const WgradArgs& a);
 int64_t wgrad2_rows(int64_t R, int N, int C, int ks);
 int launch_wgrad2(const WgradArgs& a, hipStream_t s);
+// A step's weight gradients as ONE launch (wgrad2.hip): job j's chunks are workgroups
+// [blk0[j], blk0[j+1]); every job must be wgrad2_group_supported.
+constexpr int MAX_WJOBS = 8;
+struct WgradGroup {
+  WgradArgs job[MAX_WJOBS];
+  int variant[MAX_WJOBS], wn[MAX_WJOBS], wc[MAX_WJOBS];
+  int64_t blk0[MAX_WJOBS + 1];
+  int njobs;
+};
+bool wgrad2_group_supported(const WgradArgs& a);
+int launch_wgrad2_group(const WgradArgs* jobs, int n, hipStream_t s);
 // Staged ELBO head (head_staged.hip): shapes the fused heads do not cover.
 struct StagedHeadArgs {
   int64_t B;

@@ -14,6 +14,8 @@
 //    the slabs in a fixed order (deterministic, no atomics).
 #include <stdlib.h>
 
+#include <utility>
+
 #include "kernels.h"
 
 namespace vqhmm {
@@ -22,21 +24,26 @@ namespace {
 constexpr int RT = 64;  // rows per stage
 }
 
+// LDS floats of one wgrad2 body: dY stage, X stage, bias partials, row-wave exchange
+template <int NPAD, int CPAD>
+constexpr int w2_lds_floats() { return RT * (NPAD + 4) + (RT + 2) * (CPAD + 4) + 256 + 1536; }
+constexpr int W2_LDS_MAX = RT * 68 + (RT + 2) * 68 + 256 + 1536;
+
+// One chunk (workgroup) of the split-K weight gradient; smem = w2_lds_floats<NPAD, CPAD>() floats.
 template <int NBW, int CBW, int KS, int NPAD, int CPAD, int WR>
-__global__ __launch_bounds__(256) void wgrad2_kernel(WgradArgs a, int WN, int WC) {
+__device__ __forceinline__ void wgrad2_body(const WgradArgs& a, int WN, int WC, int64_t chunk, float* smem) {
   constexpr int LDA = NPAD + 4, LDB = CPAD + 4;  // 4*LD = 16 (mod 32): conflict-free b32 column reads
   constexpr int DY4 = RT * NPAD / 4;             // float4 slots of the dY stage
   constexpr int X4 = (RT + 2) * CPAD / 4;        // float4 slots of the X stage
   constexpr int PD = (DY4 + 255) / 256, PX = (X4 + 255) / 256;
-  __shared__ float dys[RT * LDA];
-  __shared__ float xs[(RT + 2) * LDB];
-  __shared__ float bred[256];
-  __shared__ float xbuf[1536];  // row-wave exchange (WR > 1 only with NBW = CBW = 1)
+  float* dys = smem;                  // [RT][LDA]
+  float* xs = dys + RT * LDA;         // [RT + 2][LDB]
+  float* bred = xs + (RT + 2) * LDB;  // [256]
+  float* xbuf = bred + 256;           // [1536] row-wave exchange (WR > 1 only with NBW = CBW = 1)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lg4 = lane >> 4, l16 = lane & 15;
   const int wr = wave % WR, wc = (wave / WR) % WC, wn = wave / (WR * WC);
-  const int64_t chunk = blockIdx.x;
   const int64_t rbeg = chunk * a.rows_per_chunk;
   const int64_t rend = min(a.R, rbeg + a.rows_per_chunk);
 
@@ -218,6 +225,96 @@ __global__ __launch_bounds__(256) void wgrad2_kernel(WgradArgs a, int WN, int WC
   }
 }
 
+template <int NBW, int CBW, int KS, int NPAD, int CPAD, int WR>
+__global__ __launch_bounds__(256) void wgrad2_kernel(WgradArgs a, int WN, int WC) {
+  extern __shared__ float4 smem4[];
+  wgrad2_body<NBW, CBW, KS, NPAD, CPAD, WR>(a, WN, WC, blockIdx.x, reinterpret_cast<float*>(smem4));
+}
+
+// ---- all of a step's weight gradients in ONE launch (WgradGroup): workgroup b runs chunk
+// b - blk0[j] of job j.  Each job is one of the launch shapes below (variant id = its row in
+// w2_variant, +10 for k = 3), so every body keeps its own register/LDS layout; big jobs come
+// first so their workgroups start first and the small ones fill the tail.
+#define VQHMM_W2_VARIANTS(KSV, O)                                     \
+  case O + 0: wgrad2_body<4, 1, KSV, 64, 64, 1>(a, WN, WC, ch, sm); break; \
+  case O + 1: wgrad2_body<2, 1, KSV, 32, 64, 1>(a, WN, WC, ch, sm); break; \
+  case O + 2: wgrad2_body<1, 2, KSV, 64, 32, 1>(a, WN, WC, ch, sm); break; \
+  case O + 3: wgrad2_body<1, 1, KSV, 16, 64, 1>(a, WN, WC, ch, sm); break; \
+  case O + 4: wgrad2_body<1, 1, KSV, 64, 16, 1>(a, WN, WC, ch, sm); break; \
+  case O + 5: wgrad2_body<1, 1, KSV, 16, 32, 2>(a, WN, WC, ch, sm); break; \
+  case O + 6: wgrad2_body<1, 1, KSV, 32, 16, 2>(a, WN, WC, ch, sm); break; \
+  case O + 7: wgrad2_body<1, 1, KSV, 32, 32, 1>(a, WN, WC, ch, sm); break; \
+  case O + 8: wgrad2_body<1, 1, KSV, 16, 16, 4>(a, WN, WC, ch, sm); break;
+
+__global__ __launch_bounds__(256) void wgrad2_group_kernel(WgradGroup g) {
+  __shared__ float sm[W2_LDS_MAX];
+  int j = 0;
+  while (j + 1 < g.njobs && (int64_t)blockIdx.x >= g.blk0[j + 1]) ++j;
+  const WgradArgs& a = g.job[j];
+  const int WN = g.wn[j], WC = g.wc[j];
+  const int64_t ch = (int64_t)blockIdx.x - g.blk0[j];
+  switch (g.variant[j]) {
+    VQHMM_W2_VARIANTS(1, 0)
+    VQHMM_W2_VARIANTS(3, 10)
+    default: break;
+  }
+}
+#undef VQHMM_W2_VARIANTS
+
+// launch shape of a job: variant id (see above) and its wave split (WN, WC); -1 if none
+static int w2_variant(int N, int C, int ks, int* WN, int* WC) {
+  const int nbn = (int)cdiv(N, 16), nbc = (int)cdiv(C, 16);
+  int v;
+  if (nbn == 4 && nbc == 4) { v = 0; *WN = 1; *WC = 4; }
+  else if (nbn == 2 && nbc == 4) { v = 1; *WN = 1; *WC = 4; }
+  else if (nbn == 4 && nbc == 2) { v = 2; *WN = 4; *WC = 1; }
+  else if (nbn == 1 && nbc == 4) { v = 3; *WN = 1; *WC = 4; }
+  else if (nbn == 4 && nbc == 1) { v = 4; *WN = 4; *WC = 1; }
+  else if (nbn == 1 && nbc == 2) { v = 5; *WN = 1; *WC = 2; }
+  else if (nbn == 2 && nbc == 1) { v = 6; *WN = 2; *WC = 1; }
+  else if (nbn == 2 && nbc == 2) { v = 7; *WN = 2; *WC = 2; }
+  else if (nbn == 1 && nbc == 1) { v = 8; *WN = 1; *WC = 1; }
+  else if (nbn <= 4 && nbc <= 4) { v = 0; *WN = 1; *WC = 4; }
+  else return -1;
+  return v + (ks == 3 ? 10 : 0);
+}
+
+bool wgrad2_group_supported(const WgradArgs& a) {
+  int wn, wc;
+  return !a.x_cf && a.N <= 64 && a.C <= 64 && (a.ks == 1 || a.ks == 3) && w2_variant(a.N, a.C, a.ks, &wn, &wc) >= 0;
+}
+
+int launch_wgrad2_group(const WgradArgs* jobs, int n, hipStream_t s) {
+  if (n < 1 || n > MAX_WJOBS) return VQHMM_EINVAL;
+  WgradGroup g{};
+  static const bool pipe = [] {
+    const char* e = getenv("VQHMM_WGRAD_PIPE");
+    return !(e && e[0] == '0');
+  }();
+  // biggest outputs first (their chunks run longest)
+  int ord[MAX_WJOBS];
+  for (int i = 0; i < n; ++i) ord[i] = i;
+  for (int i = 1; i < n; ++i)
+    for (int k = i; k > 0; --k) {
+      const WgradArgs &x = jobs[ord[k]], &y = jobs[ord[k - 1]];
+      if ((int64_t)x.N * x.C * x.ks > (int64_t)y.N * y.C * y.ks) std::swap(ord[k], ord[k - 1]);
+    }
+  g.njobs = n;
+  g.blk0[0] = 0;
+  for (int i = 0; i < n; ++i) {
+    const WgradArgs& a = jobs[ord[i]];
+    if (!wgrad2_group_supported(a) || a.rows_per_chunk % RT) return VQHMM_EINVAL;
+    g.job[i] = a;
+    g.job[i].pipe = pipe;
+    g.variant[i] = w2_variant(a.N, a.C, a.ks, &g.wn[i], &g.wc[i]);
+    g.blk0[i + 1] = g.blk0[i] + cdiv(a.R, a.rows_per_chunk);
+  }
+  if (g.blk0[n] == 0) return VQHMM_OK;
+  wgrad2_group_kernel<<<(unsigned)g.blk0[n], 256, 0, s>>>(g);
+  VQHMM_LAUNCH_CHECK();
+  return VQHMM_OK;
+}
+
 bool wgrad2_supported(const WgradArgs& a) { return !a.x_cf && a.N <= 64 && a.C <= 64; }
 
 // chunks per launch for big outputs (tuning override VQHMM_WGRAD_BIG_CHUNKS, read once)
@@ -259,7 +356,8 @@ static int launch_w2(const WgradArgs& a, int WN, int WC, hipStream_t s) {
   }();
   WgradArgs ap = a;
   ap.pipe = pipe;
-  wgrad2_kernel<NBW, CBW, KS, NPAD, CPAD, WR><<<(unsigned)nchunks, 256, 0, s>>>(ap, WN, WC);
+  wgrad2_kernel<NBW, CBW, KS, NPAD, CPAD, WR>
+      <<<(unsigned)nchunks, 256, w2_lds_floats<NPAD, CPAD>() * sizeof(float), s>>>(ap, WN, WC);
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
 }
