@@ -113,7 +113,9 @@ int vqhmm_fwdbwd_f32(const float* log_pi, const float* log_A, const float* em, c
  * and the backward must get the same workspace, dims, B and T.
  * loss: device fp32 scalar; loss_accum (nullable): device fp64 scalar += loss
  *   (train_model's epoch_loss, :158, without a per-step host sync).
- * need_grad = 0 computes only the loss.
+ * need_grad = 0 computes only the loss; 2 = as 1, but the loss (and loss_accum) are left to the
+ *   backward: vqhmm_elbo_bwd_adam_f32 with its loss pointers finalizes them in its own last
+ *   launches (one launch fewer per step).
  * norm: NULL, or a device int64[2] {valid_count, batch} replacing the batch's own
  *   loss normalisers mask.sum() (:120) and B (:131, :135).  Pass the GLOBAL batch's
  *   values when this batch is one shard of it: the shards' losses and gradients then
@@ -134,12 +136,14 @@ int vqhmm_elbo_bwd_f32(const vqhmm_dims_t* dims, const float* const* params, con
  * also applies vqhmm_adam_f32's update to every parameter element (same formula, same
  * device step counter and ticket), saving the separate update launch; grad still receives
  * the full gradient.  params[i] must be param + offset[i] of vqhmm_param_layout (the flat
- * buffer Adam updates in place).  adam_grad_scale multiplies the gradient inside Adam only. */
+ * buffer Adam updates in place).  adam_grad_scale multiplies the gradient inside Adam only.
+ * loss / loss_accum: NULL, or (after a forward with need_grad = 2) where the forward's loss is
+ * finalized, as vqhmm_elbo_fwd_f32 would have. */
 int vqhmm_elbo_bwd_adam_f32(const vqhmm_dims_t* dims, const float* const* params, const float* x,
                             const int64_t* norm, int64_t B, int64_t T, float beta, void* workspace,
                             size_t ws_bytes, float* grad, float* param, float* exp_avg, float* exp_avg_sq,
                             double lr, double beta1, double beta2, double eps, int64_t* step,
-                            float adam_grad_scale, void* stream);
+                            float adam_grad_scale, float* loss, double* loss_accum, void* stream);
 /* Device addresses (inside the workspace) of the last forward's loss and of its
  * pieces [recon, prior, entropy] (for tests).  Host-only, no GPU access. */
 int vqhmm_elbo_pieces(const vqhmm_dims_t* dims, int64_t B, int64_t T, const void* workspace,

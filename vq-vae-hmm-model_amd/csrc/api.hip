@@ -86,6 +86,7 @@ struct ElboPlan {
   double* part;
   float *sW1, *sb1, *sW2, *sb2, *sq0;
   float *loss, *pieces;
+  int64_t* cnt;  // valid count written by the prologue (loss finalized in the backward)
   // staged head (shapes the fused heads do not cover): Prior MLP as 1x1 convs
   bool staged;
   bool wave_head;  // head_wave.hip (else head_mfma / head.hip)
@@ -152,6 +153,7 @@ ElboPlan plan_elbo(const vqhmm_dims_t* d, int64_t B, int64_t T, void* ws) {
   }
   p.loss = c.take<float>(1);
   p.pieces = c.take<float>(4);
+  p.cnt = c.take<int64_t>(1);
   p.dg2 = c.take<float>(R * ld4(H));
   p.dg1 = c.take<float>(R * ld4(H));
   p.dqd = c.take<float>(R * ld4(K));
@@ -195,7 +197,7 @@ ConvArgs conv_base(const ElboPlan& p) {
 
 extern "C" {
 
-int32_t vqhmm_abi_version(void) { return 4; }
+int32_t vqhmm_abi_version(void) { return 5; }
 
 int vqhmm_param_layout(const vqhmm_dims_t* d, int64_t off[VQHMM_NPARAMS + 1]) {
   if (!dims_ok(d) || !off) return VQHMM_EINVAL;
@@ -288,7 +290,7 @@ struct StepCtx {
   const int64_t* lengths;
   const int64_t* norm;  // null or device {valid_count, batch} (kernels.h loss_norm_batch)
   float beta;
-  int need_grad;
+  int need_grad;    // 2: as 1, but the loss is finalized by the backward's tail launch (defer_loss)
   float* loss;
   double* loss_accum;
   const float* gscale;
@@ -436,6 +438,7 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       a.wc_img_d = p.img[S_DEC1_DG];
       a.Ecopy = p.Ecopy;
       a.Wcopy = p.Wcopy;
+      if (c.need_grad == 2 && !c.norm) { a.lengths = c.lengths; a.cnt = p.cnt; }
       return launch_prologue(a, s);
     }
     case S_COMPOSE:  // runs inside S_TOPCL's launch
@@ -475,6 +478,7 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       return launch_head(h, p.hgrid, s);
     }
     case S_FINAL:
+      if (c.need_grad == 2) return VQHMM_OK;  // the backward's tail launch finalizes the loss
       return launch_finalize_loss(p.part, p.hgrid, c.lengths, c.norm, p.B, p.T, p.D, c.beta, c.loss, c.loss_accum,
                                   p.pieces, s);
     case S_LOGIT_BWD:
@@ -528,6 +532,10 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       ta.q0slab = p.sq0;
       ta.q0chunks = p.staged ? 1 : p.hgrid;
       ta.lp = LogPriorGradArgs{nullptr, w[LOG_PRIOR], p.K, c.beta, c.norm, p.B, c.gscale, g + off[LOG_PRIOR]};
+      if (c.loss) {  // the forward ran with need_grad = 2
+        ta.fin_part = p.part; ta.fin_nblk = p.hgrid; ta.fin_cnt = p.cnt; ta.fin_B = p.B; ta.fin_T = p.T;
+        ta.fin_D = p.D; ta.fin_loss = c.loss; ta.fin_accum = c.loss_accum; ta.fin_pieces = p.pieces;
+      }
       return launch_grad_tail(ta, s);
     }
     case S_COMPOSE_BWD: {
@@ -598,7 +606,9 @@ extern "C" {
 int vqhmm_elbo_fwd_f32(const vqhmm_dims_t* d, const float* const* w, const float* x, const float* u, int u_layout,
                        const int64_t* lengths, const int64_t* norm, int64_t B, int64_t T, float beta, int need_grad,
                        void* ws, size_t ws_bytes, float* loss, double* loss_accum, void* stream) {
-  if (!dims_ok(d) || !w || B <= 0 || T <= 0 || !x || !u || !lengths || !ws || !loss) return VQHMM_EINVAL;
+  if (!dims_ok(d) || !w || B <= 0 || T <= 0 || !x || !u || !lengths || !ws || !loss || need_grad < 0 ||
+      need_grad > 2)
+    return VQHMM_EINVAL;
   for (int i = 0; i < VQHMM_NPARAMS; ++i)
     if (!w[i]) return VQHMM_EINVAL;
   ElboPlan p = plan_elbo(d, B, T, ws);
@@ -624,7 +634,7 @@ int vqhmm_elbo_bwd_f32(const vqhmm_dims_t* d, const float* const* w, const float
 int vqhmm_elbo_bwd_adam_f32(const vqhmm_dims_t* d, const float* const* w, const float* x, const int64_t* norm,
                             int64_t B, int64_t T, float beta, void* ws, size_t ws_bytes, float* g, float* param,
                             float* exp_avg, float* exp_avg_sq, double lr, double beta1, double beta2, double eps,
-                            int64_t* step, float grad_scale, void* stream) {
+                            int64_t* step, float grad_scale, float* loss, double* loss_accum, void* stream) {
   if (!dims_ok(d) || !w || B <= 0 || T <= 0 || !x || !ws || !g || !param || !exp_avg || !exp_avg_sq || !step)
     return VQHMM_EINVAL;
   ElboPlan p = plan_elbo(d, B, T, ws);
@@ -634,7 +644,7 @@ int vqhmm_elbo_bwd_adam_f32(const vqhmm_dims_t* d, const float* const* w, const 
   for (int i = 0; i < VQHMM_NPARAMS; ++i)  // the last launch updates param in place: w must be its views
     if (w[i] != param + off[i]) return VQHMM_EINVAL;
   AdamArgs ad{param, exp_avg, exp_avg_sq, step, lr, beta1, beta2, eps, grad_scale};
-  StepCtx c{w, x, nullptr, 0, nullptr, norm, beta, 1, nullptr, nullptr, nullptr, g, &ad};
+  StepCtx c{w, x, nullptr, 0, nullptr, norm, beta, 1, loss, loss_accum, nullptr, g, &ad};
   for (int st = BWD_FIRST; st <= BWD_LAST; ++st)
     if (int rc = run_stage(p, c, st, (hipStream_t)stream)) return rc;
   return VQHMM_OK;

@@ -62,14 +62,17 @@ __device__ __forceinline__ float loss_norm_batch(const int64_t* norm, int64_t B)
 // finalize_loss: loss = recon + beta*(prior - entropy) (VQ_VAE_HMM_fixed.py:137) from the head's
 // per-workgroup partials part[nblk][4] = recon_sum, init_sum, trans_sum, ent_sum; run by the 256
 // threads of ONE workgroup; red = 5*256 doubles of LDS.
+// cnt (nullable): the batch's valid count already reduced on the device (the prologue's), used
+// instead of a pass over lengths when norm is null.
 __device__ inline void finalize_loss_block(const double* part, int nblk, const int64_t* lengths, const int64_t* norm,
                                            int64_t B, int T, int D, float beta, float* loss, double* accum,
-                                           float* pieces, double* red) {
+                                           float* pieces, double* red, const int64_t* cnt = nullptr) {
   const int tid = threadIdx.x;
   double v[5] = {0, 0, 0, 0, 0};
   for (int i = tid; i < nblk; i += 256)
     for (int k = 0; k < 4; ++k) v[k] += part[i * 4 + k];
-  for (int64_t b = tid; !norm && b < B; b += 256) {
+  if (!norm && cnt && tid == 0) v[4] = (double)*cnt;
+  for (int64_t b = tid; !norm && !cnt && b < B; b += 256) {
     const int64_t L = lengths[b];
     v[4] += (double)(L <= 0 ? 0 : (L < T ? L : T));
   }
@@ -248,6 +251,16 @@ struct TailArgs {
   const float* q0slab;   // [q0chunks][K]: sum_b q[b, :, 0] partials (log_prior gradient), or null
   int64_t q0chunks;
   LogPriorGradArgs lp;   // q0sum unused (the tail block reduces q0slab itself)
+  // loss finalize deferred from the forward (fin_loss set): one more workgroup runs
+  // finalize_loss_block on the head's partials with the prologue's valid count
+  const double* fin_part;
+  int fin_nblk;
+  const int64_t* fin_cnt;
+  int64_t fin_B;
+  int fin_T, fin_D;
+  float* fin_loss;
+  double* fin_accum;
+  float* fin_pieces;
 };
 // torch.optim.Adam over the flat buffers (misc.hip adam_kernel / compose_adam_kernel)
 struct AdamArgs {
@@ -296,6 +309,8 @@ struct PrologueArgs {  // step prologue: x, u -> PCL, the composed decoder conv1
   float* wc_img_d;
   float* Ecopy;     // (K, H) / (H, H, 3) copies of the embedding and decoder.conv1's weight for the
   float* Wcopy;     // fused compose + Adam launch, or null
+  const int64_t* lengths;  // with cnt: the last block writes the batch's valid count
+  int64_t* cnt;            // (sum_b min(max(L_b, 0), T)) for a loss finalized in the backward, or null
   unsigned nbx, nbu;                // set by launch_prologue
   unsigned img_blk0[MAX_WIMG + 1];  // set by launch_prologue: first block of each image
 };

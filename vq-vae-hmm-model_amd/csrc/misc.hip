@@ -101,6 +101,12 @@ __global__ __launch_bounds__(256) void grad_tail_kernel(TailArgs ta) {
   __shared__ float red[256];
   __shared__ float scratch[256];
   const int64_t nblk = ta.blk_start[ta.nseg];
+  if (ta.fin_loss && (int64_t)blockIdx.x == nblk + (ta.q0slab ? 1 : 0)) {  // ---- the forward's loss
+    __shared__ double fred[5 * 256];
+    finalize_loss_block(ta.fin_part, ta.fin_nblk, nullptr, ta.lp.norm, ta.fin_B, ta.fin_T, ta.fin_D, ta.lp.beta,
+                        ta.fin_loss, ta.fin_accum, ta.fin_pieces, fred, ta.fin_cnt);
+    return;
+  }
   if ((int64_t)blockIdx.x >= nblk) {  // ---- log_prior gradient (VQ_VAE_HMM_fixed.py:71,:123,:131)
     const LogPriorGradArgs& lp = ta.lp;
     const int K = lp.K;
@@ -190,7 +196,7 @@ int launch_grad_tail(TailArgs& a, hipStream_t s) {
   if (a.nseg > MAX_SEGS || (a.q0slab && a.lp.K > 256)) return VQHMM_EINVAL;
   a.blk_start[0] = 0;
   for (int i = 0; i < a.nseg; ++i) a.blk_start[i + 1] = a.blk_start[i] + cdiv(a.s[i].len, 64);
-  const int64_t nb = a.blk_start[a.nseg] + (a.q0slab ? 1 : 0);
+  const int64_t nb = a.blk_start[a.nseg] + (a.q0slab ? 1 : 0) + (a.fin_loss ? 1 : 0);
   if (nb == 0) return VQHMM_OK;
   grad_tail_kernel<<<(unsigned)nb, 256, 0, s>>>(a);
   VQHMM_LAUNCH_CHECK();
@@ -550,11 +556,25 @@ __global__ __launch_bounds__(256) void prologue_kernel(PrologueArgs a) {
     to_pcl_slot(a.u, a.U, a.B, a.T, a.usc, a.ust, a.up, (int64_t)(bx - a.nbx) * 256 + threadIdx.x);
   } else if (bx < a.nbx + a.nbu + (unsigned)a.H) {
     compose_fwd_block(a.W, a.E, a.H, a.K, a.Wc, (int)(bx - a.nbx - a.nbu), cs, a.wc_img_f, a.wc_img_d, a.Ecopy, a.Wcopy);
-  } else {
+  } else if (bx < a.nbx + a.nbu + (unsigned)a.H + a.img_blk0[a.nimg]) {
     const unsigned ib = bx - a.nbx - a.nbu - (unsigned)a.H;
     int j = 0;
     while (j + 1 < a.nimg && ib >= a.img_blk0[j + 1]) ++j;
     wimg_slice(a.img[j], (int64_t)(ib - a.img_blk0[j]) * 256);
+  } else {  // the batch's valid count mask.sum() (VQ_VAE_HMM_fixed.py:111,:120), fixed order
+    __shared__ unsigned long long cred[256];
+    unsigned long long c = 0;
+    for (int64_t b = threadIdx.x; b < a.B; b += 256) {
+      const int64_t L = a.lengths[b];
+      c += (unsigned long long)(L <= 0 ? 0 : (L < a.T ? L : a.T));
+    }
+    cred[threadIdx.x] = c;
+    __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+      if ((int)threadIdx.x < st) cred[threadIdx.x] += cred[threadIdx.x + st];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) *a.cnt = (int64_t)cred[0];
   }
 }
 int launch_prologue(PrologueArgs a, hipStream_t s) {
@@ -566,7 +586,7 @@ int launch_prologue(PrologueArgs a, hipStream_t s) {
   for (int j = 0; j < a.nimg; ++j)
     a.img_blk0[j + 1] = a.img_blk0[j] + (unsigned)cdiv(c2_image_floats(a.img[j].N, a.img[j].Kc, a.img[j].ks), 256);
   const size_t lds = (size_t)(a.H * 3 + a.K * a.H) * 4;
-  prologue_kernel<<<a.nbx + a.nbu + (unsigned)a.H + a.img_blk0[a.nimg], 256, lds, s>>>(a);
+  prologue_kernel<<<a.nbx + a.nbu + (unsigned)a.H + a.img_blk0[a.nimg] + (a.cnt ? 1u : 0u), 256, lds, s>>>(a);
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
 }

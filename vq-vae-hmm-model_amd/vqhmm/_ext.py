@@ -12,7 +12,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libvqhmm.so")
 NPARAMS = 18
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 _ERRORS = {-1: "invalid argument", -2: "kernel launch failed", -3: "workspace too small",
            -4: "unsupported shape"}
@@ -49,7 +49,8 @@ _SIGS = {
                                           c_vp, c_vp, c_sz, c_vp, c_vp]),
     "vqhmm_elbo_bwd_adam_f32": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(c_vp), c_vp, c_vp, c_i64, c_i64,
                                                c_f32, c_vp, c_sz, c_vp, c_vp, c_vp, c_vp, ctypes.c_double,
-                                               ctypes.c_double, ctypes.c_double, ctypes.c_double, c_vp, c_f32, c_vp]),
+                                               ctypes.c_double, ctypes.c_double, ctypes.c_double, c_vp, c_f32, c_vp,
+                                               c_vp, c_vp]),
     "vqhmm_elbo_pieces": (ctypes.c_int, [ctypes.POINTER(Dims), c_i64, c_i64, c_vp, ctypes.POINTER(c_vp),
                                          ctypes.POINTER(c_vp)]),
     "vqhmm_adam_f32": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.c_double, ctypes.c_double,

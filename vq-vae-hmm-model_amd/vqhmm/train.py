@@ -169,15 +169,16 @@ class TrainState:
         ws = self.workspace(B, T)
         st = _ext.stream_ptr(self.device)
         d = ctypes.byref(self.dims)
+        # need_grad = 2: the loss is finalized in the backward's tail launch (one launch fewer)
         _ext.check(self.lib.vqhmm_elbo_fwd_f32(d, self.ptrs, _ext.ptr(x), _ext.ptr(u), lay, _ext.ptr(lengths),
-                                               _ext.ptr(norm), B, T, float(beta), 1, _ext.ptr(ws), ws.numel(),
+                                               _ext.ptr(norm), B, T, float(beta), 2, _ext.ptr(ws), ws.numel(),
                                                _ext.ptr(self.loss), _ext.ptr(self.epoch_acc), st), "elbo forward")
         b1, b2 = self.betas
         rc = self.lib.vqhmm_elbo_bwd_adam_f32(d, self.ptrs, _ext.ptr(x), _ext.ptr(norm), B, T, float(beta),
                                               _ext.ptr(ws), ws.numel(), _ext.ptr(self.grad), _ext.ptr(self.flat),
                                               _ext.ptr(self.exp_avg), _ext.ptr(self.exp_avg_sq), self.lr, b1, b2,
                                               self.eps, _ext.ptr(self.step_dev), self.grad_scale(norm is not None),
-                                              st)
+                                              _ext.ptr(self.loss), _ext.ptr(self.epoch_acc), st)
         _ext.check(rc, "elbo backward + adam")
 
     def _fused_adam_ok(self, max_norm=None):
