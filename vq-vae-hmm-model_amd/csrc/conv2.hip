@@ -442,8 +442,10 @@ __global__ __launch_bounds__((64 * C2wOcc<NB, KCP>::MAXW)) void conv2w_kernel(Co
   }
   const float sc = a.scale ? *a.scale : 1.0f;
 
+  // tile = blockIdx.x + gridDim.x * (wave + nwv * k): every workgroup (CU) gets within one tile of
+  // the same count, and inside it the extra tiles go to different waves (SIMDs)
   const int64_t stride = (int64_t)gridDim.x * nwv;
-  int64_t tile = (int64_t)blockIdx.x * nwv + wave;
+  int64_t tile = (int64_t)wave * gridDim.x + blockIdx.x;
   float4 pf[C::PF];
 #pragma unroll
   for (int k = 0; k < C::PF; ++k) {

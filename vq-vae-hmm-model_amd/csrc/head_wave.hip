@@ -263,7 +263,8 @@ __global__ __launch_bounds__(256, 2) void elbo_head_wave_kernel(HeadArgs a) {
   // windows dealt across the grid first: w = k * (4 * grid) + wave * grid + block
   const int64_t nwin = cdiv(a.R, WOWN);
   const int64_t stride = 4 * (int64_t)gridDim.x;
-  int64_t w = (int64_t)wave * gridDim.x + blockIdx.x;
+  // the slot rotates with the block so the waves that get one window more sit on different SIMDs
+  int64_t w = (int64_t)((wave + blockIdx.x) & 3) * gridDim.x + blockIdx.x;
   // (a wave sees 1-2 windows at the cfg2 sizes, so rows are loaded at the window's start —
   // phase A waits only for u — rather than prefetched a window ahead in registers)
   for (; w < nwin; w += stride) {

@@ -10,7 +10,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libvqhmm.so")
+# VQHMM_LIB_PATH: load another build of the same library (kernel A/B experiments only)
+LIB_PATH = os.environ.get("VQHMM_LIB_PATH") or os.path.join(_HERE, "libvqhmm.so")
 NPARAMS = 18
 ABI_VERSION = 5
 
