@@ -357,11 +357,12 @@ __global__ __launch_bounds__(256, (C2Occ<NB, KCP, TAIL>::W)) void conv2_kernel(C
         }
     }
     const int64_t next = tile + gridDim.x;
-    if (next < ntiles) {
+    {  // unconditional: see conv2w_kernel
+      const int64_t pt = next < ntiles ? next : tile;
 #pragma unroll
       for (int k = 0; k < C::PF; ++k) {
         const int s = tid + k * 256;
-        pf[k] = x_raw(a, next * C::BM, s < C::XF4 ? s : 0, C::KCW);
+        pf[k] = x_raw(a, pt * C::BM, s < C::XF4 ? s : 0, C::KCW);
       }
     }
     // ---- MFMA: acc[nb][pb] = Y^T block (16 n x 16 rows)
@@ -473,11 +474,14 @@ __global__ __launch_bounds__((64 * C2wOcc<NB, KCP>::MAXW)) void conv2w_kernel(Co
         auxv[nb][0] = *reinterpret_cast<const float4*>(a.aux + (r < a.R ? r : a.R - 1) * ldn + min(nb * 16 + 4 * lg4, ldn - 4));
     }
     const int64_t next = tile + stride;
-    if (next < ntiles) {
+    {  // unconditional (a past-the-end tile reads clamped rows, unused): a conditional prefetch makes
+       // the compiler's vmcnt accounting assume it may be absent, so the epilogue's wait for the aux
+       // loads would also wait for the prefetch
+      const int64_t pt = next < ntiles ? next : tile;
 #pragma unroll
       for (int k = 0; k < C::PF; ++k) {
         const int s = lane + k * 64;
-        pf[k] = x_raw(a, next * 16, s < C::XF4 ? s : 0, C::KCW);
+        pf[k] = x_raw(a, pt * 16, s < C::XF4 ? s : 0, C::KCW);
       }
     }
     f32x4 acc[NB][1];

@@ -30,8 +30,13 @@ constexpr int w2_lds_floats() { return RT * (NPAD + 4) + (RT + 2) * (CPAD + 4) +
 constexpr int W2_LDS_MAX = RT * 68 + (RT + 2) * 68 + 256 + 1536;
 
 // One chunk (workgroup) of the split-K weight gradient; smem = w2_lds_floats<NPAD, CPAD>() floats.
-template <int NBW, int CBW, int KS, int NPAD, int CPAD, int WR>
+// PK (k = 3, 3*C <= 16): the three taps share ONE 16-wide MFMA column block, column j = tap*C + c
+// (a per-lane gather from the X stage), so a narrow-input layer (enc_conv1 C = 5, the composed
+// decoder conv1 C = K = 3) issues a third of the MFMAs of the tap-major form.
+template <int NBW, int CBW, int KS, int NPAD, int CPAD, int WR, bool PK = false>
 __device__ __forceinline__ void wgrad2_body(const WgradArgs& a, int WN, int WC, int64_t chunk, float* smem) {
+  static_assert(!PK || (KS == 3 && CBW == 1), "packed taps: k = 3, one column block");
+  constexpr int KA = PK ? 1 : KS;  // accumulator tap blocks
   constexpr int LDA = NPAD + 4, LDB = CPAD + 4;  // 4*LD = 16 (mod 32): conflict-free b32 column reads
   constexpr int DY4 = RT * NPAD / 4;             // float4 slots of the dY stage
   constexpr int X4 = (RT + 2) * CPAD / 4;        // float4 slots of the X stage
@@ -84,9 +89,12 @@ __device__ __forceinline__ void wgrad2_body(const WgradArgs& a, int WN, int WC, 
     return (r >= 0 && r < a.R && c < ldc) ? v : make_float4(0.f, 0.f, 0.f, 0.f);
   };
 
-  f32x4 acc[KS][NBW][CBW];
+  // packed taps: this lane's column j = l16 -> (tap, c)
+  const int ptap = PK ? l16 / a.C : 0, pcc = PK ? l16 - (l16 / a.C) * a.C : 0;
+  const bool pvalid = PK && l16 < 3 * a.C;
+  f32x4 acc[KA][NBW][CBW];
 #pragma unroll
-  for (int tp = 0; tp < KS; ++tp)
+  for (int tp = 0; tp < KA; ++tp)
 #pragma unroll
     for (int i = 0; i < NBW; ++i)
 #pragma unroll
@@ -127,17 +135,22 @@ __device__ __forceinline__ void wgrad2_body(const WgradArgs& a, int WN, int WC, 
     // each): the operands of step s + 1 are read from LDS while the MFMAs of step s run (two
     // register sets, sched_barrier keeps the reads ahead); each accumulator's chain is unchanged
     constexpr int NST = 4 * (4 / WR);
-    float av[2][NBW], bv[2][KS][CBW];
-    auto load = [&](int st, float (&a_)[NBW], float (&b_)[KS][CBW]) {
+    float av[2][NBW], bv[2][KA][CBW];
+    auto load = [&](int st, float (&a_)[NBW], float (&b_)[KA][CBW]) {
       const int sl = wr + (st >> 2) * WR, e = st & 3;
       const int rr = sl * 16 + 4 * lg4 + e;
 #pragma unroll
       for (int i = 0; i < NBW; ++i) a_[i] = dys[rr * LDA + (wn + i * WN) * 16 + l16];
+      if constexpr (PK) {
+        const float xv = xs[(rr + ptap) * LDB + pcc];
+        b_[0][0] = pvalid ? xv : 0.f;
+      } else {
 #pragma unroll
-      for (int tp = 0; tp < KS; ++tp) {
-        const int xrow = rr + (KS == 3 ? tp : 1);
+        for (int tp = 0; tp < KS; ++tp) {
+          const int xrow = rr + (KS == 3 ? tp : 1);
 #pragma unroll
-        for (int j = 0; j < CBW; ++j) b_[tp][j] = xs[xrow * LDB + (wc + j * WC) * 16 + l16];
+          for (int j = 0; j < CBW; ++j) b_[tp][j] = xs[xrow * LDB + (wc + j * WC) * 16 + l16];
+        }
       }
     };
     if (a.pipe) {
@@ -148,7 +161,7 @@ __device__ __forceinline__ void wgrad2_body(const WgradArgs& a, int WN, int WC, 
         if (st + 1 < NST) load(st + 1, av[cb ^ 1], bv[cb ^ 1]);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int tp = 0; tp < KS; ++tp)
+        for (int tp = 0; tp < KA; ++tp)
 #pragma unroll
           for (int j = 0; j < CBW; ++j)
 #pragma unroll
@@ -160,7 +173,7 @@ __device__ __forceinline__ void wgrad2_body(const WgradArgs& a, int WN, int WC, 
       for (int st = 0; st < NST; ++st) {
         load(st, av[0], bv[0]);
 #pragma unroll
-        for (int tp = 0; tp < KS; ++tp)
+        for (int tp = 0; tp < KA; ++tp)
 #pragma unroll
           for (int j = 0; j < CBW; ++j)
 #pragma unroll
@@ -174,20 +187,20 @@ __device__ __forceinline__ void wgrad2_body(const WgradArgs& a, int WN, int WC, 
     __syncthreads();
     if (wr == w) {
 #pragma unroll
-      for (int tp = 0; tp < KS; ++tp)
+      for (int tp = 0; tp < KA; ++tp)
 #pragma unroll
         for (int i = 0; i < NBW; ++i)
 #pragma unroll
           for (int j = 0; j < CBW; ++j)
 #pragma unroll
             for (int v = 0; v < 4; ++v)
-              xch[(wave / WR) * (KS * NBW * CBW * 4 * 64) + (((tp * NBW + i) * CBW + j) * 4 + v) * 64 + lane] =
+              xch[(wave / WR) * (KA * NBW * CBW * 4 * 64) + (((tp * NBW + i) * CBW + j) * 4 + v) * 64 + lane] =
                   acc[tp][i][j][v];
     }
     __syncthreads();
     if (wr == 0) {
 #pragma unroll
-      for (int tp = 0; tp < KS; ++tp)
+      for (int tp = 0; tp < KA; ++tp)
 #pragma unroll
         for (int i = 0; i < NBW; ++i)
 #pragma unroll
@@ -195,13 +208,13 @@ __device__ __forceinline__ void wgrad2_body(const WgradArgs& a, int WN, int WC, 
 #pragma unroll
             for (int v = 0; v < 4; ++v)
               acc[tp][i][j][v] +=
-                  xch[(wave / WR) * (KS * NBW * CBW * 4 * 64) + (((tp * NBW + i) * CBW + j) * 4 + v) * 64 + lane];
+                  xch[(wave / WR) * (KA * NBW * CBW * 4 * 64) + (((tp * NBW + i) * CBW + j) * 4 + v) * 64 + lane];
     }
   }
   if (wr == 0) {
     float* out = a.slab + chunk * (int64_t)a.N * a.C * KS;
 #pragma unroll
-    for (int tp = 0; tp < KS; ++tp)
+    for (int tp = 0; tp < KA; ++tp)
 #pragma unroll
       for (int i = 0; i < NBW; ++i)
 #pragma unroll
@@ -210,7 +223,11 @@ __device__ __forceinline__ void wgrad2_body(const WgradArgs& a, int WN, int WC, 
           for (int v = 0; v < 4; ++v) {
             const int n = (wn + i * WN) * 16 + 4 * lg4 + v;
             const int c = (wc + j * WC) * 16 + l16;
-            if (n < a.N && c < a.C) out[((int64_t)n * a.C + c) * KS + tp] = acc[tp][i][j][v];
+            if constexpr (PK) {
+              if (n < a.N && pvalid) out[((int64_t)n * a.C + pcc) * KS + ptap] = acc[tp][i][j][v];
+            } else {
+              if (n < a.N && c < a.C) out[((int64_t)n * a.C + c) * KS + tp] = acc[tp][i][j][v];
+            }
           }
   }
   if (a.bias_slab) {
@@ -256,10 +273,20 @@ __global__ __launch_bounds__(256) void wgrad2_group_kernel(WgradGroup g) {
   switch (g.variant[j]) {
     VQHMM_W2_VARIANTS(1, 0)
     VQHMM_W2_VARIANTS(3, 10)
+    case 20: wgrad2_body<1, 1, 3, 64, 16, 1, true>(a, WN, WC, ch, sm); break;
     default: break;
   }
 }
 #undef VQHMM_W2_VARIANTS
+
+// A/B switch: VQHMM_WGRAD_PACK=0 keeps the tap-major form for narrow inputs (read once)
+static bool packed_taps() {
+  static const bool v = [] {
+    const char* e = getenv("VQHMM_WGRAD_PACK");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
 
 // launch shape of a job: variant id (see above) and its wave split (WN, WC); -1 if none
 static int w2_variant(int N, int C, int ks, int* WN, int* WC) {
@@ -276,6 +303,7 @@ static int w2_variant(int N, int C, int ks, int* WN, int* WC) {
   else if (nbn == 1 && nbc == 1) { v = 8; *WN = 1; *WC = 1; }
   else if (nbn <= 4 && nbc <= 4) { v = 0; *WN = 1; *WC = 4; }
   else return -1;
+  if (ks == 3 && nbn == 4 && 3 * C <= 16 && packed_taps()) return 20;  // taps packed into one block
   return v + (ks == 3 ? 10 : 0);
 }
 
