@@ -13,9 +13,13 @@ import sys
 
 # (bench.py section, stage / kernel key) -> substring of the profiled kernel name
 MAP = {
-    ("cfg2", "elbo_head"): "elbo_head_mfma_kernel<3, 8, 8>",
+    ("cfg2", "elbo_head"): "elbo_head_wave_kernel<3, 8, 8, 4>",
     ("cfg2", "inputs_to_pcl+compose_fwd"): "prologue_kernel",
-    ("cfg2", "reduce_slabs"): "reduce_slabs_kernel",
+    ("cfg2", "grad_tail(reduce_slabs+log_prior_grad)"): "grad_tail_kernel",
+    ("cfg2", "wgrad_group(all 6 weight gradients)"): "wgrad2_group_kernel",
+    ("cfg2", "dec_conv2+to_params"): "conv2w_kernel<4, 4, 3, 1, true>",
+    ("cfg2", "dec_conv2_dgrad"): "conv2w_kernel<4, 4, 3, 2, false>",
+    ("cfg2", "compose_bwd[+adam]"): "compose_adam_kernel",
     ("vq_cfg3", "vq_argmin"): "vq_rows_kernel<16, 2, false",
     ("viterbi_cfg5", "viterbi_cfg5"): "viterbi_kernel<8, true>",
     ("fwdbwd_cfg4", "fwdbwd_cfg4"): "fwdbwd_kernel<8, true>",
