@@ -244,3 +244,27 @@ def test_infer_and_hard_regimes():
     u = torch.tensor(g["u"]).cuda()
     path, score = vqhmm.viterbi_regimes(m, x.cuda(), u)
     assert path.shape == x[:, 0].shape and (path >= 0).all() and (path < q.shape[1]).all()
+
+
+@pytest.mark.parametrize("K,TH,U,B,T,layout", [(3, 128, 4, 5, 37, 0), (8, 128, 4, 3, 101, 1), (8, 64, 3, 2, 50, 0),
+                                               (4, 256, 4, 2, 29, 1), (2, 128, 1, 1, 7, 0)])
+def test_prior_mfma_vs_torch(K, TH, U, B, T, layout):
+    """Prior.forward on MFMA (csrc/prior.hip) against the same MLP in torch fp32 on the CPU
+    (VQ_VAE_HMM_fixed.py:59-71): position counts that are not multiples of the 16-position tile,
+    both u layouts (:64-65), K*K from 4 to 64, TH 64 / 128 / 256."""
+    import vqhmm
+    torch.manual_seed(K * 100 + TH + U)
+    m = vqhmm.VAE_HMM(5, 32, K, 16, u_dim=U, trans_hidden=TH)
+    u = torch.randn(B, U, T)
+    if layout == 1:
+        u = u.transpose(1, 2).contiguous()
+    with torch.no_grad():
+        log_pi, log_A = m.cuda().prior(u.cuda())
+    pr = m.prior.cpu()
+    uu = u if layout == 1 else u.permute(0, 2, 1)
+    with torch.no_grad():
+        z = pr.transition_net(uu.reshape(-1, U)).reshape(B, T, K, K)
+        ref = torch.log_softmax(z, dim=-1)
+        ref_pi = torch.log_softmax(pr.log_prior, dim=0)
+    assert_close(log_A.cpu(), ref, 1e-5, "log_A", atol=1e-6)
+    assert_close(log_pi.cpu(), ref_pi, 1e-6, "log_pi", atol=1e-7)

@@ -459,6 +459,7 @@ __global__ __launch_bounds__(256) void prior_fwd_wave_kernel(PriorArgs p) {
 int launch_prior_fwd(const PriorArgs& p, hipStream_t s) {
   const int64_t N = p.B * p.T;
   if (N == 0) return VQHMM_OK;
+  if (prior_mfma_supported(p) && (p.TH == 64 || p.TH == 128 || p.TH == 256)) return launch_prior_mfma(p, s);
   if (p.K <= 8 && p.U <= 8) {
     const dim3 grid((unsigned)cdiv(N, 256));
     if (p.K <= 4)

@@ -240,6 +240,9 @@ bool head_mfma_supported(const HeadArgs& a);
 int launch_head_mfma(const HeadArgs& a, int grid, hipStream_t s);
 int launch_head(const HeadArgs& a, int grid, hipStream_t s);
 int launch_prior_fwd(const PriorArgs& p, hipStream_t s);
+// Prior.forward on MFMA (prior.hip): K*K <= 64, U <= 4, TH in {64, 128, 256}
+bool prior_mfma_supported(const PriorArgs& p);
+int launch_prior_mfma(const PriorArgs& p, hipStream_t s);
 // Backward tail (misc.hip grad_tail_kernel), ONE launch: every gradient segment's slabs summed in a
 // fixed chunk order (deterministic, no atomics) and scaled; one extra workgroup reduces the q0 slab
 // and writes the log_prior gradient.
