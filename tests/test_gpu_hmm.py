@@ -71,9 +71,23 @@ def test_viterbi_cfg5_long_sequence():
     assert np.array_equal(score.cpu().numpy(), rs)
 
 
+# K <= 8 forward-backward has two kernels: the LDS-resident one (whenever its table fits and one
+# round of workgroups covers the batch) and the streaming one (VQHMM_FB_RES=0, read per call)
+FB_KERNELS = ["resident", "streaming"]
+
+
+def use_fb_kernel(monkeypatch, kernel):
+    if kernel == "streaming":
+        monkeypatch.setenv("VQHMM_FB_RES", "0")
+    else:
+        monkeypatch.delenv("VQHMM_FB_RES", raising=False)
+
+
+@pytest.mark.parametrize("kernel", FB_KERNELS)
 @pytest.mark.parametrize("K,B,T", CASES)
-def test_forward_backward_vs_fp64(K, B, T):
+def test_forward_backward_vs_fp64(K, B, T, kernel, monkeypatch):
     import vqhmm
+    use_fb_kernel(monkeypatch, kernel)
     log_pi, log_A, em = random_hmm(K * 11 + B, B, T, K)
     rng = np.random.default_rng(K + 1)
     L = rng.integers(0, T + 1, B).astype(np.int64)
@@ -100,13 +114,15 @@ def test_forward_backward_long_T_precision():
     assert np.all(np.abs(logZ.cpu().numpy() - rz) <= 1e-5 * np.abs(rz))
 
 
+@pytest.mark.parametrize("kernel", FB_KERNELS)
 @pytest.mark.parametrize("K", [3, 8, 13, 32])
-def test_forward_backward_extreme_tables(K):
+def test_forward_backward_extreme_tables(K, kernel, monkeypatch):
     """Tables that push the fast base-2 step out of range, so chunks take the exact
     max-shifted recomputation: left-to-right transitions (log 0 = -inf), emissions of
     about -1e3 nats, a window with hundreds of nats of emission spread, and
     near-deterministic transitions.  Same 1e-5 contract vs the fp64 oracle."""
     import vqhmm
+    use_fb_kernel(monkeypatch, kernel)
     B, T = 6, 150
     rng = np.random.default_rng(K + 100)
     log_pi, log_A, em = random_hmm(K + 200, B, T, K)
@@ -127,6 +143,44 @@ def test_forward_backward_extreme_tables(K):
     assert np.abs(gamma.cpu().numpy() - rg).max() <= 1e-5
     z = logZ.cpu().numpy()
     assert np.all(np.abs(z - rz) <= 1e-5 * np.maximum(1.0, np.abs(rz)))
+
+
+@pytest.mark.parametrize("kernel", FB_KERNELS)
+@pytest.mark.parametrize("K,spread", [(8, 10.0), (8, 35.0), (8, 90.0), (4, 35.0), (3, 90.0)])
+def test_forward_backward_tier_fallbacks(K, spread, kernel, monkeypatch):
+    """Emission spreads that keep the linear tier in range (10), push some states below
+    2^-96 so chunks fall back to the base-2 log tier (35), or beyond its range too (90),
+    mixed per sequence and per window, at T = 512 (16 chunks per wave)."""
+    import vqhmm
+    use_fb_kernel(monkeypatch, kernel)
+    B, T = 5, 512
+    log_pi, log_A, em = random_hmm(K * 3 + int(spread), B, T, K)
+    em = em.astype(np.float64)
+    em[1] *= spread
+    em[2, 100:140] *= spread
+    em[3, 300:] *= spread
+    em = em.astype(np.float32)
+    L = np.array([T, T, T, 400, 1], np.int64)
+    gamma, logZ = vqhmm.forward_backward(*gpu(log_pi, log_A, em), torch.from_numpy(L))
+    rg, rz = hmm_ref.forward_backward_f64(log_pi, log_A, em, L)
+    assert np.abs(gamma.cpu().numpy() - rg).max() <= 1e-5
+    assert np.all(np.abs(logZ.cpu().numpy() - rz) <= 1e-5 * np.maximum(1.0, np.abs(rz)))
+
+
+@pytest.mark.parametrize("K,B,T", [(8, 300, 64), (4, 1100, 40), (8, 2, 560), (2, 3, 1000)])
+def test_forward_backward_resident_boundaries(K, B, T):
+    """Shapes at the resident kernel's limits: several workgroups per CU (small T), batches
+    near one round, and T past the LDS table (streaming kernel)."""
+    import vqhmm
+    log_pi, log_A, em = random_hmm(K * 13 + B + T, B, T, K)
+    L = np.random.default_rng(T).integers(0, T + 1, B).astype(np.int64)
+    L[0] = T
+    gamma, logZ = vqhmm.forward_backward(*gpu(log_pi, log_A, em), torch.from_numpy(L))
+    rg, rz = hmm_ref.forward_backward_f64(log_pi, log_A, em, L)
+    assert np.abs(gamma.cpu().numpy() - rg).max() <= 1e-5
+    live = L > 0
+    z = logZ.cpu().numpy()
+    assert np.all(np.abs(z[live] - rz[live]) <= 1e-5 * np.maximum(1.0, np.abs(rz[live])))
 
 
 def test_gamma_sums_to_one_and_viterbi_on_model_tables():

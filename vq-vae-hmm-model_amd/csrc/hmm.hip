@@ -100,6 +100,13 @@ constexpr int DPP_HALF_MIRROR = 0x141;  // l -> 7 - l within 8 lanes
 constexpr int DPP_ROR4 = 0x124;         // row_ror:4 (16-lane rows)
 constexpr int DPP_ROR8 = 0x128;         // row_ror:8
 
+struct OpMax {
+  __device__ float operator()(float a, float b) const { return fmaxf(a, b); }
+};
+struct OpAdd {
+  __device__ float operator()(float a, float b) const { return a + b; }
+};
+
 // all-reduce over the KP lanes of one axis of a sequence's lane group:
 // INNER = lanes g % KP (stride 1), else lanes g / KP (stride KP)
 template <int KP, bool INNER, typename Op>
@@ -129,12 +136,6 @@ __device__ __forceinline__ float allred(float v, Op op) {
   }
   return v;
 }
-struct OpMax {
-  __device__ float operator()(float a, float b) const { return fmaxf(a, b); }
-};
-struct OpAdd {
-  __device__ float operator()(float a, float b) const { return a + b; }
-};
 
 // first arg-max over one axis (lowest index wins ties); one-time use, shuffles are fine
 template <int KP, bool INNER>
@@ -510,15 +511,46 @@ int launch_viterbi(const float* log_pi, const float* log_A, const float* em, con
 // may have dropped a significant term, or an all -inf column) is recomputed
 // from its saved start state with the max-shifted log-sum-exp, normalised
 // every step — same contract, rare path.
+//
+// Linear tier (tried first on every chunk).  Inside a chunk the recursions run on
+// x = 2^(al - frame) with the per-step table m(i, j) = 2^((lg A(i,j) + lg e(j)) lg e)
+// precomputed off the chain, so a step is one multiply and the add-reduction:
+//   alpha: x_t(j) = sum_i x_{t-1}(i) m_t(i, j),   beta: x_t(i) = sum_j m_{t+1}(i, j) x_{t+1}(j)
+// Every FB_LNORM-th step rescales by 2^-k, k = the exponent of the running max (exact, a
+// power of two; its max-reduction runs beside the chain's add-reduction).  The chunk starts
+// from the log-domain state (x = 2^(al - max al)) and ends by converting back (al = lg x), so
+// chunk boundaries keep the log-domain range.  A chunk in which some live entry leaves
+// [2^-FB_LIM, 2^FB_LIM] (nothing below 2^-126 can then have carried weight) falls back to the
+// log tier above from the saved start state.  The per-step stores are lg x: a per-step
+// constant offset, which gamma's softmax over the states cancels.
 // Workspace: al [B][T][K], then be' [B][T][K] with be'[t+1] = be_t (base 2).
 constexpr float F32_LOWEST = -3.402823466e38f;
 constexpr float LOG2E_F = 1.44269504088896341f;
 constexpr double LN2_D = 0.69314718055994531;
 constexpr float FB_LIM = 96.f;  // fast-step column sums must stay within 2^(+-FB_LIM)
 constexpr int FB_NORM = 4;      // fast steps renormalise by the running max every FB_NORM steps
+constexpr int FB_LNORM = 8;     // the linear tier rescales every FB_LNORM steps (and at each chunk start)
 
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 __device__ __forceinline__ float flog2(float x) { return __builtin_amdgcn_logf(x); }
+
+// the linear tier's per-step table of a staged chunk (alpha: step s has the parity of t = s;
+// beta: data step s serves t = s - 1)
+template <int K, bool W16, bool BETA>
+__device__ __forceinline__ void read_lin_chunk(const float* sl, const LaneMap<K, W16>& lm, float* ml) {
+  using Gm = Geo<K, W16>;
+  constexpr int HC = Gm::HC;
+#pragma unroll
+  for (int s = 0; s < HC; ++s) {
+    const int p = (s + (BETA ? 1 : 0)) & 1;
+    const float a = lm.a_ok[p] ? sl[lm.a_off[p] + s * K * K] : NEG_INF;
+    const float e = lm.e_ok[p] ? sl[lm.e_off[p] + s * K] : 0.f;
+    ml[s] = fexp2((a + e) * LOG2E_F);
+  }
+}
+
+// out-of-range test of the linear tier's live entries
+__device__ __forceinline__ bool lin_bad(float lo, float hi) { return !(lo >= 0x1p-96f) || !(hi <= 0x1p96f); }
 
 template <int N>
 __device__ __forceinline__ float tree_sum(const float* v) {  // pairwise (fixed order)
@@ -564,7 +596,7 @@ __global__ __launch_bounds__(128) void fwdbwd_kernel(const float* __restrict__ l
                                                      const float* __restrict__ log_A, const float* __restrict__ em,
                                                      const int64_t* __restrict__ lengths, int64_t B, int T,
                                                      float* __restrict__ gamma, float* __restrict__ logZ,
-                                                     float* __restrict__ ws) {
+                                                     float* __restrict__ ws, int lin_tier) {
   using Gm = Geo<K, W16>;
   using Rg = Ring<K, W16>;
   constexpr int KP = Gm::KP, G = Gm::G, SPW = Gm::SPW, R = Rg::R, HC = Gm::HC;
@@ -601,7 +633,7 @@ __global__ __launch_bounds__(128) void fwdbwd_kernel(const float* __restrict__ l
   // flush vbuf -> dst rows [t0, t0 + HC) of the wave's sequences (t < T only).
   // Every lane of a group stores its step value unmasked (lanes sharing a
   // state write the same word); the wave's LDS ops retire in order.
-  auto flush = [&](float* dst, int t0) {
+  auto flush = [&](float* dst, int t0, bool linear) {
     asm volatile("" ::: "memory");
     constexpr int NF = (VB + 63) / 64;
 #pragma unroll
@@ -609,14 +641,15 @@ __global__ __launch_bounds__(128) void fwdbwd_kernel(const float* __restrict__ l
       const int idx = k * 64 + lane;
       if (VB % 64 == 0 || idx < VB) {
         const int q = idx / (HC * KP), r = idx - q * (HC * KP), s = r / KP, j = r - s * KP;
-        const float v = vbuf[idx];
+        const float v = linear ? flog2(vbuf[idx]) : vbuf[idx];
         if (j < K && b0 + q < B && t0 + s < T) dst[((b0 + q) * (int64_t)T + t0 + s) * K + j] = v;
       }
     }
     asm volatile("" ::: "memory");
   };
-  float av[HC], dv[HC], xv[HC], mv[HC];
+  float av[HC], dv[HC], xv[HC], mv[HC], ml[HC];
   float rng = 0.f;  // max |lg column sum| over the chunk's live fast steps
+  float x = 0.f, lo = 1.f, hi = 1.f;  // linear tier: chain value, range of the live entries
 
   if (wave == 0) {
     // ------------------------------------------------------------ alpha
@@ -660,25 +693,82 @@ __global__ __launch_bounds__(128) void fwdbwd_kernel(const float* __restrict__ l
         vrow[s * KP + (p == 0 ? jo : ji)] = al;  // state j = the lane's j-coordinate
       });
     };
+    // linear tier (see above); sk = the chunk's frame shifts (base 2)
+    float sk = 0.f;
+    auto lin_steps = [&](int t0, bool first, float e0, auto check) {
+      constexpr bool CHECK = decltype(check)::value;
+      static_for<HC>([&](auto si) {
+        constexpr int s = decltype(si)::value, p = s & 1;
+        if (s == 0 && first) {  // x_0 on the inner axis from al_0 = lg pi + lg e_0
+          const float a0 = (L > 0 && jo < K) ? lp2 + e0 : NEG_INF;
+          const float m0 = allred<KP, true>(a0, OpMax{});
+          const float m0s = m0 == NEG_INF ? 0.f : m0;
+          x = fexp2(a0 - m0s);
+          sk = m0s;
+          if (L > 0 && jo < K) lo = fminf(lo, x);
+          vrow[jo] = x;
+          return;
+        }
+        const bool upd = !CHECK || t0 + s < L;
+        const float v = x * ml[s];
+        int k = 0;
+        if constexpr (s % FB_LNORM == FB_LNORM / 2) k = __builtin_amdgcn_frexp_expf(allred<KP, p == 1>(x, OpMax{}));
+        float y = allred<KP, p == 1>(v, OpAdd{});
+        if constexpr (s % FB_LNORM == FB_LNORM / 2) y = __builtin_amdgcn_ldexpf(y, -k);
+        const bool chk = upd && lm.e_ok[p];
+        lo = chk ? fminf(lo, y) : lo;
+        hi = chk ? fmaxf(hi, y) : hi;
+        if (upd) {
+          x = y;
+          sk += (float)k;
+        }
+        vrow[s * KP + (p == 0 ? jo : ji)] = x;
+      });
+    };
     for (int c = 0; c < nchunks; ++c) {
       stage_chunk<K, W16>(log_A, em, b0, B, T, min(c + R - 1, nchunks - 1), ring + ((c + R - 1) % R) * Gm::SLOT,
                           lane);
       wait_vm<Rg::WAIT>();
-      read_fb_chunk<K, W16, false>(ring + (c % R) * Gm::SLOT, lm, av, dv, xv);
+      const float* sl = ring + (c % R) * Gm::SLOT;
       const int t0 = c * HC;
       const float al_c = al;
-      rng = 0.f;
-      if (t0 + HC <= Lmin) steps(t0, c == 0, std::false_type{}, std::false_type{});
-      else steps(t0, c == 0, std::false_type{}, std::true_type{});
-      if (__builtin_amdgcn_ballot_w64(rng > FB_LIM)) {  // rare: recompute the chunk exactly
-        al = al_c;
-        steps(t0, c == 0, std::true_type{}, std::true_type{});
+      bool linear = false;
+      if (lin_tier) {
+        read_lin_chunk<K, W16, false>(sl, lm, ml);
+        const float e0 = c == 0 && lm.e_ok[0] ? sl[lm.e_off[0]] * LOG2E_F : NEG_INF;
+        lo = hi = 1.f;
+        if (c > 0) {  // state of step t0 - 1 (odd: outer axis) -> its frame
+          const float m = allred<KP, false>(al, OpMax{});
+          const float ms = m == NEG_INF ? 0.f : m;
+          x = fexp2(al - ms);
+          sk = ms;
+          if (t0 < L && ji < K) lo = fminf(lo, x);
+        }
+        if (t0 + HC <= Lmin) lin_steps(t0, c == 0, e0, std::false_type{});
+        else lin_steps(t0, c == 0, e0, std::true_type{});
+        linear = !__builtin_amdgcn_ballot_w64(lin_bad(lo, hi));
       }
+      if (linear) {
+        if (t0 < L) {  // (a sequence that ended before the chunk keeps its state; its axis is not the outer one)
+          al = flog2(x);
+          S2 += (double)sk;
+        }
+      } else {
+        read_fb_chunk<K, W16, false>(sl, lm, av, dv, xv);
+        al = al_c;
+        rng = 0.f;
+        if (t0 + HC <= Lmin) steps(t0, c == 0, std::false_type{}, std::false_type{});
+        else steps(t0, c == 0, std::false_type{}, std::true_type{});
+        if (__builtin_amdgcn_ballot_w64(rng > FB_LIM)) {  // rare: recompute the chunk exactly
+          al = al_c;
+          steps(t0, c == 0, std::true_type{}, std::true_type{});
+        }
 #pragma unroll
-      for (int s = 0; s < HC; ++s) xv[s] = t0 + s < L ? xv[s] : 0.f;
-      S2 += (double)tree_sum<HC>(mv);
-      SE += (double)tree_sum<HC>(xv);
-      flush(ws_al, t0);
+        for (int s = 0; s < HC; ++s) xv[s] = t0 + s < L ? xv[s] : 0.f;
+        S2 += (double)tree_sum<HC>(mv);
+        SE += (double)tree_sum<HC>(xv);
+      }
+      flush(ws_al, t0, linear);
     }
     // logZ from the state axis held after step L-1 (even t: inner)
     const int tl = L - 1;
@@ -727,21 +817,57 @@ __global__ __launch_bounds__(128) void fwdbwd_kernel(const float* __restrict__ l
         vrow[s * KP + (p == 0 ? ji : jo)] = be;  // state i = the lane's i-coordinate; slot s <-> be'[t + 1]
       });
     };
+    auto lin_steps = [&](int d0, bool last, auto check) {
+      constexpr bool CHECK = decltype(check)::value;
+      static_for<HC>([&](auto si) {
+        constexpr int s = HC - 1 - decltype(si)::value, p = (s + 1) & 1;  // p = parity of t
+        if (s == 0 && last) return;                                       // t = -1
+        const bool upd = !CHECK || d0 + s - 1 < L - 1;
+        const float v = ml[s] * x;
+        int kx = 0;
+        if constexpr (s % FB_LNORM == FB_LNORM / 2) kx = __builtin_amdgcn_frexp_expf(allred<KP, p == 0>(x, OpMax{}));
+        float y = allred<KP, p == 0>(v, OpAdd{});
+        if constexpr (s % FB_LNORM == FB_LNORM / 2) y = __builtin_amdgcn_ldexpf(y, -kx);
+        const bool chk = upd && lm.e_ok[p ^ 1];
+        lo = chk ? fminf(lo, y) : lo;
+        hi = chk ? fmaxf(hi, y) : hi;
+        if (upd) x = y;
+        vrow[s * KP + (p == 0 ? ji : jo)] = x;
+      });
+    };
     for (int c = 0; c < nchunks; ++c) {
       const int k = nchunks - 1 - c;
       stage_chunk<K, W16>(log_A, em, b0, B, T, max(k - (R - 1), 0), ring + ((c + R - 1) % R) * Gm::SLOT, lane);
       wait_vm<Rg::WAIT>();
-      read_fb_chunk<K, W16, true>(ring + (c % R) * Gm::SLOT, lm, av, dv, xv);
+      const float* sl = ring + (c % R) * Gm::SLOT;
       const int d0 = k * HC;
       const float be_c = be;
-      rng = 0.f;
-      if (d0 + HC <= Lmin) steps(d0, k == 0, std::false_type{}, std::false_type{});
-      else steps(d0, k == 0, std::false_type{}, std::true_type{});
-      if (__builtin_amdgcn_ballot_w64(rng > FB_LIM)) {
-        be = be_c;
-        steps(d0, k == 0, std::true_type{}, std::true_type{});
+      bool linear = false;
+      if (lin_tier) {
+        read_lin_chunk<K, W16, true>(sl, lm, ml);
+        // state of data step d0 + HC (even t = d0 + HC - 1 ... held on the inner axis) -> its frame
+        const float m = allred<KP, true>(be, OpMax{});
+        x = fexp2(be - (m == NEG_INF ? 0.f : m));
+        lo = hi = 1.f;
+        if (d0 + HC - 1 < L - 1 && jo < K) lo = fminf(lo, x);
+        if (d0 + HC <= Lmin) lin_steps(d0, k == 0, std::false_type{});
+        else lin_steps(d0, k == 0, std::true_type{});
+        linear = !__builtin_amdgcn_ballot_w64(lin_bad(lo, hi));
       }
-      flush(ws_be, d0);
+      if (linear) {
+        be = flog2(x);
+      } else {
+        read_fb_chunk<K, W16, true>(sl, lm, av, dv, xv);
+        be = be_c;
+        rng = 0.f;
+        if (d0 + HC <= Lmin) steps(d0, k == 0, std::false_type{}, std::false_type{});
+        else steps(d0, k == 0, std::false_type{}, std::true_type{});
+        if (__builtin_amdgcn_ballot_w64(rng > FB_LIM)) {
+          be = be_c;
+          steps(d0, k == 0, std::true_type{}, std::true_type{});
+        }
+      }
+      flush(ws_be, d0, linear);
     }
   }
 
@@ -780,11 +906,527 @@ __global__ __launch_bounds__(128) void fwdbwd_kernel(const float* __restrict__ l
   }
 }
 
+static int fb_lin_tier();
+
 template <int K, bool W16>
 static void fwdbwd_go(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths, int64_t B,
                       int64_t T, float* gamma, float* logZ, float* ws, hipStream_t s) {
   const dim3 grid((unsigned)cdiv(B, Geo<K, W16>::SPW));
-  fwdbwd_kernel<K, W16><<<grid, 128, 0, s>>>(log_pi, log_A, em, lengths, B, (int)T, gamma, logZ, ws);
+  fwdbwd_kernel<K, W16><<<grid, 128, 0, s>>>(log_pi, log_A, em, lengths, B, (int)T, gamma, logZ, ws, fb_lin_tier());
+}
+
+// ------------------------------------------------- forward-backward, LDS-resident table
+// For T up to ~550 the whole per-step table of a workgroup's SPW sequences fits in LDS, so
+// HBM is read once: log_A and em are linearised once into m(i, j) = 2^((lg A + lg e) lg e)
+// (the linear tier's table) and BOTH chains run on it, alpha upward and beta downward.
+// Beta uses alpha's lane map at each data step d (map parity = d's parity; it reduces over
+// the j axis, alpha over the i axis — both chains then alternate axes consistently), so one
+// lane-major table [T/4][64 lanes][4 steps] serves both with one ds_read_b128 per 4 steps.
+//
+// One workgroup = 4 waves on SPW sequences, one per SIMD:
+//   wave 0  alpha chain        wave 2  linearises chunks 0 .. hF-1 (upward), flushes alpha
+//   wave 1  beta chain         wave 3  linearises chunks nch-1 .. hF (downward), flushes beta
+// Iteration it (one LDS barrier each): alpha runs chunk it, beta data chunk nch-1-it; the
+// helpers linearise the chunks the chains take next (global loads issued one iteration
+// ahead) and flush what the chains produced in iteration it-1.  A chain value is stored for
+// the other direction (LDS history) and gamma_t = softmax(al_t + be_t) is formed by whichever
+// flush comes second: alpha's flush of t when be'[t+1] is already flushed (t/HC + (t+1)/HC >=
+// nch), beta's flush when al_t is (t/HC + (t+1)/HC <= nch - 2); the few t between (= nch - 1)
+// after the loop.  No workspace traffic: HBM sees log_A + em once and gamma once.
+// The chains run the linear tier, with the log-tier / exact fallbacks reading the raw tables
+// straight from global memory (rare path).
+namespace {
+constexpr int FR_HC = 16;  // steps per chunk of the resident kernel
+
+template <int K>
+struct FbRes {
+  using Gm = Geo<K, false>;
+  static constexpr int KP = Gm::KP, G = Gm::G, SPW = Gm::SPW, HC = FR_HC;
+  static constexpr int VB = SPW * HC * KP;  // one chunk of chain values [SPW][HC][KP]
+  static_assert(VB % 64 == 0, "flush covers whole wave passes");
+  // LDS floats for a given T: table, two histories [SPW][HH][KP], vbuf [dir][2][VB], 4 flags
+  __host__ __device__ static int hh(int T) { return ((T + HC - 1) / HC / 2 + 1) * HC; }
+  static size_t lds_bytes(int T) {
+    const size_t tp = (size_t)cdiv(T, HC) * HC;
+    return (tp * 64 + 2 * (size_t)SPW * hh(T) * KP + 4 * (size_t)VB + 4) * sizeof(float);
+  }
+};
+}  // namespace
+
+template <int K>
+__global__ __launch_bounds__(256) void fwdbwd_resident_kernel(const float* __restrict__ log_pi,
+                                                              const float* __restrict__ log_A,
+                                                              const float* __restrict__ em,
+                                                              const int64_t* __restrict__ lengths, int64_t B, int T,
+                                                              float* __restrict__ gamma, float* __restrict__ logZ,
+                                                              int lin_tier, unsigned long long* __restrict__ prof) {
+  using F = FbRes<K>;
+  constexpr int KP = F::KP, G = F::G, SPW = F::SPW, HC = F::HC, VB = F::VB;
+  extern __shared__ float4 smem_fr[];
+  float* Mt = reinterpret_cast<float*>(smem_fr);
+  const int nchT = (int)cdiv(T, HC), HH = F::hh(T);
+  float* hist_a = Mt + (size_t)nchT * HC * 64;  // al_t at [q][t][state]
+  float* hist_b = hist_a + SPW * HH * KP;       // be'[d] at [q][d - dbase][state]
+  float* vb = hist_b + SPW * HH * KP;           // [dir][buf][VB]
+  int* flags = reinterpret_cast<int*>(vb + 4 * VB);
+
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, grp = lane / G, g = lane % G;
+  const int64_t b0 = (int64_t)blockIdx.x * SPW;
+  const int64_t b = b0 + grp;
+  const bool live = b < B;
+  const int64_t Lr = live ? lengths[b] : 0;
+  const int L = (int)(Lr <= 0 ? 0 : (Lr < T ? Lr : T));
+  int Lmax = L;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) Lmax = max(Lmax, __shfl_xor(Lmax, o));
+  Lmax = __builtin_amdgcn_readfirstlane(Lmax);
+  const int nch = (int)cdiv(Lmax, HC), hF = (nch + 1) / 2;
+  const int dbase = ((nch - 1) / 2) * HC;  // first data step kept in hist_b
+  const int jo = g % KP, ji = g / KP;
+  // lane map per parity p of the data step: p = 0: (i, j) = (ji, jo); p = 1: (jo, ji)
+  int aoff[2], ej[2];
+  bool aok[2], eok[2], iok[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int i = p == 0 ? ji : jo, j = p == 0 ? jo : ji;
+    aok[p] = i < K && j < K;
+    eok[p] = j < K;
+    iok[p] = i < K;
+    aoff[p] = aok[p] ? i * K + j : 0;
+    ej[p] = eok[p] ? j : 0;
+  }
+  const int64_t bc = live ? b : B - 1;  // dead groups read a valid sequence, never use it
+  const float* Ab = log_A + bc * (int64_t)T * K * K;
+  const float* Eb = em + bc * (int64_t)T * K;
+
+  // ---- helpers: raw loads of a chunk into registers, then m = 2^((a + e) lg e) into the table
+  float ra[HC], re[HC];
+  auto load_raw = [&](int c) {
+    if (c * HC + HC <= T) {  // whole chunk: one base per parity, immediate offsets
+      const float* pa[2] = {Ab + (int64_t)c * HC * K * K + aoff[0], Ab + (int64_t)c * HC * K * K + aoff[1]};
+      const float* pe[2] = {Eb + (int64_t)c * HC * K + ej[0], Eb + (int64_t)c * HC * K + ej[1]};
+#pragma unroll
+      for (int s = 0; s < HC; ++s) {
+        const int p = s & 1;
+        ra[s] = aok[p] ? pa[p][s * K * K] : NEG_INF;
+        re[s] = eok[p] ? pe[p][s * K] : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < HC; ++s) {
+        const int p = s & 1;
+        const int t = min(c * HC + s, T - 1);
+        ra[s] = aok[p] ? Ab[(int64_t)t * K * K + aoff[p]] : NEG_INF;
+        re[s] = eok[p] ? Eb[(int64_t)t * K + ej[p]] : 0.f;
+      }
+    }
+  };
+  auto linearise = [&](int c) {
+#pragma unroll
+    for (int q = 0; q < HC / 4; ++q) {
+      float4 m;
+      m.x = fexp2((ra[4 * q] + re[4 * q]) * LOG2E_F);
+      m.y = fexp2((ra[4 * q + 1] + re[4 * q + 1]) * LOG2E_F);
+      m.z = fexp2((ra[4 * q + 2] + re[4 * q + 2]) * LOG2E_F);
+      m.w = fexp2((ra[4 * q + 3] + re[4 * q + 3]) * LOG2E_F);
+      *reinterpret_cast<float4*>(&Mt[((size_t)(c * (HC / 4) + q) * 64 + lane) * 4]) = m;
+    }
+  };
+  // raw log-domain values of a chunk for the fallback tiers (emx = max_j e, off the chain)
+  float av[HC], dv[HC], xv[HC], mv[HC], ml[HC];
+  auto read_raw = [&](int c, bool beta) {
+#pragma unroll
+    for (int s = 0; s < HC; ++s) {
+      const int p = s & 1;
+      const int t = min(c * HC + s, T - 1);
+      const float a = aok[p] ? Ab[(int64_t)t * K * K + aoff[p]] : NEG_INF;
+      const float e = eok[p] ? Eb[(int64_t)t * K + ej[p]] : 0.f;
+      const float ein = eok[0] ? Eb[(int64_t)t * K + ej[0]] : NEG_INF;
+      float emx = allred<KP, true>(ein, OpMax{});
+      emx = emx == NEG_INF ? 0.f : emx;
+      if (beta) {
+        av[s] = (a + (e - emx)) * LOG2E_F;
+      } else {
+        av[s] = a * LOG2E_F;
+        dv[s] = (e - emx) * LOG2E_F;
+        xv[s] = emx;
+      }
+    }
+  };
+  auto read_table = [&](int c) {
+#pragma unroll
+    for (int q = 0; q < HC / 4; ++q) {
+      const float4 m = *reinterpret_cast<const float4*>(&Mt[((size_t)(c * (HC / 4) + q) * 64 + lane) * 4]);
+      ml[4 * q] = m.x;
+      ml[4 * q + 1] = m.y;
+      ml[4 * q + 2] = m.z;
+      ml[4 * q + 3] = m.w;
+    }
+  };
+
+  // ---- chains
+  const float lp2 = jo < K ? log_pi[jo] * LOG2E_F : 0.f;
+  float al = NEG_INF, be = 0.f, x = 0.f, sk = 0.f, lo = 1.f, hi = 1.f, rng = 0.f;
+  double S2 = 0.0, SE = 0.0;
+
+  auto alpha_chunk = [&](int c) {
+    const int t0 = c * HC;
+    float* vrow = vb + (c & 1) * VB + grp * HC * KP;
+    // log tier (EXACT: max-shifted log-sum-exp; CHECK: some sequence ends inside the chunk)
+    auto steps = [&](bool first, auto exact, auto check) {
+      constexpr bool EXACT = decltype(exact)::value, CHECK = decltype(check)::value;
+      static_for<HC>([&](auto si) {
+        constexpr int s = decltype(si)::value, p = s & 1;
+        if (s == 0 && first) {
+          al = (L > 0 && jo < K) ? lp2 + dv[0] : NEG_INF;
+          mv[0] = 0.f;
+          vrow[jo] = al;
+          return;
+        }
+        const bool upd = !CHECK || t0 + s < L;
+        const float v = al + av[s];
+        float mus = 0.f;
+        if constexpr (EXACT || s % FB_NORM == 0) {
+          const float mu = allred<KP, p == 1>(al, OpMax{});
+          mus = mu == NEG_INF ? 0.f : mu;
+        }
+        float nal;
+        if constexpr (EXACT) {
+          const float mm = fmaxf(allred<KP, p == 1>(v, OpMax{}), F32_LOWEST);
+          const float sm = allred<KP, p == 1>(fexp2(v - mm), OpAdd{});
+          nal = (mm + flog2(sm)) + (dv[s] - mus);
+        } else {
+          const float ls = flog2(allred<KP, p == 1>(fexp2(v), OpAdd{}));
+          nal = ls + (dv[s] - mus);
+          rng = fmaxf(rng, fabsf((eok[p] && upd) ? ls : 0.f));
+        }
+        mv[s] = upd ? mus : 0.f;
+        if (upd) al = nal;
+        vrow[s * KP + (p == 0 ? jo : ji)] = al;
+      });
+    };
+    auto lin_steps = [&](bool first, float e0, auto check) {
+      constexpr bool CHECK = decltype(check)::value;
+      static_for<HC>([&](auto si) {
+        constexpr int s = decltype(si)::value, p = s & 1;
+        if (s == 0 && first) {
+          const float a0 = (L > 0 && jo < K) ? lp2 + e0 : NEG_INF;
+          const float m0 = allred<KP, true>(a0, OpMax{});
+          const float m0s = m0 == NEG_INF ? 0.f : m0;
+          x = fexp2(a0 - m0s);
+          sk = m0s;
+          if (L > 0 && jo < K) lo = fminf(lo, x);
+          vrow[jo] = x;
+          return;
+        }
+        const bool upd = !CHECK || t0 + s < L;
+        const float v = x * ml[s];
+        int k = 0;
+        if constexpr (s % FB_LNORM == FB_LNORM / 2) k = __builtin_amdgcn_frexp_expf(allred<KP, p == 1>(x, OpMax{}));
+        float y = allred<KP, p == 1>(v, OpAdd{});
+        if constexpr (s % FB_LNORM == FB_LNORM / 2) y = __builtin_amdgcn_ldexpf(y, -k);
+        const bool chk = upd && eok[p];
+        lo = chk ? fminf(lo, y) : lo;
+        hi = chk ? fmaxf(hi, y) : hi;
+        if (upd) {
+          x = y;
+          sk += (float)k;
+        }
+        vrow[s * KP + (p == 0 ? jo : ji)] = x;
+      });
+    };
+    const float al_c = al;
+    bool linear = false;
+    if (lin_tier) {
+      read_table(c);
+      const float e0 = c == 0 && eok[0] ? Eb[ej[0]] * LOG2E_F : NEG_INF;
+      lo = hi = 1.f;
+      if (c > 0) {
+        const float m = allred<KP, false>(al, OpMax{});
+        const float ms = m == NEG_INF ? 0.f : m;
+        x = fexp2(al - ms);
+        sk = ms;
+        if (t0 < L && ji < K) lo = fminf(lo, x);
+      }
+      if (__builtin_amdgcn_ballot_w64(t0 + HC > L) == 0) lin_steps(c == 0, e0, std::false_type{});
+      else lin_steps(c == 0, e0, std::true_type{});
+      linear = !__builtin_amdgcn_ballot_w64(lin_bad(lo, hi));
+    }
+    float dS2 = 0.f, dSE = 0.f;  // (one accumulation after the branch keeps S2 / SE in registers)
+    if (linear) {
+      if (t0 < L) {
+        al = flog2(x);
+        dS2 = sk;
+      }
+    } else {
+      read_raw(c, false);
+      al = al_c;
+      rng = 0.f;
+      steps(c == 0, std::false_type{}, std::true_type{});
+      if (__builtin_amdgcn_ballot_w64(rng > FB_LIM)) {
+        al = al_c;
+        steps(c == 0, std::true_type{}, std::true_type{});
+      }
+#pragma unroll
+      for (int s = 0; s < HC; ++s) xv[s] = t0 + s < L ? xv[s] : 0.f;
+      dS2 = tree_sum<HC>(mv);
+      dSE = tree_sum<HC>(xv);
+    }
+    S2 += (double)dS2;
+    SE += (double)dSE;
+    if (lane == 0) flags[c & 1] = linear;
+  };
+
+  // beta on data chunk k (data step d serves t = d - 1; map parity = d's parity)
+  auto beta_chunk = [&](int k, int buf) {
+    const int d0 = k * HC;
+    float* vrow = vb + (2 + buf) * VB + grp * HC * KP;
+    auto steps = [&](bool last, auto exact) {
+      constexpr bool EXACT = decltype(exact)::value;
+      static_for<HC>([&](auto si) {
+        constexpr int s = HC - 1 - decltype(si)::value, p = s & 1;
+        if (s == 0 && last) return;  // t = -1
+        const bool upd = d0 + s - 1 < L - 1;
+        const float v = av[s] + be;
+        float nus = 0.f;
+        if constexpr (EXACT || s % FB_NORM == 0) {
+          const float nu = allred<KP, p == 0>(be, OpMax{});
+          nus = nu == NEG_INF ? 0.f : nu;
+        }
+        float nb;
+        if constexpr (EXACT) {
+          const float mm = fmaxf(allred<KP, p == 0>(v, OpMax{}), F32_LOWEST);
+          const float sm = allred<KP, p == 0>(fexp2(v - mm), OpAdd{});
+          nb = (mm + flog2(sm)) - nus;
+        } else {
+          const float ls = flog2(allred<KP, p == 0>(fexp2(v), OpAdd{}));
+          nb = ls - nus;
+          rng = fmaxf(rng, fabsf((iok[p] && upd) ? ls : 0.f));
+        }
+        if (upd) be = nb;
+        vrow[s * KP + (p == 0 ? ji : jo)] = be;
+      });
+    };
+    auto lin_steps = [&](bool last, auto check) {
+      constexpr bool CHECK = decltype(check)::value;
+      static_for<HC>([&](auto si) {
+        constexpr int s = HC - 1 - decltype(si)::value, p = s & 1;
+        if (s == 0 && last) return;
+        const bool upd = !CHECK || d0 + s - 1 < L - 1;
+        const float v = ml[s] * x;
+        int kx = 0;
+        if constexpr (s % FB_LNORM == FB_LNORM / 2) kx = __builtin_amdgcn_frexp_expf(allred<KP, p == 0>(x, OpMax{}));
+        float y = allred<KP, p == 0>(v, OpAdd{});
+        if constexpr (s % FB_LNORM == FB_LNORM / 2) y = __builtin_amdgcn_ldexpf(y, -kx);
+        const bool chk = upd && iok[p];
+        lo = chk ? fminf(lo, y) : lo;
+        hi = chk ? fmaxf(hi, y) : hi;
+        if (upd) x = y;
+        vrow[s * KP + (p == 0 ? ji : jo)] = x;
+      });
+    };
+    const float be_c = be;
+    bool linear = false;
+    if (lin_tier) {
+      read_table(k);
+      // state of data step d0 + HC (odd last step of the chunk: the j axis of map 1 = outer)
+      const float m = allred<KP, false>(be, OpMax{});
+      x = fexp2(be - (m == NEG_INF ? 0.f : m));
+      lo = hi = 1.f;
+      if (d0 + HC - 1 < L - 1 && ji < K) lo = fminf(lo, x);
+      const bool full = d0 + HC <= L;  // every step of the chunk is live for this sequence
+      if (__builtin_amdgcn_ballot_w64(!full) == 0) lin_steps(k == 0, std::false_type{});
+      else lin_steps(k == 0, std::true_type{});
+      linear = !__builtin_amdgcn_ballot_w64(lin_bad(lo, hi));
+    }
+    if (linear) {
+      be = flog2(x);
+    } else {
+      read_raw(k, true);
+      be = be_c;
+      rng = 0.f;
+      steps(k == 0, std::false_type{});
+      if (__builtin_amdgcn_ballot_w64(rng > FB_LIM)) {
+        be = be_c;
+        steps(k == 0, std::true_type{});
+      }
+    }
+    if (lane == 0) flags[2 + buf] = linear;
+  };
+
+  // ---- flushes (helpers): chain values -> history and/or gamma
+  auto seqlen = [&](int q) {
+    const int64_t bq = b0 + q;
+    if (bq >= B) return -1;
+    const int64_t l = lengths[bq];
+    return (int)(l <= 0 ? 0 : (l < T ? l : T));
+  };
+  // sequence lengths of the flush lanes (pass r covers sequence (r * 64 + lane) / (HC * KP))
+  int Lfl[VB / 64];
+#pragma unroll
+  for (int r = 0; r < VB / 64; ++r) Lfl[r] = seqlen((r * 64 + lane) / (HC * KP));
+  // softmax over the KP-lane state group of lanes idx % KP (padding states masked)
+  auto store_gamma = [&](int q, int t, int j, float xs, bool own) {
+    const float xm = (j < K) ? xs : NEG_INF;
+    const float mx = allred<KP, true>(xm, OpMax{});
+    const float ex = (j < K && mx != NEG_INF) ? fexp2(xm - mx) : 0.f;
+    const float sm = allred<KP, true>(ex, OpAdd{});
+    if (own && j < K) gamma[((b0 + q) * (int64_t)T + t) * K + j] = ex * __builtin_amdgcn_rcpf(sm);
+  };
+  auto flush_alpha = [&](int c) {
+    const bool lin = flags[c & 1] != 0;
+    const float* src = vb + (c & 1) * VB;
+#pragma unroll
+    for (int r = 0; r < VB / 64; ++r) {
+      const int idx = r * 64 + lane;
+      const int q = idx / (HC * KP), rr = idx - q * (HC * KP), s = rr / KP, j = rr - s * KP;
+      const int t = c * HC + s;
+      const float v = lin ? flog2(src[idx]) : src[idx];
+      if (t < HH) hist_a[(q * HH + t) * KP + j] = v;
+      const int Lq = Lfl[r];
+      const bool ok = Lq >= 0 && t < T;
+      const bool own = ok && (t >= Lq - 1 || t / HC + (t + 1) / HC >= nch);
+      const bool past = ok && t >= Lq;  // gamma_t = 0 past the sequence
+      float xs = v;
+      if (own && t < Lq - 1) xs += hist_b[(q * HH + (t + 1 - dbase)) * KP + j];
+      store_gamma(q, t, j, xs, own && !past);
+      if (past && j < K) gamma[((b0 + q) * (int64_t)T + t) * K + j] = 0.f;
+    }
+  };
+  auto flush_beta = [&](int k, int buf) {
+    const bool lin = flags[2 + buf] != 0;
+    const float* src = vb + (2 + buf) * VB;
+#pragma unroll
+    for (int r = 0; r < VB / 64; ++r) {
+      const int idx = r * 64 + lane;
+      const int q = idx / (HC * KP), rr = idx - q * (HC * KP), s = rr / KP, j = rr - s * KP;
+      const int d = k * HC + s, t = d - 1;
+      const float v = lin ? flog2(src[idx]) : src[idx];
+      if (d >= dbase && d - dbase < HH) hist_b[(q * HH + (d - dbase)) * KP + j] = v;
+      const int Lq = Lfl[r];
+      const bool own = Lq >= 0 && t >= 0 && t < Lq - 1 && t / HC + d / HC <= nch - 2;
+      const float xs = own ? hist_a[(q * HH + t) * KP + j] + v : 0.f;
+      store_gamma(q, t, j, xs, own);
+    }
+  };
+
+  // ---- schedule
+  if (wave == 2 && nch > 0) {
+    load_raw(0);
+    linearise(0);
+    if (1 < hF) load_raw(1);
+  } else if (wave == 3 && nch - 1 >= hF) {
+    load_raw(nch - 1);
+    linearise(nch - 1);
+    if (nch - 2 >= hF) load_raw(nch - 2);
+  }
+  lds_barrier();
+  unsigned long long pt0 = 0, pbusy = 0, plin = 0;  // (VQHMM_FB_PROF: per-wave cycle counts)
+  if (prof) pt0 = __builtin_amdgcn_s_memtime();
+  for (int it = 0; it <= nch; ++it) {
+    unsigned long long ta = 0, tb = 0;
+    if (prof) ta = __builtin_amdgcn_s_memtime();
+    if (wave == 0) {
+      if (it < nch) alpha_chunk(it);
+    } else if (wave == 1) {
+      if (it < nch) beta_chunk(nch - 1 - it, it & 1);
+    } else if (wave == 2) {
+      if (it + 1 < hF) {
+        linearise(it + 1);
+        if (it + 2 < hF) load_raw(it + 2);
+      }
+      if (prof) tb = __builtin_amdgcn_s_memtime();
+      if (it >= 1) flush_alpha(it - 1);
+    } else {
+      const int c = nch - 2 - it;
+      if (c >= hF) {
+        linearise(c);
+        if (c - 1 >= hF) load_raw(c - 1);
+      }
+      if (prof) tb = __builtin_amdgcn_s_memtime();
+      if (it >= 1) flush_beta(nch - it, (it - 1) & 1);
+    }
+    if (prof) {
+      __builtin_amdgcn_s_waitcnt(0);
+      const unsigned long long tc = __builtin_amdgcn_s_memtime();
+      pbusy += tc - ta;
+      plin += tb ? tb - ta : 0;
+    }
+    lds_barrier();
+  }
+  if (prof && lane == 0) {
+    unsigned long long* o = prof + ((size_t)blockIdx.x * 4 + wave) * 4;
+    o[0] = __builtin_amdgcn_s_memtime() - pt0;
+    o[1] = pbusy;
+    o[2] = plin;
+    o[3] = (unsigned long long)nch;
+  }
+
+  if (wave == 0) {  // logZ from the state axis held after step L-1 (even t: inner)
+    const int tl = L - 1;
+    const bool held_inner = (tl <= 0) || ((tl & 1) == 0);
+    const int st = held_inner ? jo : ji;
+    const float x0 = st < K ? al : NEG_INF;
+    const float mx = held_inner ? allred<KP, true>(x0, OpMax{}) : allred<KP, false>(x0, OpMax{});
+    const float mxs = fmaxf(mx, F32_LOWEST);
+    const float ex = fexp2(x0 - mxs);
+    const float sx = held_inner ? allred<KP, true>(ex, OpAdd{}) : allred<KP, false>(ex, OpAdd{});
+    if (live && g == 0)
+      logZ[b] = L > 0 ? (float)(LN2_D * (S2 + (double)mxs + (double)flog2(sx)) + SE)
+                      : __builtin_bit_cast(float, 0x7fc00000u);
+  } else if (wave == 2) {  // the steps between the two flush rules: t/HC + (t+1)/HC == nch - 1
+    const int tb = max(((nch - 1) / 2) * HC - 1, 0);
+    for (int idx = lane; idx < SPW * 2 * HC * KP; idx += 64) {  // wave-uniform trip count
+      const int q = idx / (2 * HC * KP), rr = idx - q * (2 * HC * KP), s = rr / KP, j = rr - s * KP;
+      const int t = tb + s;
+      const int Lq = seqlen(q);
+      const bool own = Lq >= 0 && t < Lq - 1 && t / HC + (t + 1) / HC == nch - 1;
+      const float xs = own ? hist_a[(q * HH + t) * KP + j] + hist_b[(q * HH + (t + 1 - dbase)) * KP + j] : 0.f;
+      store_gamma(q, t, j, xs, own);
+    }
+  } else if (wave == 3) {  // steps no chain reached: t >= nch * HC
+    const int t0 = nch * HC, nt = T - t0;
+    for (int64_t idx = lane; idx < (int64_t)SPW * nt * K; idx += 64) {
+      const int q = (int)(idx / ((int64_t)nt * K));
+      const int64_t rr = idx - (int64_t)q * nt * K;
+      if (b0 + q < B) gamma[((b0 + q) * (int64_t)T + t0) * K + rr] = 0.f;
+    }
+  }
+}
+
+static int fb_lin_tier() {  // VQHMM_FB_LIN=0: log tier only (A/B switch)
+  static const int lin = [] {
+    const char* e = getenv("VQHMM_FB_LIN");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  return lin;
+}
+
+// the resident kernel when its LDS fits (VQHMM_FB_RES=0: always the streaming kernel)
+static bool fwdbwd_resident_ok(int64_t B, int64_t K, int64_t T) {
+  const char* env = getenv("VQHMM_FB_RES");  // read per call: the tests switch kernels between calls
+  if ((env && env[0] == '0') || K < 1 || K > 8 || T > 4096) return false;
+  const int kp = K <= 2 ? 2 : K <= 4 ? 4 : 8;
+  const size_t bytes = kp == 2 ? FbRes<2>::lds_bytes((int)T) : kp == 4 ? FbRes<4>::lds_bytes((int)T)
+                                                                     : FbRes<8>::lds_bytes((int)T);
+  if (bytes > 160 * 1024) return false;
+  // one round of workgroups only: a second round doubles the chain time, and the streaming
+  // kernel (two reads of the table, twice the workgroups per CU) is then faster
+  const int64_t spw = 64 / (kp * kp), per_cu = (160 * 1024) / (int64_t)bytes;
+  return cdiv(B, spw) <= 256 * per_cu;
+}
+
+template <int K>
+static void fwdbwd_res_go(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths, int64_t B,
+                          int64_t T, float* gamma, float* logZ, void* ws, hipStream_t s) {
+  const dim3 grid((unsigned)cdiv(B, FbRes<K>::SPW));
+  static const bool prof = [] {
+    const char* e = getenv("VQHMM_FB_PROF");  // diagnostic: per-wave cycle counts into the workspace
+    return e && e[0] == '1';
+  }();
+  fwdbwd_resident_kernel<K><<<grid, 256, FbRes<K>::lds_bytes((int)T), s>>>(
+      log_pi, log_A, em, lengths, B, (int)T, gamma, logZ, fb_lin_tier(), prof ? (unsigned long long*)ws : nullptr);
 }
 
 size_t fwdbwd_ws_bytes(int64_t B, int64_t T, int64_t K) { return 2 * (size_t)B * T * K * sizeof(float); }
@@ -797,6 +1439,20 @@ int launch_fwdbwd(const float* log_pi, const float* log_A, const float* em, cons
   const bool w16 = aligned16(log_A) && aligned16(em);
   float* w = (float*)ws;
   if (K > 8) return launch_fwdbwd_wide(log_pi, log_A, em, lengths, B, T, K, gamma, logZ, w, s);
+  if (fwdbwd_resident_ok(B, K, T)) {
+    switch (K) {
+      case 1: fwdbwd_res_go<1>(log_pi, log_A, em, lengths, B, T, gamma, logZ, ws, s); break;
+      case 2: fwdbwd_res_go<2>(log_pi, log_A, em, lengths, B, T, gamma, logZ, ws, s); break;
+      case 3: fwdbwd_res_go<3>(log_pi, log_A, em, lengths, B, T, gamma, logZ, ws, s); break;
+      case 4: fwdbwd_res_go<4>(log_pi, log_A, em, lengths, B, T, gamma, logZ, ws, s); break;
+      case 5: fwdbwd_res_go<5>(log_pi, log_A, em, lengths, B, T, gamma, logZ, ws, s); break;
+      case 6: fwdbwd_res_go<6>(log_pi, log_A, em, lengths, B, T, gamma, logZ, ws, s); break;
+      case 7: fwdbwd_res_go<7>(log_pi, log_A, em, lengths, B, T, gamma, logZ, ws, s); break;
+      default: fwdbwd_res_go<8>(log_pi, log_A, em, lengths, B, T, gamma, logZ, ws, s); break;
+    }
+    VQHMM_LAUNCH_CHECK();
+    return VQHMM_OK;
+  }
   switch (K) {
     case 1: fwdbwd_go<1, false>(log_pi, log_A, em, lengths, B, T, gamma, logZ, w, s); break;
     case 2: fwdbwd_go<2, false>(log_pi, log_A, em, lengths, B, T, gamma, logZ, w, s); break;
