@@ -872,36 +872,50 @@ __global__ __launch_bounds__(128) void fwdbwd_kernel(const float* __restrict__ l
   }
 
   // ---------------------------------------------------------------- gamma
+  // (sequence, t) items spread over both waves, GU per thread with all their loads in flight
+  // before the first use
   __syncthreads();
-  for (int q = 0; q < SPW; ++q) {
-    const int64_t bq = b0 + q;
-    if (bq >= B) break;
-    const int64_t Lq0 = lengths[bq];
-    const int Lq = (int)(Lq0 <= 0 ? 0 : (Lq0 < T ? Lq0 : T));
-    for (int t = threadIdx.x; t < T; t += 128) {
-      float* gq = gamma + (bq * (int64_t)T + t) * K;
-      if (t >= Lq) {
+  constexpr int GU = 4;
+  const int nit = SPW * T;
+  for (int base = 0; base < nit; base += 128 * GU) {
+    float xs[GU][K];
+    int tt[GU], Lu[GU];
+    int64_t bu[GU];
+#pragma unroll
+    for (int u = 0; u < GU; ++u) {
+      const int idx = base + u * 128 + (int)threadIdx.x;
+      const int q = idx / T;
+      tt[u] = idx - q * T;
+      bu[u] = b0 + q;
+      const bool ok = idx < nit && bu[u] < B;
+      const int64_t l = ok ? lengths[bu[u]] : -1;
+      Lu[u] = ok ? (int)(l <= 0 ? 0 : (l < T ? l : T)) : -1;
+      const float* aq = ws_al + (bu[u] * (int64_t)T + tt[u]) * K;
+      const float* bq = ws_be + (bu[u] * (int64_t)T + tt[u] + 1) * K;
+#pragma unroll
+      for (int i = 0; i < K; ++i)
+        xs[u][i] = (tt[u] < Lu[u] ? aq[i] : 0.f) + (tt[u] < Lu[u] - 1 ? bq[i] : 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < GU; ++u) {
+      if (Lu[u] < 0) continue;
+      float* gq = gamma + (bu[u] * (int64_t)T + tt[u]) * K;
+      if (tt[u] >= Lu[u]) {
 #pragma unroll
         for (int i = 0; i < K; ++i) gq[i] = 0.f;
         continue;
       }
-      const float* aq = ws_al + (bq * (int64_t)T + t) * K;
-      const float* bb = ws_be + (bq * (int64_t)T + t + 1) * K;
-      float x[K];
       float mx = NEG_INF;
 #pragma unroll
-      for (int i = 0; i < K; ++i) {
-        x[i] = aq[i] + (t < Lq - 1 ? bb[i] : 0.f);
-        mx = fmaxf(mx, x[i]);
-      }
+      for (int i = 0; i < K; ++i) mx = fmaxf(mx, xs[u][i]);
       float sm = 0.f;
 #pragma unroll
       for (int i = 0; i < K; ++i) {
-        x[i] = mx == NEG_INF ? 0.f : fexp2(x[i] - mx);
-        sm += x[i];
+        xs[u][i] = mx == NEG_INF ? 0.f : fexp2(xs[u][i] - mx);
+        sm += xs[u][i];
       }
 #pragma unroll
-      for (int i = 0; i < K; ++i) gq[i] = x[i] / sm;
+      for (int i = 0; i < K; ++i) gq[i] = xs[u][i] / sm;
     }
   }
 }
