@@ -100,7 +100,9 @@ __device__ __forceinline__ void wgrad2_body(const WgradArgs& a, int WN, int WC, 
 #pragma unroll
       for (int j = 0; j < CBW; ++j) acc[tp][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float bacc = 0.f;
-  const int bcol = tid % NPAD, brow0 = tid / NPAD, bstep = 256 / NPAD;
+  constexpr int bstep = 256 / NPAD;
+  static_assert(RT % bstep == 0, "bias rows per thread");
+  const int bcol = tid % NPAD, brow0 = tid / NPAD;
 
   float4 pdy[PD], px[PX];
   load_dy(rbeg, pdy);
@@ -128,8 +130,12 @@ __device__ __forceinline__ void wgrad2_body(const WgradArgs& a, int WN, int WC, 
       load_dy(r0 + RT, pdy);
       load_x(r0 + RT, px);
     }
-    if (a.bias_slab) {
-      for (int row = brow0; row < RT; row += bstep) bacc += dys[row * LDA + bcol];
+    if (a.bias_slab) {  // RT / bstep rows per thread for every thread (RT % bstep == 0): all reads in flight
+      float bp[RT / bstep];
+#pragma unroll
+      for (int k = 0; k < RT / bstep; ++k) bp[k] = dys[(brow0 + k * bstep) * LDA + bcol];
+#pragma unroll
+      for (int k = 0; k < RT / bstep; ++k) bacc += bp[k];
     }
     // this wave's 16-row slices of the stage, as 4 * (4 / WR) MFMA steps (one row per lane group
     // each): the operands of step s + 1 are read from LDS while the MFMAs of step s run (two
