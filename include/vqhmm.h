@@ -215,6 +215,20 @@ int vqhmm_forward_f32(const vqhmm_dims_t* dims, const float* const* params, cons
 int vqhmm_prior_f32(const vqhmm_dims_t* dims, const float* const* params, const float* u, int u_layout,
                     int64_t B, int64_t T, float* log_pi, float* log_A, void* stream);
 
+/* ------------------------------------------- fused Prior -> Viterbi ----
+ * the Viterbi path of vqhmm_viterbi_f32 over the tables vqhmm_prior_f32 would write
+ * (Prior.forward VQ_VAE_HMM_fixed.py:59-71), computed per chunk on the chip from u and never stored:
+ * HBM reads u (4U B per position) instead of log_A (4K^2 B, written then read).  u as in
+ * vqhmm_prior_f32 (u_layout 0: (B,U,T), 1: (B,T,U)); em (B,T,K); lengths (B) int64 ->
+ * path (B,T) int32, score (B).  path / score equal vqhmm_viterbi_f32 on vqhmm_prior_f32's log_pi and
+ * log_A bit for bit.  K <= 8, u_dim <= 4, trans_hidden in {64, 128, 256}; other dims ->
+ * VQHMM_EUNSUPPORTED (run vqhmm_prior_f32 + vqhmm_viterbi_f32).  Workspace:
+ * vqhmm_prior_viterbi_workspace_size(dims, B, T) bytes. */
+size_t vqhmm_prior_viterbi_workspace_size(const vqhmm_dims_t* dims, int64_t B, int64_t T);
+int vqhmm_prior_viterbi_f32(const vqhmm_dims_t* dims, const float* const* params, const float* u, int u_layout,
+                            const float* em, const int64_t* lengths, int64_t B, int64_t T, int32_t* path,
+                            float* score, void* workspace, size_t ws_bytes, void* stream);
+
 /* ------------------------------------------------------- hard regimes ----
  * regime_probs.argmax(dim=1) of softmax(encode(x), dim=1) — backtesting.py:154-155,
  * src/backtesting.py:105-107, VQ_VAE+HMM.ipynb:830, visualize.ipynb:74.  One fused

@@ -112,3 +112,55 @@ def test_viterbi_regimes_vs_c_oracle(case):
     rp, rs = c_oracle.viterbi(log_pi.cpu().numpy(), log_A.cpu().numpy(), em.cpu().numpy(), L.numpy())
     assert np.array_equal(path.cpu().numpy(), rp)
     assert np.array_equal(score.cpu().numpy().view(np.uint32), rs.view(np.uint32))
+
+
+@pytest.mark.parametrize("K,U,TH,B,T,lay", [
+    (1, 4, 64, 37, 45, 0), (2, 3, 64, 20, 100, 0), (3, 4, 128, 70, 333, 0), (3, 2, 64, 9, 17, 1),
+    (4, 4, 64, 33, 129, 1), (5, 4, 128, 9, 200, 0), (6, 1, 256, 11, 77, 0), (7, 4, 64, 13, 300, 1),
+    (8, 4, 128, 37, 250, 0), (8, 4, 256, 5, 64, 0), (8, 4, 128, 6, 1000, 0)])
+def test_prior_viterbi_fused_bit_exact(K, U, TH, B, T, lay):
+    """Fused Prior-MLP -> Viterbi: the same path and score bits as
+    Prior.forward's log_A fed to the Viterbi kernel, and as the C oracle on that log_A;
+    ragged lengths (0, 1, 2, T, random), T not a multiple of the chunk, B not a multiple of
+    the workgroup's sequences."""
+    import vqhmm
+    torch.manual_seed(1000 * K + TH + U)
+    prior = vqhmm.Prior(K, u_dim=U, trans_hidden=TH)
+    with torch.no_grad():  # sharper tables than the default init: paths that actually switch
+        prior.transition_net[2].weight.mul_(4.0)
+        prior.log_prior.normal_()
+    prior = prior.cuda()
+    u = 2.0 * torch.randn(B, U, T)
+    if lay == 1:
+        u = u.transpose(1, 2).contiguous()
+    u = u.cuda()
+    em = torch.log_softmax(3.0 * torch.randn(B, T, K), dim=2).cuda()
+    L = torch.randint(1, T + 1, (B,))
+    L[0] = T
+    if B > 3:
+        L[1], L[2], L[3] = 0, 1, 2
+    got = vqhmm.prior_viterbi(prior, u, em, L)
+    assert got is not None
+    with torch.no_grad():
+        log_pi, log_A = prior(u)
+    ref = vqhmm.viterbi(log_pi, log_A, em, L)
+    assert torch.equal(got[0].cpu(), ref[0].cpu())
+    assert np.array_equal(got[1].cpu().numpy().view(np.uint32), ref[1].cpu().numpy().view(np.uint32))
+    rp, rs = c_oracle.viterbi(log_pi.cpu().numpy(), log_A.cpu().numpy(), em.cpu().numpy(), L.numpy())
+    assert np.array_equal(got[0].cpu().numpy(), rp)
+    assert np.array_equal(got[1].cpu().numpy().view(np.uint32), rs.view(np.uint32))
+    if K > 1:
+        assert len(np.unique(rp[rp >= 0])) > 1
+
+
+def test_prior_viterbi_outside_fused_range_falls_back():
+    """K > 8 (or TH outside {64, 128, 256}): prior_viterbi reports None and viterbi_regimes
+    runs Prior.forward + Viterbi (both native) with the same contract."""
+    import vqhmm
+    prior = vqhmm.Prior(9, u_dim=4, trans_hidden=64).cuda()
+    u = torch.randn(3, 4, 40, device="cuda")
+    em = torch.log_softmax(torch.randn(3, 40, 9, device="cuda"), dim=2)
+    assert vqhmm.prior_viterbi(prior, u, em) is None
+    prior = vqhmm.Prior(3, u_dim=4, trans_hidden=32).cuda()
+    em = torch.log_softmax(torch.randn(3, 40, 3, device="cuda"), dim=2)
+    assert vqhmm.prior_viterbi(prior, u, em) is None

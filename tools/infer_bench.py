@@ -1,5 +1,6 @@
 """End-to-end viterbi_regimes cost split: encoder + emission
-log_softmax, Prior.forward (log_A materialised), Viterbi, at a cfg5-shaped shard.
+log_softmax, Prior.forward (log_A materialised), Viterbi, vs the fused Prior-MLP -> Viterbi
+kernel (vqhmm_prior_viterbi_f32), at a cfg5-shaped shard.
 usage: python tools/infer_bench.py [B] [T]"""
 import os
 import sys
@@ -37,11 +38,15 @@ def main():
     with torch.no_grad():
         t_enc, em = timeit(lambda: torch.log_softmax(m.encode(x), dim=1).transpose(1, 2).contiguous())
         t_pri, (log_pi, log_A) = timeit(lambda: m.prior(u))
-        t_vit, _ = timeit(lambda: viterbi(log_pi, log_A, em, None))
+        t_vit, ref = timeit(lambda: viterbi(log_pi, log_A, em, None))
+        t_fus, got = timeit(lambda: vqhmm.prior_viterbi(m.prior, u, em))
+        t_all0, _ = timeit(lambda: vqhmm.viterbi_regimes(m, x, u, fused=False))
         t_all, _ = timeit(lambda: vqhmm.viterbi_regimes(m, x, u))
     gb = log_A.numel() * 4 / 1e9
     print(f"B={B} T={T} K={K}: encode+log_softmax {t_enc:.0f} us, prior (log_A {gb:.2f} GB) {t_pri:.0f} us, "
-          f"viterbi {t_vit:.0f} us, viterbi_regimes end-to-end {t_all:.0f} us")
+          f"viterbi {t_vit:.0f} us | fused prior+viterbi {t_fus:.0f} us (identical paths) | "
+          f"viterbi_regimes end-to-end unfused {t_all0:.0f} us, fused {t_all:.0f} us")
+    assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1]), "fused path differs"
 
 
 if __name__ == "__main__":

@@ -862,4 +862,28 @@ int vqhmm_prior_f32(const vqhmm_dims_t* d, const float* const* w, const float* u
   return launch_prior_fwd(p, s);
 }
 
+size_t vqhmm_prior_viterbi_workspace_size(const vqhmm_dims_t* d, int64_t B, int64_t T) {
+  if (!dims_ok(d) || B < 0 || T < 0) return 0;
+  return 256 + viterbi_ws_bytes(B, T, d->K);
+}
+
+int vqhmm_prior_viterbi_f32(const vqhmm_dims_t* d, const float* const* w, const float* u, int u_layout,
+                            const float* em, const int64_t* lengths, int64_t B, int64_t T, int32_t* path,
+                            float* score, void* ws, size_t ws_bytes, void* stream) {
+  if (!dims_ok(d) || !w || B < 0 || T < 0) return VQHMM_EINVAL;
+  if (B == 0 || T == 0) return VQHMM_OK;
+  if (!u || !em || !lengths || !path || !score) return VQHMM_EINVAL;
+  PriorArgs p{};
+  p.B = B; p.T = (int)T; p.K = d->K; p.U = d->u_dim; p.TH = d->trans_hidden; p.u = u;
+  if (u_layout == 0) { p.u_sc = T; p.u_st = 1; } else { p.u_sc = 1; p.u_st = d->u_dim; }
+  p.W1 = w[TN0_W]; p.b1 = w[TN0_B]; p.W2 = w[TN2_W]; p.b2 = w[TN2_B]; p.log_A = nullptr;
+  if (!prior_viterbi_supported(p) || T > (1 << 28)) return VQHMM_EUNSUPPORTED;
+  if (!ws || ws_bytes < vqhmm_prior_viterbi_workspace_size(d, B, T)) return VQHMM_EWORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  float* log_pi = (float*)ws;
+  int rc;
+  if ((rc = launch_log_softmax_vec(w[LOG_PRIOR], d->K, log_pi, s))) return rc;
+  return launch_prior_viterbi(p, log_pi, em, lengths, path, score, (char*)ws + 256, ws_bytes - 256, s);
+}
+
 }  // extern "C"

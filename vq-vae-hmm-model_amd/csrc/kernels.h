@@ -243,6 +243,11 @@ int launch_prior_fwd(const PriorArgs& p, hipStream_t s);
 // Prior.forward on MFMA (prior.hip): K*K <= 64, U <= 4, TH in {64, 128, 256}
 bool prior_mfma_supported(const PriorArgs& p);
 int launch_prior_mfma(const PriorArgs& p, hipStream_t s);
+// Fused Prior.forward -> Viterbi (prior_viterbi.hip): K <= 8, U <= 4, TH in {64, 128, 256};
+// log_pi on the device, ws = viterbi_ws_bytes(B, T, K); p.log_A unused
+bool prior_viterbi_supported(const PriorArgs& p);
+int launch_prior_viterbi(const PriorArgs& p, const float* log_pi, const float* em, const int64_t* lengths,
+                         int32_t* path, float* score, void* ws, size_t ws_bytes, hipStream_t s);
 // Backward tail (misc.hip grad_tail_kernel), ONE launch: every gradient segment's slabs summed in a
 // fixed chunk order (deterministic, no atomics) and scaled; one extra workgroup reduces the q0 slab
 // and writes the log_prior gradient.

@@ -11,46 +11,30 @@
 //   floats of log_A (coalesced across lanes).
 // The weights are staged in LDS once per workgroup.  K*K <= 64, U <= 4, TH a multiple of 16 <= 256.
 #include "kernels.h"
+#include "prior_tile.h"
 
 namespace vqhmm {
 
 namespace {
 template <int HB, int KB>
 struct PriorLds {
-  static constexpr int TH = HB * 16, KP2 = KB * 16;
-  static constexpr int LDW2 = TH + 8;  // conflict-free b128 reads of W2 rows (as conv2's c2_ldx)
-  static constexpr int LDZ = KP2 + 4;
-  float W2S[KP2 * LDW2];
-  float W1S[TH * 8];  // [h][c]: W1 (c < U), b1 at c = 4
-  float zS[4][16 * LDZ];
+  PriorW<HB, KB> w;
+  float zS[4][16 * PriorW<HB, KB>::LDZ];
 };
 }  // namespace
 
 template <int HB, int KB>
 __global__ __launch_bounds__(256) void prior_mfma_kernel(PriorArgs p, int64_t ntiles) {
   using S = PriorLds<HB, KB>;
-  constexpr int TH = S::TH;
+  constexpr int LDZ = PriorW<HB, KB>::LDZ;
   extern __shared__ float4 smem4[];
   S& sh = *reinterpret_cast<S*>(smem4);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lg4 = lane >> 4, l16 = lane & 15;
   const int K = p.K, KK = K * K, U = p.U;
-  for (int i = tid; i < S::KP2 * S::LDW2; i += 256) {
-    const int ij = i / S::LDW2, h = i - ij * S::LDW2;
-    sh.W2S[i] = (ij < KK && h < TH) ? p.W2[(int64_t)ij * TH + h] : 0.f;
-  }
-  for (int i = tid; i < TH * 8; i += 256) {
-    const int h = i >> 3, c = i & 7;
-    sh.W1S[i] = c < U ? p.W1[h * U + c] : (c == 4 ? p.b1[h] : 0.f);
-  }
+  prior_stage_weights<HB, KB>(sh.w, p.W1, p.b1, p.W2, K, U, tid, 256);
   f32x4 b2f[KB];
-#pragma unroll
-  for (int kb = 0; kb < KB; ++kb)
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int ij = kb * 16 + 4 * lg4 + v;
-      b2f[kb][v] = ij < KK ? p.b2[ij] : 0.f;
-    }
+  prior_b2_frags<KB>(b2f, p.b2, KK, lg4);
   __syncthreads();
   float* zS = sh.zS[wave];
   const int64_t N = p.B * (int64_t)p.T;
@@ -64,49 +48,13 @@ __global__ __launch_bounds__(256) void prior_mfma_kernel(PriorArgs p, int64_t nt
       const int t = (int)(n - b * p.T);
       ub = p.u[b * (int64_t)U * p.T + lg4 * p.u_sc + (int64_t)t * p.u_st];
     }
-    f32x4 z[KB];
-#pragma unroll
-    for (int kb = 0; kb < KB; ++kb) z[kb] = b2f[kb];
-    auto hid = [&](int hb) {
-      const float w1 = sh.W1S[(hb * 16 + l16) * 8 + lg4];
-      f32x4 c;
-#pragma unroll
-      for (int v = 0; v < 4; ++v) c[v] = sh.W1S[(hb * 16 + 4 * lg4 + v) * 8 + 4];
-      f32x4 h = mfma16x16x4(w1, ub, c);
-#pragma unroll
-      for (int v = 0; v < 4; ++v) h[v] = fmaxf(h[v], 0.f);
-      return h;
-    };
-    f32x4 hc = hid(0);
-#pragma unroll
-    for (int hb = 0; hb < HB; ++hb) {
-      f32x4 w2v[KB];
-#pragma unroll
-      for (int kb = 0; kb < KB; ++kb)
-        w2v[kb] = *reinterpret_cast<const f32x4*>(&sh.W2S[(kb * 16 + l16) * S::LDW2 + hb * 16 + 4 * lg4]);
-      const f32x4 hn = hb + 1 < HB ? hid(hb + 1) : hc;  // next block's hidden MFMA beside this one's
-#pragma unroll
-      for (int v = 0; v < 4; ++v)
-#pragma unroll
-        for (int kb = 0; kb < KB; ++kb) z[kb] = mfma16x16x4(w2v[kb][v], hc[v], z[kb]);
-      hc = hn;
-    }
-    // z^T fragments -> zS[position][ij], then one (position, row) per lane
-#pragma unroll
-    for (int kb = 0; kb < KB; ++kb) *reinterpret_cast<f32x4*>(&zS[l16 * S::LDZ + kb * 16 + 4 * lg4]) = z[kb];
+    prior_tile<HB, KB>(sh.w, b2f, ub, l16, lg4, zS);
     __builtin_amdgcn_wave_barrier();
     for (int idx = lane; idx < 16 * K; idx += 64) {
       const int pos = idx / K, i = idx - pos * K;
       const int64_t np = tile * 16 + pos;
       if (np >= N) continue;
-      const float* zr = &zS[pos * S::LDZ + i * K];
-      float m = -__builtin_inff();
-      for (int j = 0; j < K; ++j) m = fmaxf(m, zr[j]);
-      float s = 0.f;
-      for (int j = 0; j < K; ++j) s += __expf(zr[j] - m);
-      const float ls = m + __logf(s);
-      float* out = p.log_A + np * KK + i * K;
-      for (int j = 0; j < K; ++j) out[j] = zr[j] - ls;
+      prior_row_lsm(&zS[pos * LDZ + i * K], K, p.log_A + np * KK + i * K);
     }
     __builtin_amdgcn_wave_barrier();  // zS is rewritten by the next tile
   }
@@ -128,10 +76,11 @@ static int launch_pm(const PriorArgs& p, hipStream_t s) {
 
 template <int HB>
 static int launch_pm_k(const PriorArgs& p, hipStream_t s) {
-  const int kb = (p.K * p.K + 15) / 16;
-  if (kb <= 1) return launch_pm<HB, 1>(p, s);
-  if (kb <= 2) return launch_pm<HB, 2>(p, s);
-  return launch_pm<HB, 4>(p, s);
+  switch (prior_kb(p.K)) {
+    case 1: return launch_pm<HB, 1>(p, s);
+    case 2: return launch_pm<HB, 2>(p, s);
+    default: return launch_pm<HB, 4>(p, s);
+  }
 }
 
 int launch_prior_mfma(const PriorArgs& p, hipStream_t s) {

@@ -10,10 +10,11 @@ from . import _ext  # noqa: F401
 from .checkpoint import load_checkpoint, load_encoder, save_checkpoint, save_encoder  # noqa: F401
 from .data import DeviceChunkLoader, RandomChunkDataset, collate_fn  # noqa: F401
 from .hmm import forward_backward, quantize, regime_argmax, viterbi, vq_argmin  # noqa: F401
-from .infer import hard_regimes, infer, viterbi_regimes  # noqa: F401
+from .infer import hard_regimes, infer, prior_viterbi, viterbi_regimes  # noqa: F401
 from .model import PARAM_ORDER, VAE_HMM, Decoder, Encoder, Prior  # noqa: F401
 from .train import Trainer, TrainState, train_model  # noqa: F401
 
 __all__ = ["VAE_HMM", "Encoder", "Prior", "Decoder", "train_model", "Trainer", "TrainState", "RandomChunkDataset",
            "collate_fn", "DeviceChunkLoader", "vq_argmin", "quantize", "regime_argmax", "viterbi", "forward_backward", "PARAM_ORDER",
-           "save_checkpoint", "load_checkpoint", "save_encoder", "load_encoder", "infer", "hard_regimes", "viterbi_regimes"]
+           "save_checkpoint", "load_checkpoint", "save_encoder", "load_encoder", "infer", "hard_regimes", "viterbi_regimes",
+           "prior_viterbi"]

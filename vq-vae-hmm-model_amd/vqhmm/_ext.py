@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("VQHMM_LIB_PATH") or os.path.join(_HERE, "libvqhmm.so"
 NPARAMS = 18
 ABI_VERSION = 5
 
+EUNSUPPORTED = -4
 _ERRORS = {-1: "invalid argument", -2: "kernel launch failed", -3: "workspace too small",
            -4: "unsupported shape"}
 
@@ -73,6 +74,9 @@ _SIGS = {
                                          c_vp, c_vp, c_vp, c_sz, c_vp]),
     "vqhmm_prior_f32": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(c_vp), c_vp, ctypes.c_int, c_i64,
                                        c_i64, c_vp, c_vp, c_vp]),
+    "vqhmm_prior_viterbi_workspace_size": (c_sz, [ctypes.POINTER(Dims), c_i64, c_i64]),
+    "vqhmm_prior_viterbi_f32": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(c_vp), c_vp, ctypes.c_int, c_vp,
+                                               c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "vqhmm_regimes_f32": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(c_vp), c_vp, c_i64, c_i64, c_vp,
                                          c_vp, c_vp, c_sz, c_vp]),
     "vqhmm_argmax_f32": (ctypes.c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp]),
