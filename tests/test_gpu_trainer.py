@@ -113,3 +113,32 @@ def test_trainer_custom_loss_fn_matches_default():
     for k in RM.PARAM_ORDER:
         a, b = out[0][1][k], out[1][1][k]
         assert (a - b).abs().max().item() <= 1e-4 * max(b.abs().max().item(), 1e-30) + 1e-6, k
+
+
+@pytest.mark.parametrize("B,K,D,H,H2,T", [(128, 3, 5, 64, 32, 200), (1024, 3, 5, 64, 32, 200),
+                                          (64, 8, 16, 64, 32, 96), (40, 32, 64, 80, 72, 50)])
+def test_fused_tail_adam_bit_identical(B, K, D, H, H2, T):
+    """The single-process step's backward tail in one launch (tail_adam_kernel: slab reduction +
+    composed dW / dE + Adam, with the in-launch wait for the dWc segment) against the split path
+    (grad_tail, compose_bwd, adam_kernel): identical gradients, moments and parameters, 4 steps."""
+    import vqhmm
+    gen = torch.Generator().manual_seed(B + K)
+    x = torch.randn(B, D, T, generator=gen).cuda()
+    u = torch.randn(B, 4, T, generator=gen).cuda()
+    L = torch.randint(max(1, T // 4), T + 1, (B,), generator=gen)
+    st = []
+    for _ in range(2):
+        torch.manual_seed(3)
+        m = vqhmm.VAE_HMM(D, H, K, H2, u_dim=4, trans_hidden=64).cuda()
+        st.append(vqhmm.TrainState(m, lr=1e-3))
+    fused, split = st
+    xs, us, Ls = fused.prepare(x, u, L)
+    for _ in range(4):
+        fused.forward_backward_adam(xs, us, Ls, 0.7)
+        split.forward_backward(xs, us, Ls, 0.7)
+        split.apply_adam()
+    torch.cuda.synchronize()
+    assert torch.equal(fused.grad, split.grad)
+    assert torch.equal(fused.exp_avg, split.exp_avg) and torch.equal(fused.exp_avg_sq, split.exp_avg_sq)
+    assert torch.equal(fused.flat, split.flat)
+    assert int(fused.step_dev.item()) == int(split.step_dev.item()) == 4

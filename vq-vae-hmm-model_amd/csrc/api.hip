@@ -424,6 +424,64 @@ void wgrad_jobs(const ElboPlan& p, WgradArgs* wa) {
   }
 }
 
+// The backward's slab segments (every weight gradient's per-chunk partials) for grad_tail /
+// tail_adam; returns the index of the composed decoder conv1's dWc segment.
+int make_tail(const ElboPlan& p, const StepCtx& c, TailArgs& ta) {
+  const float* const* w = c.w;
+  int64_t off[VQHMM_NPARAMS + 1];
+  vqhmm_dims_t d{p.D, p.H, p.K, p.H2, p.U, p.TH};
+  vqhmm_param_layout(&d, off);
+  float* g = c.g;
+  const float* gs = c.gscale;
+  int n = 0;
+  auto seg = [&](const float* slab, int64_t nch, int64_t len, float* out, const float* scale) {
+    ta.s[n++] = SlabSeg{slab, out, scale, nch, len};
+  };
+  const WLayer* wl = p.wl;
+  seg(wl[0].slab, wl[0].nchunks, (int64_t)wl[0].N * wl[0].C, g + off[PAR_W], gs);  // dpar is unscaled
+  seg(wl[0].bslab, wl[0].nchunks, wl[0].N, g + off[PAR_B], gs);
+  seg(wl[1].slab, wl[1].nchunks, (int64_t)wl[1].N * wl[1].C * 3, g + off[DEC2_W], nullptr);
+  seg(wl[1].bslab, wl[1].nchunks, wl[1].N, g + off[DEC2_B], nullptr);
+  const int dwc_seg = n;
+  seg(wl[2].slab, wl[2].nchunks, (int64_t)wl[2].N * wl[2].C * 3, p.dWc, nullptr);
+  seg(wl[2].bslab, wl[2].nchunks, wl[2].N, g + off[DEC1_B], nullptr);
+  seg(wl[3].slab, wl[3].nchunks, (int64_t)wl[3].N * wl[3].C, g + off[LOGIT_W], nullptr);
+  seg(wl[3].bslab, wl[3].nchunks, wl[3].N, g + off[LOGIT_B], nullptr);
+  seg(wl[4].slab, wl[4].nchunks, (int64_t)wl[4].N * wl[4].C * 3, g + off[ENC2_W], nullptr);
+  seg(wl[4].bslab, wl[4].nchunks, wl[4].N, g + off[ENC2_B], nullptr);
+  seg(wl[5].slab, wl[5].nchunks, (int64_t)wl[5].N * wl[5].C * 3, g + off[ENC1_W], nullptr);
+  seg(wl[5].bslab, wl[5].nchunks, wl[5].N, g + off[ENC1_B], nullptr);
+  if (p.staged) {
+    seg(wl[6].slab, wl[6].nchunks, (int64_t)p.TH * p.U, g + off[TN0_W], gs);
+    seg(wl[6].bslab, wl[6].nchunks, p.TH, g + off[TN0_B], gs);
+    seg(wl[7].slab, wl[7].nchunks, (int64_t)p.K * p.K * p.TH, g + off[TN2_W], gs);
+    seg(wl[7].bslab, wl[7].nchunks, (int64_t)p.K * p.K, g + off[TN2_B], gs);
+  } else {
+    seg(p.sW1, p.hgrid, (int64_t)p.TH * p.U, g + off[TN0_W], gs);
+    seg(p.sb1, p.hgrid, p.TH, g + off[TN0_B], gs);
+    seg(p.sW2, p.hgrid, (int64_t)p.K * p.K * p.TH, g + off[TN2_W], gs);
+    seg(p.sb2, p.hgrid, (int64_t)p.K * p.K, g + off[TN2_B], gs);
+  }
+  ta.nseg = n;
+  ta.q0slab = p.sq0;
+  ta.q0chunks = p.staged ? 1 : p.hgrid;
+  ta.lp = LogPriorGradArgs{nullptr, w[LOG_PRIOR], p.K, c.beta, c.norm, p.B, c.gscale, g + off[LOG_PRIOR]};
+  if (c.loss) {  // the forward ran with need_grad = 2
+    ta.fin_part = p.part; ta.fin_nblk = p.hgrid; ta.fin_cnt = p.cnt; ta.fin_B = p.B; ta.fin_T = p.T;
+    ta.fin_D = p.D; ta.fin_loss = c.loss; ta.fin_accum = c.loss_accum; ta.fin_pieces = p.pieces;
+  }
+  return dwc_seg;
+}
+
+// VQHMM_TAIL_ADAM=0: grad_tail and compose_adam as two launches (A/B); read once
+bool tail_adam_on() {
+  static const bool v = [] {
+    const char* e = getenv("VQHMM_TAIL_ADAM");
+    return !e || atoi(e) != 0;
+  }();
+  return v;
+}
+
 int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
   const float* const* w = c.w;
   switch (st) {
@@ -494,48 +552,9 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       return launch_wgrad(wa[st - S_W_PAR], s);
     }
     case S_REDUCE: {
-      int64_t off[VQHMM_NPARAMS + 1];
-      vqhmm_dims_t d{p.D, p.H, p.K, p.H2, p.U, p.TH};
-      vqhmm_param_layout(&d, off);
-      float* g = c.g;
-      const float* gs = c.gscale;
+      if (c.adam && tail_adam_on()) return VQHMM_OK;  // in S_COMPOSE_BWD's launch (tail_adam_kernel)
       TailArgs ta{};
-      int n = 0;
-      auto seg = [&](const float* slab, int64_t nch, int64_t len, float* out, const float* scale) {
-        ta.s[n++] = SlabSeg{slab, out, scale, nch, len};
-      };
-      const WLayer* wl = p.wl;
-      seg(wl[0].slab, wl[0].nchunks, (int64_t)wl[0].N * wl[0].C, g + off[PAR_W], gs);  // dpar is unscaled
-      seg(wl[0].bslab, wl[0].nchunks, wl[0].N, g + off[PAR_B], gs);
-      seg(wl[1].slab, wl[1].nchunks, (int64_t)wl[1].N * wl[1].C * 3, g + off[DEC2_W], nullptr);
-      seg(wl[1].bslab, wl[1].nchunks, wl[1].N, g + off[DEC2_B], nullptr);
-      seg(wl[2].slab, wl[2].nchunks, (int64_t)wl[2].N * wl[2].C * 3, p.dWc, nullptr);
-      seg(wl[2].bslab, wl[2].nchunks, wl[2].N, g + off[DEC1_B], nullptr);
-      seg(wl[3].slab, wl[3].nchunks, (int64_t)wl[3].N * wl[3].C, g + off[LOGIT_W], nullptr);
-      seg(wl[3].bslab, wl[3].nchunks, wl[3].N, g + off[LOGIT_B], nullptr);
-      seg(wl[4].slab, wl[4].nchunks, (int64_t)wl[4].N * wl[4].C * 3, g + off[ENC2_W], nullptr);
-      seg(wl[4].bslab, wl[4].nchunks, wl[4].N, g + off[ENC2_B], nullptr);
-      seg(wl[5].slab, wl[5].nchunks, (int64_t)wl[5].N * wl[5].C * 3, g + off[ENC1_W], nullptr);
-      seg(wl[5].bslab, wl[5].nchunks, wl[5].N, g + off[ENC1_B], nullptr);
-      if (p.staged) {
-        seg(wl[6].slab, wl[6].nchunks, (int64_t)p.TH * p.U, g + off[TN0_W], gs);
-        seg(wl[6].bslab, wl[6].nchunks, p.TH, g + off[TN0_B], gs);
-        seg(wl[7].slab, wl[7].nchunks, (int64_t)p.K * p.K * p.TH, g + off[TN2_W], gs);
-        seg(wl[7].bslab, wl[7].nchunks, (int64_t)p.K * p.K, g + off[TN2_B], gs);
-      } else {
-        seg(p.sW1, p.hgrid, (int64_t)p.TH * p.U, g + off[TN0_W], gs);
-        seg(p.sb1, p.hgrid, p.TH, g + off[TN0_B], gs);
-        seg(p.sW2, p.hgrid, (int64_t)p.K * p.K * p.TH, g + off[TN2_W], gs);
-        seg(p.sb2, p.hgrid, (int64_t)p.K * p.K, g + off[TN2_B], gs);
-      }
-      ta.nseg = n;
-      ta.q0slab = p.sq0;
-      ta.q0chunks = p.staged ? 1 : p.hgrid;
-      ta.lp = LogPriorGradArgs{nullptr, w[LOG_PRIOR], p.K, c.beta, c.norm, p.B, c.gscale, g + off[LOG_PRIOR]};
-      if (c.loss) {  // the forward ran with need_grad = 2
-        ta.fin_part = p.part; ta.fin_nblk = p.hgrid; ta.fin_cnt = p.cnt; ta.fin_B = p.B; ta.fin_T = p.T;
-        ta.fin_D = p.D; ta.fin_loss = c.loss; ta.fin_accum = c.loss_accum; ta.fin_pieces = p.pieces;
-      }
+      make_tail(p, c, ta);
       return launch_grad_tail(ta, s);
     }
     case S_COMPOSE_BWD: {
@@ -547,6 +566,11 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
         ca.dWc = p.dWc; ca.Ecopy = p.Ecopy; ca.Wcopy = p.Wcopy; ca.H = p.H; ca.K = p.K;
         ca.g = c.g; ca.n = off[VQHMM_NPARAMS]; ca.off_w = off[DEC1_W]; ca.off_e = off[EMB];
         ca.adam = *c.adam;
+        if (tail_adam_on()) {  // the slab reduction rides here too
+          TailArgs ta{};
+          const int dwc_seg = make_tail(p, c, ta);
+          return launch_tail_adam(ta, ca, dwc_seg, s);
+        }
         return launch_compose_adam(ca, s);
       }
       const LogPriorGradArgs lp{nullptr, nullptr, p.K, c.beta, c.norm, p.B, c.gscale, nullptr};  // in S_REDUCE

@@ -294,6 +294,9 @@ struct ComposeAdamArgs {
   AdamArgs adam;
 };
 int launch_compose_adam(const ComposeAdamArgs& a, hipStream_t s);
+// grad_tail + compose_adam in one launch (misc.hip tail_adam_kernel): ta.s[dwc_seg] is the composed
+// layer's dWc segment (ca.dWc == its out); EUNSUPPORTED past 65535 blocks (then run the two)
+int launch_tail_adam(TailArgs& ta, const ComposeAdamArgs& ca, int dwc_seg, hipStream_t s);
 int launch_grad_tail(TailArgs& a, hipStream_t s);
 int launch_finalize_loss(const double* part, int nblk, const int64_t* lengths, const int64_t* norm, int64_t B, int T,
                          int D, float beta, float* loss, double* accum, float* pieces, hipStream_t s);

@@ -92,38 +92,10 @@ __device__ void block_reduce_cols(const float* slab, int64_t nch, int64_t ld, in
   }
 }
 
-// One workgroup = 64 consecutive columns of one segment x all its chunks (where a segment's rows
-// are float4-aligned, 16 lanes x float4 cover the 64 columns and 16 chunk phases keep 16 x 8 wide
-// loads in flight per column group; otherwise 64 lanes x 4 phases of scalar loads), or (last
-// block, q0slab set) the log_prior gradient.  Phases combine in a fixed order.
-__global__ __launch_bounds__(256) void grad_tail_kernel(TailArgs ta) {
-  __shared__ float part[16][64];
-  __shared__ float red[256];
-  __shared__ float scratch[256];
-  const int64_t nblk = ta.blk_start[ta.nseg];
-  if (ta.fin_loss && (int64_t)blockIdx.x == nblk + (ta.q0slab ? 1 : 0)) {  // ---- the forward's loss
-    __shared__ double fred[5 * 256];
-    finalize_loss_block(ta.fin_part, ta.fin_nblk, nullptr, ta.lp.norm, ta.fin_B, ta.fin_T, ta.fin_D, ta.lp.beta,
-                        ta.fin_loss, ta.fin_accum, ta.fin_pieces, fred, ta.fin_cnt);
-    return;
-  }
-  if ((int64_t)blockIdx.x >= nblk) {  // ---- log_prior gradient (VQ_VAE_HMM_fixed.py:71,:123,:131)
-    const LogPriorGradArgs& lp = ta.lp;
-    const int K = lp.K;
-    block_reduce_cols(ta.q0slab, ta.q0chunks, K, 0, K, red, scratch);
-    if (threadIdx.x == 0) {
-      const float c = -lp.beta / loss_norm_batch(lp.norm, lp.B);
-      const float sc = lp.scale ? *lp.scale : 1.f;
-      float m = -__builtin_inff();
-      for (int k = 0; k < K; ++k) m = fmaxf(m, lp.log_prior[k]);
-      float se = 0.f;
-      for (int k = 0; k < K; ++k) se += __expf(lp.log_prior[k] - m);
-      float tot = 0.f;
-      for (int k = 0; k < K; ++k) tot += c * red[k];
-      for (int k = 0; k < K; ++k) lp.out[k] = sc * (c * red[k] - __expf(lp.log_prior[k] - m) / se * tot);
-    }
-    return;
-  }
+// Columns [64 (blockIdx.x - blk_start[si]), +64) of segment si summed over its chunks (fixed order)
+// and written to sg.out; returns the segment index (the caller's block is one of its blocks).
+// Threads < 64 hold their column's value in *val (valid when *col < len).
+__device__ int tail_segment_block(const TailArgs& ta, float (&part)[16][64], float* val, int64_t* colp) {
   int si = 0;
   while (si + 1 < ta.nseg && (int64_t)blockIdx.x >= ta.blk_start[si + 1]) ++si;
   const SlabSeg& sg = ta.s[si];
@@ -189,7 +161,52 @@ __global__ __launch_bounds__(256) void grad_tail_kernel(TailArgs ta) {
       v += ((part[h][threadIdx.x] + part[h + 1][threadIdx.x]) + part[h + 2][threadIdx.x]) + part[h + 3][threadIdx.x];
     if (sg.scale) v *= *sg.scale;
     sg.out[col] = v;
+    *val = v;
   }
+  *colp = col;
+  return si;
+}
+
+// log_prior gradient (VQ_VAE_HMM_fixed.py:71,:123,:131) from the q0 slab; thread 0 writes lp.out.
+__device__ void tail_logprior_block(const TailArgs& ta, float* red, float* scratch) {
+  const LogPriorGradArgs& lp = ta.lp;
+  const int K = lp.K;
+  block_reduce_cols(ta.q0slab, ta.q0chunks, K, 0, K, red, scratch);
+  if (threadIdx.x == 0) {
+    const float c = -lp.beta / loss_norm_batch(lp.norm, lp.B);
+    const float sc = lp.scale ? *lp.scale : 1.f;
+    float m = -__builtin_inff();
+    for (int k = 0; k < K; ++k) m = fmaxf(m, lp.log_prior[k]);
+    float se = 0.f;
+    for (int k = 0; k < K; ++k) se += __expf(lp.log_prior[k] - m);
+    float tot = 0.f;
+    for (int k = 0; k < K; ++k) tot += c * red[k];
+    for (int k = 0; k < K; ++k) lp.out[k] = sc * (c * red[k] - __expf(lp.log_prior[k] - m) / se * tot);
+  }
+}
+
+// One workgroup = 64 consecutive columns of one segment x all its chunks (where a segment's rows
+// are float4-aligned, 16 lanes x float4 cover the 64 columns and 16 chunk phases keep 16 x 8 wide
+// loads in flight per column group; otherwise 64 lanes x 4 phases of scalar loads), or (last
+// block, q0slab set) the log_prior gradient.  Phases combine in a fixed order.
+__global__ __launch_bounds__(256) void grad_tail_kernel(TailArgs ta) {
+  __shared__ float part[16][64];
+  __shared__ float red[256];
+  __shared__ float scratch[256];
+  const int64_t nblk = ta.blk_start[ta.nseg];
+  if (ta.fin_loss && (int64_t)blockIdx.x == nblk + (ta.q0slab ? 1 : 0)) {  // ---- the forward's loss
+    __shared__ double fred[5 * 256];
+    finalize_loss_block(ta.fin_part, ta.fin_nblk, nullptr, ta.lp.norm, ta.fin_B, ta.fin_T, ta.fin_D, ta.lp.beta,
+                        ta.fin_loss, ta.fin_accum, ta.fin_pieces, fred, ta.fin_cnt);
+    return;
+  }
+  if ((int64_t)blockIdx.x >= nblk) {  // ---- log_prior gradient
+    tail_logprior_block(ta, red, scratch);
+    return;
+  }
+  float v;
+  int64_t col;
+  tail_segment_block(ta, part, &v, &col);
 }
 
 int launch_grad_tail(TailArgs& a, hipStream_t s) {
@@ -206,58 +223,148 @@ int launch_grad_tail(TailArgs& a, hipStream_t s) {
 // Blocks [0, nb): 256 consecutive elements each: gradient (decoder.conv1 weight from dWc and the
 // embedding copy; every other element as reduced) then Adam.  Blocks nb .. nb+K-1: one embedding
 // row k each, dE[k][h] with 4 thread groups splitting o (combined in a fixed order), then Adam.
+// composed decoder conv1: element block cb < cdiv(H*H*3, 256) of dW (256 elements), else row
+// k = cb - that of dE; gradient into g, then Adam (compose_adam_kernel / tail_adam_kernel)
+__device__ void compose_adam_block(const ComposeAdamArgs& a, int64_t cb, int64_t tn, float (&part)[4][256]) {
+  const AdamArgs& ad = a.adam;
+  const int H = a.H, K = a.K;
+  const int64_t nw = cdiv((int64_t)H * H * 3, 256);
+  if (cb < nw) {
+    const int64_t j = cb * 256 + threadIdx.x;
+    if (j < (int64_t)H * H * 3) {
+      const int64_t i = a.off_w + j;
+      const AdamElem e = adam_load(ad, i, tn);
+      const int o = (int)(j / (3 * H)), rem = (int)(j - (int64_t)o * 3 * H), h = rem / 3, tap = rem - 3 * h;
+      float sacc = 0.f;
+#pragma unroll 4
+      for (int k = 0; k < K; ++k) sacc = fmaf(a.dWc[((int64_t)o * K + k) * 3 + tap], a.Ecopy[(int64_t)k * H + h], sacc);
+      a.g[i] = sacc;
+      adam_apply(ad, i, sacc, e);
+    }
+    return;
+  }
+  const int k = (int)(cb - nw);
+  const int grp = threadIdx.x >> 6;
+  for (int h0 = 0; h0 < H; h0 += 64) {
+    const int h = h0 + (threadIdx.x & 63);
+    float sacc = 0.f;
+    if (h < H)
+#pragma unroll 8  // loads of 8 o-steps in flight; the fma chain order is unchanged
+      for (int o = grp; o < H; o += 4)
+#pragma unroll
+        for (int tap = 0; tap < 3; ++tap)
+          sacc = fmaf(a.dWc[((int64_t)o * K + k) * 3 + tap], a.Wcopy[((int64_t)o * H + h) * 3 + tap], sacc);
+    part[grp][threadIdx.x & 63] = sacc;
+    __syncthreads();
+    if (threadIdx.x < 64 && h < H) {
+      const int64_t i = a.off_e + (int64_t)k * H + h;
+      const AdamElem e = adam_load(ad, i, tn);
+      const float gv = ((part[0][threadIdx.x] + part[1][threadIdx.x]) + part[2][threadIdx.x]) + part[3][threadIdx.x];
+      a.g[i] = gv;
+      adam_apply(ad, i, gv, e);
+    }
+    __syncthreads();
+  }
+}
+
+// Blocks [0, nb): 256 consecutive elements each: Adam on the reduced gradient, except the composed
+// decoder conv1 weight / embedding (compose_adam_block), which follow.
 __global__ __launch_bounds__(256) void compose_adam_kernel(ComposeAdamArgs a) {
   __shared__ float part[4][256];
   const AdamArgs& ad = a.adam;
   const int64_t tn = (*ad.step & 0xffffffffll) + 1;
-  const int H = a.H, K = a.K;
   const int64_t nb = cdiv(a.n, 256);
   if ((int64_t)blockIdx.x < nb) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const bool live = i < a.n && !(i >= a.off_e && i < a.off_e + (int64_t)K * H);
-    if (live) {
-      const AdamElem e = adam_load(ad, i, tn);
-      float gv;
-      if (i >= a.off_w && i < a.off_w + (int64_t)H * H * 3) {
-        const int64_t j = i - a.off_w;
-        const int o = (int)(j / (3 * H)), rem = (int)(j - (int64_t)o * 3 * H), h = rem / 3, tap = rem - 3 * h;
-        float sacc = 0.f;
-        for (int k = 0; k < K; ++k) sacc = fmaf(a.dWc[((int64_t)o * K + k) * 3 + tap], a.Ecopy[(int64_t)k * H + h], sacc);
-        gv = sacc;
-        a.g[i] = gv;
-      } else {
-        gv = a.g[i];
-      }
-      adam_apply(ad, i, gv, e);
-    }
+    const bool composed = (i >= a.off_w && i < a.off_w + (int64_t)a.H * a.H * 3) ||
+                          (i >= a.off_e && i < a.off_e + (int64_t)a.K * a.H);
+    if (i < a.n && !composed) adam_apply(ad, i, a.g[i], adam_load(ad, i, tn));
   } else {
-    const int k = (int)(blockIdx.x - nb);
-    const int grp = threadIdx.x >> 6;
-    for (int h0 = 0; h0 < H; h0 += 64) {
-      const int h = h0 + (threadIdx.x & 63);
-      float sacc = 0.f;
-      if (h < H)
-        for (int o = grp; o < H; o += 4)
-#pragma unroll
-          for (int tap = 0; tap < 3; ++tap)
-            sacc = fmaf(a.dWc[((int64_t)o * K + k) * 3 + tap], a.Wcopy[((int64_t)o * H + h) * 3 + tap], sacc);
-      part[grp][threadIdx.x & 63] = sacc;
-      __syncthreads();
-      if (threadIdx.x < 64 && h < H) {
-        const int64_t i = a.off_e + (int64_t)k * H + h;
-        const AdamElem e = adam_load(ad, i, tn);
-        const float gv = ((part[0][threadIdx.x] + part[1][threadIdx.x]) + part[2][threadIdx.x]) + part[3][threadIdx.x];
-        a.g[i] = gv;
-        adam_apply(ad, i, gv, e);
-      }
-      __syncthreads();
-    }
+    compose_adam_block(a, (int64_t)blockIdx.x - nb, tn, part);
   }
   adam_ticket(ad.step, tn);
 }
 
+// The whole backward tail of a single-process step in ONE launch: grad_tail's blocks, each applying
+// Adam to the columns it has just reduced, then the composed decoder conv1's dW / dE blocks
+// (compose_adam_block).  Block order: [segment blocks][log_prior][loss finalize][composed].
+// The composed blocks need the whole reduced dWc: every block of the dWc segment releases its
+// columns (device-scope fence) and adds 1 << 48 to *step; a composed block spins (bounded, acquire
+// polls, one acquire fence after) until that field reaches the segment's block count.  All blocks are co-resident (a few
+// hundred 256-thread blocks) and the dWc blocks precede the waiting ones in dispatch order.  The
+// Adam ticket counts in bits 32..47; the last block rewrites *step = t, clearing both fields.
+__global__ __launch_bounds__(256) void tail_adam_kernel(TailArgs ta, ComposeAdamArgs a, int dwc_seg, int dwc_blocks) {
+  __shared__ float part[16][64];
+  __shared__ float red[256];
+  __shared__ float scratch[256];
+  __shared__ float cpart[4][256];
+  const AdamArgs& ad = a.adam;
+  const int64_t tn = (*ad.step & 0xffffffffll) + 1;
+  const int64_t nblk = ta.blk_start[ta.nseg];
+  const int64_t b = blockIdx.x;
+  const int64_t finb = nblk + (ta.q0slab ? 1 : 0), comp0 = finb + (ta.fin_loss ? 1 : 0);
+  auto* st = reinterpret_cast<unsigned long long*>(ad.step);
+  if (b < nblk) {
+    float v = 0.f;
+    int64_t col;
+    const int si = tail_segment_block(ta, part, &v, &col);
+    const SlabSeg& sg = ta.s[si];
+    if (si == dwc_seg) {
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        __threadfence();
+        atomicAdd(st, 1ull << 48);
+      }
+    } else if (threadIdx.x < 64 && col < sg.len) {
+      const int64_t i = (sg.out - a.g) + col;
+      adam_apply(ad, i, v, adam_load(ad, i, tn));
+    }
+  } else if (ta.q0slab && b == nblk) {
+    tail_logprior_block(ta, red, scratch);
+    if (threadIdx.x == 0)
+      for (int k = 0; k < ta.lp.K; ++k) {
+        const int64_t i = (ta.lp.out - a.g) + k;
+        adam_apply(ad, i, ta.lp.out[k], adam_load(ad, i, tn));
+      }
+  } else if (ta.fin_loss && b == finb) {
+    __shared__ double fred[5 * 256];
+    finalize_loss_block(ta.fin_part, ta.fin_nblk, nullptr, ta.lp.norm, ta.fin_B, ta.fin_T, ta.fin_D, ta.lp.beta,
+                        ta.fin_loss, ta.fin_accum, ta.fin_pieces, fred, ta.fin_cnt);
+  } else {
+    if (threadIdx.x == 0) {
+      for (int spin = 0; spin < (1 << 22); ++spin) {
+        // relaxed: an acquire load would invalidate this XCD's L2 on every poll
+        const unsigned long long w = __hip_atomic_load(st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((int)(w >> 48) >= dwc_blocks) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    compose_adam_block(a, b - comp0, tn, cpart);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long old = atomicAdd(st, 1ull << 32);
+    if (((old >> 32) & 0xffffull) == gridDim.x - 1) atomicExch(st, (unsigned long long)tn);
+  }
+}
+
+int launch_tail_adam(TailArgs& ta, const ComposeAdamArgs& ca, int dwc_seg, hipStream_t s) {
+  if (ta.nseg > MAX_SEGS || (ta.q0slab && ta.lp.K > 256) || dwc_seg < 0 || dwc_seg >= ta.nseg) return VQHMM_EINVAL;
+  ta.blk_start[0] = 0;
+  for (int i = 0; i < ta.nseg; ++i) ta.blk_start[i + 1] = ta.blk_start[i] + cdiv(ta.s[i].len, 64);
+  const int64_t ncomp = cdiv((int64_t)ca.H * ca.H * 3, 256) + ca.K;
+  const int64_t nb = ta.blk_start[ta.nseg] + (ta.q0slab ? 1 : 0) + (ta.fin_loss ? 1 : 0) + ncomp;
+  if (nb >= 65536) return VQHMM_EUNSUPPORTED;  // ticket field
+  const int dwc_blocks = (int)cdiv(ta.s[dwc_seg].len, 64);
+  tail_adam_kernel<<<(unsigned)nb, 256, 0, s>>>(ta, ca, dwc_seg, dwc_blocks);
+  VQHMM_LAUNCH_CHECK();
+  return VQHMM_OK;
+}
+
 int launch_compose_adam(const ComposeAdamArgs& a, hipStream_t s) {
-  const int64_t nb = cdiv(a.n, 256) + a.K;
+  const int64_t nb = cdiv(a.n, 256) + cdiv((int64_t)a.H * a.H * 3, 256) + a.K;
   compose_adam_kernel<<<(unsigned)nb, 256, 0, s>>>(a);
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
@@ -344,6 +451,7 @@ __global__ __launch_bounds__(256) void compose_bwd_kernel(const float* dWc, cons
     const int g = threadIdx.x >> 6;
     for (int h = threadIdx.x & 63; h < H; h += 64) {
       float s = 0.f;
+#pragma unroll 8
       for (int o = g; o < H; o += 4)
 #pragma unroll
         for (int tap = 0; tap < 3; ++tap)
