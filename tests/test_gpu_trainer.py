@@ -142,3 +142,45 @@ def test_fused_tail_adam_bit_identical(B, K, D, H, H2, T):
     assert torch.equal(fused.exp_avg, split.exp_avg) and torch.equal(fused.exp_avg_sq, split.exp_avg_sq)
     assert torch.equal(fused.flat, split.flat)
     assert int(fused.step_dev.item()) == int(split.step_dev.item()) == 4
+
+
+_SPLIT_TAIL = r"""
+import sys, torch
+sys.path.insert(0, sys.argv[1])
+import vqhmm
+B, T = 96, 150
+gen = torch.Generator().manual_seed(5)
+x = torch.randn(B, 5, T, generator=gen).cuda()
+u = torch.randn(B, 4, T, generator=gen).cuda()
+L = torch.randint(30, T + 1, (B,), generator=gen)
+torch.manual_seed(3)
+m = vqhmm.VAE_HMM(5, 64, 3, 32, u_dim=4, trans_hidden=128).cuda()
+st = vqhmm.TrainState(m, lr=1e-3)
+xs, us, Ls = st.prepare(x, u, L)
+for _ in range(2):
+    st.forward_backward(xs, us, Ls, 0.5)
+    st.apply_adam()
+for _ in range(2):
+    st.forward_backward_adam(xs, us, Ls, 0.5)
+torch.cuda.synchronize()
+torch.save({"grad": st.grad.cpu(), "flat": st.flat.cpu(), "m": st.exp_avg.cpu(), "v": st.exp_avg_sq.cpu()}, sys.argv[2])
+"""
+
+
+def test_fused_tail_matches_separate_launches(tmp_path):
+    """The one-launch backward tail (tail_kernel, both the DP form and the Adam-fused form) gives
+    the same bits as grad_tail + compose_bwd / compose_adam as separate launches (VQHMM_TAIL_FUSED=0,
+    read once per process, so each side runs in its own process)."""
+    import os
+    import subprocess
+    import sys
+    from conftest import ROOT
+    pkg = os.path.join(ROOT, "vq-vae-hmm-model_amd")
+    out = {}
+    for flag in ("1", "0"):
+        f = str(tmp_path / f"tail{flag}.pt")
+        subprocess.run([sys.executable, "-c", _SPLIT_TAIL, pkg, f], check=True, timeout=300,
+                       env=dict(os.environ, VQHMM_TAIL_FUSED=flag))
+        out[flag] = torch.load(f, weights_only=True)
+    for k in ("grad", "flat", "m", "v"):
+        assert torch.equal(out["1"][k], out["0"][k]), k

@@ -87,6 +87,7 @@ struct ElboPlan {
   float *sW1, *sb1, *sW2, *sb2, *sq0;
   float *loss, *pieces;
   int64_t* cnt;  // valid count written by the prologue (loss finalized in the backward)
+  unsigned long long* sync;  // the backward tail's in-launch dWc counter, zeroed by the prologue
   // staged head (shapes the fused heads do not cover): Prior MLP as 1x1 convs
   bool staged;
   bool wave_head;  // head_wave.hip (else head_mfma / head.hip)
@@ -154,6 +155,7 @@ ElboPlan plan_elbo(const vqhmm_dims_t* d, int64_t B, int64_t T, void* ws) {
   p.loss = c.take<float>(1);
   p.pieces = c.take<float>(4);
   p.cnt = c.take<int64_t>(1);
+  p.sync = c.take<unsigned long long>(1);
   p.dg2 = c.take<float>(R * ld4(H));
   p.dg1 = c.take<float>(R * ld4(H));
   p.dqd = c.take<float>(R * ld4(K));
@@ -473,10 +475,10 @@ int make_tail(const ElboPlan& p, const StepCtx& c, TailArgs& ta) {
   return dwc_seg;
 }
 
-// VQHMM_TAIL_ADAM=0: grad_tail and compose_adam as two launches (A/B); read once
-bool tail_adam_on() {
+// VQHMM_TAIL_FUSED=0: grad_tail and compose_bwd / compose_adam as two launches (A/B); read once
+bool tail_fused_on() {
   static const bool v = [] {
-    const char* e = getenv("VQHMM_TAIL_ADAM");
+    const char* e = getenv("VQHMM_TAIL_FUSED");
     return !e || atoi(e) != 0;
   }();
   return v;
@@ -497,6 +499,7 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       a.Ecopy = p.Ecopy;
       a.Wcopy = p.Wcopy;
       if (c.need_grad == 2 && !c.norm) { a.lengths = c.lengths; a.cnt = p.cnt; }
+      a.sync = p.sync;
       return launch_prologue(a, s);
     }
     case S_COMPOSE:  // runs inside S_TOPCL's launch
@@ -552,7 +555,7 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       return launch_wgrad(wa[st - S_W_PAR], s);
     }
     case S_REDUCE: {
-      if (c.adam && tail_adam_on()) return VQHMM_OK;  // in S_COMPOSE_BWD's launch (tail_adam_kernel)
+      if (tail_fused_on()) return VQHMM_OK;  // in S_COMPOSE_BWD's launch (tail_kernel)
       TailArgs ta{};
       make_tail(p, c, ta);
       return launch_grad_tail(ta, s);
@@ -561,18 +564,21 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       int64_t off[VQHMM_NPARAMS + 1];
       vqhmm_dims_t d{p.D, p.H, p.K, p.H2, p.U, p.TH};
       vqhmm_param_layout(&d, off);
-      if (c.adam) {  // + Adam on every element: the step's last launch
-        ComposeAdamArgs ca{};
-        ca.dWc = p.dWc; ca.Ecopy = p.Ecopy; ca.Wcopy = p.Wcopy; ca.H = p.H; ca.K = p.K;
-        ca.g = c.g; ca.n = off[VQHMM_NPARAMS]; ca.off_w = off[DEC1_W]; ca.off_e = off[EMB];
+      ComposeAdamArgs ca{};
+      ca.dWc = p.dWc; ca.H = p.H; ca.K = p.K;
+      ca.g = c.g; ca.n = off[VQHMM_NPARAMS]; ca.off_w = off[DEC1_W]; ca.off_e = off[EMB];
+      if (c.adam) {  // this launch updates the parameters: E / W from the prologue's copies
+        ca.Ecopy = p.Ecopy; ca.Wcopy = p.Wcopy;
         ca.adam = *c.adam;
-        if (tail_adam_on()) {  // the slab reduction rides here too
-          TailArgs ta{};
-          const int dwc_seg = make_tail(p, c, ta);
-          return launch_tail_adam(ta, ca, dwc_seg, s);
-        }
-        return launch_compose_adam(ca, s);
+      } else {
+        ca.Ecopy = w[EMB]; ca.Wcopy = w[DEC1_W];
       }
+      if (tail_fused_on()) {  // slab reduction + composed dW / dE (+ Adam) in one launch
+        TailArgs ta{};
+        const int dwc_seg = make_tail(p, c, ta);
+        return launch_tail(ta, ca, dwc_seg, p.sync, c.adam != nullptr, s);
+      }
+      if (c.adam) return launch_compose_adam(ca, s);
       const LogPriorGradArgs lp{nullptr, nullptr, p.K, c.beta, c.norm, p.B, c.gscale, nullptr};  // in S_REDUCE
       return launch_compose_bwd(p.dWc, w[DEC1_W], w[EMB], p.H, p.K, c.g + off[DEC1_W], c.g + off[EMB], lp, s);
     }
@@ -684,6 +690,8 @@ int vqhmm_elbo_stage_info(const vqhmm_dims_t* d, int64_t B, int64_t T, int stage
     const char* nm = kStageNames[stage];
     if (p.wgroup && stage == S_W_ENC1) nm = "wgrad_group(all 6 weight gradients)";
     else if (p.wgroup && stage >= S_W_PAR && stage < S_W_ENC1) nm = "(wgrad: in wgrad_group)";
+    else if (tail_fused_on() && stage == S_REDUCE) nm = "(grad_tail: in the tail launch)";
+    else if (tail_fused_on() && stage == S_COMPOSE_BWD) nm = "tail(grad_tail+compose_bwd[+adam])";
     strncpy(name, nm, name_len - 1);
     name[name_len - 1] = 0;
   }

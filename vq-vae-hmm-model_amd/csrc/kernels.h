@@ -294,9 +294,10 @@ struct ComposeAdamArgs {
   AdamArgs adam;
 };
 int launch_compose_adam(const ComposeAdamArgs& a, hipStream_t s);
-// grad_tail + compose_adam in one launch (misc.hip tail_adam_kernel): ta.s[dwc_seg] is the composed
-// layer's dWc segment (ca.dWc == its out); EUNSUPPORTED past 65535 blocks (then run the two)
-int launch_tail_adam(TailArgs& ta, const ComposeAdamArgs& ca, int dwc_seg, hipStream_t s);
+// grad_tail + compose_bwd (+ Adam: compose_adam) in one launch (misc.hip tail_kernel): ta.s[dwc_seg]
+// is the composed layer's dWc segment (ca.dWc == its out); *sync zeroed by the step's prologue
+int launch_tail(TailArgs& ta, const ComposeAdamArgs& ca, int dwc_seg, unsigned long long* sync, bool adam,
+                hipStream_t s);
 int launch_grad_tail(TailArgs& a, hipStream_t s);
 int launch_finalize_loss(const double* part, int nblk, const int64_t* lengths, const int64_t* norm, int64_t B, int T,
                          int D, float beta, float* loss, double* accum, float* pieces, hipStream_t s);
@@ -322,6 +323,7 @@ struct PrologueArgs {  // step prologue: x, u -> PCL, the composed decoder conv1
   float* Wcopy;     // fused compose + Adam launch, or null
   const int64_t* lengths;  // with cnt: the last block writes the batch's valid count
   int64_t* cnt;            // (sum_b min(max(L_b, 0), T)) for a loss finalized in the backward, or null
+  unsigned long long* sync;  // zeroed: the backward tail's in-launch counter (launch_tail), or null
   unsigned nbx, nbu;                // set by launch_prologue
   unsigned img_blk0[MAX_WIMG + 1];  // set by launch_prologue: first block of each image
 };

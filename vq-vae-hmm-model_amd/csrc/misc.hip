@@ -225,6 +225,7 @@ int launch_grad_tail(TailArgs& a, hipStream_t s) {
 // row k each, dE[k][h] with 4 thread groups splitting o (combined in a fixed order), then Adam.
 // composed decoder conv1: element block cb < cdiv(H*H*3, 256) of dW (256 elements), else row
 // k = cb - that of dE; gradient into g, then Adam (compose_adam_kernel / tail_adam_kernel)
+template <bool ADAM>
 __device__ void compose_adam_block(const ComposeAdamArgs& a, int64_t cb, int64_t tn, float (&part)[4][256]) {
   const AdamArgs& ad = a.adam;
   const int H = a.H, K = a.K;
@@ -233,13 +234,14 @@ __device__ void compose_adam_block(const ComposeAdamArgs& a, int64_t cb, int64_t
     const int64_t j = cb * 256 + threadIdx.x;
     if (j < (int64_t)H * H * 3) {
       const int64_t i = a.off_w + j;
-      const AdamElem e = adam_load(ad, i, tn);
+      AdamElem e{};
+      if constexpr (ADAM) e = adam_load(ad, i, tn);
       const int o = (int)(j / (3 * H)), rem = (int)(j - (int64_t)o * 3 * H), h = rem / 3, tap = rem - 3 * h;
       float sacc = 0.f;
 #pragma unroll 4
       for (int k = 0; k < K; ++k) sacc = fmaf(a.dWc[((int64_t)o * K + k) * 3 + tap], a.Ecopy[(int64_t)k * H + h], sacc);
       a.g[i] = sacc;
-      adam_apply(ad, i, sacc, e);
+      if constexpr (ADAM) adam_apply(ad, i, sacc, e);
     }
     return;
   }
@@ -258,10 +260,9 @@ __device__ void compose_adam_block(const ComposeAdamArgs& a, int64_t cb, int64_t
     __syncthreads();
     if (threadIdx.x < 64 && h < H) {
       const int64_t i = a.off_e + (int64_t)k * H + h;
-      const AdamElem e = adam_load(ad, i, tn);
       const float gv = ((part[0][threadIdx.x] + part[1][threadIdx.x]) + part[2][threadIdx.x]) + part[3][threadIdx.x];
       a.g[i] = gv;
-      adam_apply(ad, i, gv, e);
+      if constexpr (ADAM) adam_apply(ad, i, gv, adam_load(ad, i, tn));
     }
     __syncthreads();
   }
@@ -280,30 +281,31 @@ __global__ __launch_bounds__(256) void compose_adam_kernel(ComposeAdamArgs a) {
                           (i >= a.off_e && i < a.off_e + (int64_t)a.K * a.H);
     if (i < a.n && !composed) adam_apply(ad, i, a.g[i], adam_load(ad, i, tn));
   } else {
-    compose_adam_block(a, (int64_t)blockIdx.x - nb, tn, part);
+    compose_adam_block<true>(a, (int64_t)blockIdx.x - nb, tn, part);
   }
   adam_ticket(ad.step, tn);
 }
 
-// The whole backward tail of a single-process step in ONE launch: grad_tail's blocks, each applying
-// Adam to the columns it has just reduced, then the composed decoder conv1's dW / dE blocks
-// (compose_adam_block).  Block order: [segment blocks][log_prior][loss finalize][composed].
-// The composed blocks need the whole reduced dWc: every block of the dWc segment releases its
-// columns (device-scope fence) and adds 1 << 48 to *step; a composed block spins (bounded, acquire
-// polls, one acquire fence after) until that field reaches the segment's block count.  All blocks are co-resident (a few
-// hundred 256-thread blocks) and the dWc blocks precede the waiting ones in dispatch order.  The
-// Adam ticket counts in bits 32..47; the last block rewrites *step = t, clearing both fields.
-__global__ __launch_bounds__(256) void tail_adam_kernel(TailArgs ta, ComposeAdamArgs a, int dwc_seg, int dwc_blocks) {
+// The whole backward tail in ONE launch: grad_tail's blocks (ADAM: each then applies Adam to the
+// columns it has just reduced), then the composed decoder conv1's dW / dE blocks
+// (compose_adam_block; ADAM: + their Adam).  Block order: [segment blocks][log_prior][loss
+// finalize][composed].  The composed blocks need the whole reduced dWc: every block of the dWc
+// segment releases its columns (device-scope fence) and adds 1 to *sync (zeroed by the step's
+// prologue); a composed block spins (bounded, relaxed polls, one acquire fence after) until *sync
+// reaches the segment's block count.  All blocks are co-resident (a few hundred 256-thread blocks)
+// and the dWc blocks precede the waiting ones in dispatch order.
+template <bool ADAM>
+__global__ __launch_bounds__(256) void tail_kernel(TailArgs ta, ComposeAdamArgs a, int dwc_seg, int dwc_blocks,
+                                                   unsigned long long* sync) {
   __shared__ float part[16][64];
   __shared__ float red[256];
   __shared__ float scratch[256];
   __shared__ float cpart[4][256];
   const AdamArgs& ad = a.adam;
-  const int64_t tn = (*ad.step & 0xffffffffll) + 1;
+  const int64_t tn = ADAM ? (*ad.step & 0xffffffffll) + 1 : 0;
   const int64_t nblk = ta.blk_start[ta.nseg];
   const int64_t b = blockIdx.x;
   const int64_t finb = nblk + (ta.q0slab ? 1 : 0), comp0 = finb + (ta.fin_loss ? 1 : 0);
-  auto* st = reinterpret_cast<unsigned long long*>(ad.step);
   if (b < nblk) {
     float v = 0.f;
     int64_t col;
@@ -313,15 +315,15 @@ __global__ __launch_bounds__(256) void tail_adam_kernel(TailArgs ta, ComposeAdam
       __syncthreads();
       if (threadIdx.x == 0) {
         __threadfence();
-        atomicAdd(st, 1ull << 48);
+        atomicAdd(sync, 1ull);
       }
-    } else if (threadIdx.x < 64 && col < sg.len) {
+    } else if (ADAM && threadIdx.x < 64 && col < sg.len) {
       const int64_t i = (sg.out - a.g) + col;
       adam_apply(ad, i, v, adam_load(ad, i, tn));
     }
   } else if (ta.q0slab && b == nblk) {
     tail_logprior_block(ta, red, scratch);
-    if (threadIdx.x == 0)
+    if (ADAM && threadIdx.x == 0)
       for (int k = 0; k < ta.lp.K; ++k) {
         const int64_t i = (ta.lp.out - a.g) + k;
         adam_apply(ad, i, ta.lp.out[k], adam_load(ad, i, tn));
@@ -334,31 +336,28 @@ __global__ __launch_bounds__(256) void tail_adam_kernel(TailArgs ta, ComposeAdam
     if (threadIdx.x == 0) {
       for (int spin = 0; spin < (1 << 22); ++spin) {
         // relaxed: an acquire load would invalidate this XCD's L2 on every poll
-        const unsigned long long w = __hip_atomic_load(st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((int)(w >> 48) >= dwc_blocks) break;
+        if (__hip_atomic_load(sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned long long)dwc_blocks) break;
         __builtin_amdgcn_s_sleep(1);
       }
     }
     __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    compose_adam_block(a, b - comp0, tn, cpart);
+    compose_adam_block<ADAM>(a, b - comp0, tn, cpart);
   }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned long long old = atomicAdd(st, 1ull << 32);
-    if (((old >> 32) & 0xffffull) == gridDim.x - 1) atomicExch(st, (unsigned long long)tn);
-  }
+  if constexpr (ADAM) adam_ticket(ad.step, tn);
 }
 
-int launch_tail_adam(TailArgs& ta, const ComposeAdamArgs& ca, int dwc_seg, hipStream_t s) {
-  if (ta.nseg > MAX_SEGS || (ta.q0slab && ta.lp.K > 256) || dwc_seg < 0 || dwc_seg >= ta.nseg) return VQHMM_EINVAL;
+int launch_tail(TailArgs& ta, const ComposeAdamArgs& ca, int dwc_seg, unsigned long long* sync, bool adam,
+                hipStream_t s) {
+  if (ta.nseg > MAX_SEGS || (ta.q0slab && ta.lp.K > 256) || dwc_seg < 0 || dwc_seg >= ta.nseg || !sync)
+    return VQHMM_EINVAL;
   ta.blk_start[0] = 0;
   for (int i = 0; i < ta.nseg; ++i) ta.blk_start[i + 1] = ta.blk_start[i] + cdiv(ta.s[i].len, 64);
   const int64_t ncomp = cdiv((int64_t)ca.H * ca.H * 3, 256) + ca.K;
   const int64_t nb = ta.blk_start[ta.nseg] + (ta.q0slab ? 1 : 0) + (ta.fin_loss ? 1 : 0) + ncomp;
-  if (nb >= 65536) return VQHMM_EUNSUPPORTED;  // ticket field
   const int dwc_blocks = (int)cdiv(ta.s[dwc_seg].len, 64);
-  tail_adam_kernel<<<(unsigned)nb, 256, 0, s>>>(ta, ca, dwc_seg, dwc_blocks);
+  if (adam) tail_kernel<true><<<(unsigned)nb, 256, 0, s>>>(ta, ca, dwc_seg, dwc_blocks, sync);
+  else tail_kernel<false><<<(unsigned)nb, 256, 0, s>>>(ta, ca, dwc_seg, dwc_blocks, sync);
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
 }
@@ -658,6 +657,7 @@ __device__ __forceinline__ void wimg_slice(const WImgJob& j, int64_t i0) {
 __global__ __launch_bounds__(256) void prologue_kernel(PrologueArgs a) {
   extern __shared__ float cs[];
   const unsigned bx = blockIdx.x;
+  if (bx == 0 && threadIdx.x == 0 && a.sync) *a.sync = 0ull;  // the backward tail's dWc counter
   if (bx < a.nbx) {
     to_pcl_slot(a.x, a.D, a.B, a.T, a.xsc, a.xst, a.xp, (int64_t)bx * 256 + threadIdx.x);
   } else if (bx < a.nbx + a.nbu) {
