@@ -144,17 +144,18 @@ def test_fused_tail_adam_bit_identical(B, K, D, H, H2, T):
     assert int(fused.step_dev.item()) == int(split.step_dev.item()) == 4
 
 
-_SPLIT_TAIL = r"""
+_SPLIT_RUN = r"""
 import sys, torch
 sys.path.insert(0, sys.argv[1])
 import vqhmm
+D, H, K, H2 = (int(v) for v in sys.argv[3].split(","))
 B, T = 96, 150
 gen = torch.Generator().manual_seed(5)
-x = torch.randn(B, 5, T, generator=gen).cuda()
+x = torch.randn(B, D, T, generator=gen).cuda()
 u = torch.randn(B, 4, T, generator=gen).cuda()
 L = torch.randint(30, T + 1, (B,), generator=gen)
 torch.manual_seed(3)
-m = vqhmm.VAE_HMM(5, 64, 3, 32, u_dim=4, trans_hidden=128).cuda()
+m = vqhmm.VAE_HMM(D, H, K, H2, u_dim=4, trans_hidden=128).cuda()
 st = vqhmm.TrainState(m, lr=1e-3)
 xs, us, Ls = st.prepare(x, u, L)
 for _ in range(2):
@@ -163,14 +164,14 @@ for _ in range(2):
 for _ in range(2):
     st.forward_backward_adam(xs, us, Ls, 0.5)
 torch.cuda.synchronize()
-torch.save({"grad": st.grad.cpu(), "flat": st.flat.cpu(), "m": st.exp_avg.cpu(), "v": st.exp_avg_sq.cpu()}, sys.argv[2])
+torch.save({"grad": st.grad.cpu(), "flat": st.flat.cpu(), "m": st.exp_avg.cpu(), "v": st.exp_avg_sq.cpu(),
+            "loss": st.loss.cpu()}, sys.argv[2])
 """
 
 
-def test_fused_tail_matches_separate_launches(tmp_path):
-    """The one-launch backward tail (tail_kernel, both the DP form and the Adam-fused form) gives
-    the same bits as grad_tail + compose_bwd / compose_adam as separate launches (VQHMM_TAIL_FUSED=0,
-    read once per process, so each side runs in its own process)."""
+def _run_both(tmp_path, env, dims):
+    """The same 4 steps in two fresh processes, env=1 and env=0 (the switches are read once per
+    process); loss, gradient, moments and parameters must agree bit for bit."""
     import os
     import subprocess
     import sys
@@ -178,9 +179,22 @@ def test_fused_tail_matches_separate_launches(tmp_path):
     pkg = os.path.join(ROOT, "vq-vae-hmm-model_amd")
     out = {}
     for flag in ("1", "0"):
-        f = str(tmp_path / f"tail{flag}.pt")
-        subprocess.run([sys.executable, "-c", _SPLIT_TAIL, pkg, f], check=True, timeout=300,
-                       env=dict(os.environ, VQHMM_TAIL_FUSED=flag))
+        f = str(tmp_path / f"{env}{flag}.pt")
+        subprocess.run([sys.executable, "-c", _SPLIT_RUN, pkg, f, ",".join(map(str, dims))], check=True,
+                       timeout=300, env=dict(os.environ, **{env: flag}))
         out[flag] = torch.load(f, weights_only=True)
-    for k in ("grad", "flat", "m", "v"):
+    for k in ("grad", "flat", "m", "v", "loss"):
         assert torch.equal(out["1"][k], out["0"][k]), k
+
+
+def test_fused_tail_matches_separate_launches(tmp_path):
+    """The one-launch backward tail (tail_kernel, both the DP form and the Adam-fused form) gives
+    the same bits as grad_tail + compose_bwd / compose_adam as separate launches (VQHMM_TAIL_FUSED=0)."""
+    _run_both(tmp_path, "VQHMM_TAIL_FUSED", (5, 64, 3, 32))
+
+
+@pytest.mark.parametrize("dims", [(5, 64, 3, 32), (16, 64, 8, 32), (5, 48, 4, 40)])
+def test_fused_conv_pairs_match_separate_launches(tmp_path, dims):
+    """enc_conv1 -> enc_conv2 and dec_conv1 -> dec_conv2 fused into one launch each (conv2f_kernel:
+    14-row tiles, the front rows computed in-tile) against the two-launch path (VQHMM_CONV_FUSE=0)."""
+    _run_both(tmp_path, "VQHMM_CONV_FUSE", dims)

@@ -125,18 +125,23 @@ __device__ __forceinline__ void c2_mfma_tile(const float* Ws, const float* Xw, i
 
 // Epilogue of one tile (ACT: 0 none, 1 ReLU, 2 ReLU-backward mask by aux, 3 none + the softmax
 // backward of the row, see ConvArgs::lb_*).
+// Rows of a 16-row block outside [rlo, rhi) get their values (acc) but no stores: the fused
+// front conv's halo rows and the rows past a 14-row fused tile belong to the neighbouring tiles.
 template <int NB, int PB, int ACT>
 __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a, int64_t m0, int wave, int lg4, int l16,
                                                f32x4 (&acc)[NB][PB], const float4 (&auxv)[NB][PB],
                                                const float (&bias_r)[NB][4], const float (&tw)[NB][4],
-                                               f32x4 tb0, float sc, bool tail) {
+                                               f32x4 tb0, float sc, bool tail, int rlo = 0, int rhi = 16) {
   // lane (lg4, l16) holds channels nb*16 + 4*lg4 + v of row m0 + (wave*PB+pb)*16 + l16
+  const bool own = l16 >= rlo && l16 < rhi;
 #pragma unroll
     for (int pb = 0; pb < PB; ++pb) {
       const int64_t r = m0 + (wave * PB + pb) * 16 + l16;
       int64_t b;
       int t;
       const bool valid = row_bt(r, a.R, a.T, b, t);
+      const bool st_r = own && r < a.R;  // this row is stored (PCL)
+      const bool st_v = own && valid;    // ... and is a valid position (CF)
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb) {
         f32x4 y;
@@ -158,7 +163,7 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a, int64_t m0, in
             float yk[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) yk[k] = __shfl(y[k], l16);
-            if (r < a.R) {
+            if (st_r) {
               const float lsc = a.lb_scale ? *a.lb_scale : 1.f;
               const float4 q4 = *reinterpret_cast<const float4*>(a.lb_q + r * 4);
               const float4 x4 = *reinterpret_cast<const float4*>(a.lb_dqx + r * 4);
@@ -198,8 +203,8 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a, int64_t m0, in
             }
           }
         }
-        if (a.out && r < a.R && n0 < ld4(a.N)) *reinterpret_cast<f32x4*>(a.out + r * ld4(a.N) + n0) = y;
-        if (a.out_cf && valid) {
+        if (a.out && st_r && n0 < ld4(a.N)) *reinterpret_cast<f32x4*>(a.out + r * ld4(a.N) + n0) = y;
+        if (a.out_cf && st_v) {
 #pragma unroll
           for (int v = 0; v < 4; ++v)
             if (n0 + v < a.N) a.out_cf[(b * a.N + n0 + v) * a.T + t] = y[v];
@@ -216,8 +221,8 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a, int64_t m0, in
         const int c0 = 4 * lg4;
 #pragma unroll
         for (int v = 0; v < 4; ++v) z[v] = valid ? z[v] : 0.f;
-        if (a.t_out && r < a.R && c0 < ld4(a.C2)) *reinterpret_cast<f32x4*>(a.t_out + r * ld4(a.C2) + c0) = z;
-        if (a.t_cf0 && valid) {
+        if (a.t_out && st_r && c0 < ld4(a.C2)) *reinterpret_cast<f32x4*>(a.t_out + r * ld4(a.C2) + c0) = z;
+        if (a.t_cf0 && st_v) {
 #pragma unroll
           for (int v = 0; v < 4; ++v) {
             const int c2 = c0 + v;
@@ -243,8 +248,8 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a, int64_t m0, in
           f32x4 qv;
 #pragma unroll
           for (int v = 0; v < 4; ++v) qv[v] = valid ? e[v] / s : 0.f;  // 0 in pad channels (e = 0)
-          if (a.q_out && r < a.R && c0 < ld4(a.C2)) *reinterpret_cast<f32x4*>(a.q_out + r * ld4(a.C2) + c0) = qv;
-          if (a.q_cf && valid) {
+          if (a.q_out && st_r && c0 < ld4(a.C2)) *reinterpret_cast<f32x4*>(a.q_out + r * ld4(a.C2) + c0) = qv;
+          if (a.q_cf && st_v) {
 #pragma unroll
             for (int v = 0; v < 4; ++v)
               if (c0 + v < a.C2) a.q_cf[(b * a.C2 + c0 + v) * a.T + t] = qv[v];
@@ -261,7 +266,7 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a, int64_t m0, in
               const int pi = __shfl_xor(bi, o);
               if (argmax_beats(pq, pi, bq, bi)) { bq = pq; bi = pi; }
             }
-            if (valid && lg4 == 0) a.reg_out[b * a.T + t] = bi;
+            if (st_v && lg4 == 0) a.reg_out[b * a.T + t] = bi;
           }
         }
       }
@@ -507,6 +512,175 @@ __global__ __launch_bounds__((64 * C2wOcc<NB, KCP>::MAXW)) void conv2w_kernel(Co
     conv2_epilogue<NB, 1, ACT>(a, m0, 0, lg4, l16, acc, auxv, bias_r, tw, tb0, sc, TAIL);
     tile = next;
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Fused pair: a k=3 ReLU "front" conv (<= 16 -> Kc channels, Kc <= 64) feeding this k=3 conv
+// (enc_conv1 -> enc_conv2 + to_logits, composed dec_conv1 -> dec_conv2 + to_params).  Tiles of 14
+// output rows; per tile the wave computes the front conv's 16 rows m0-1 .. m0+14 (one MFMA block
+// over 18 input rows in its X1 slot), stores its own rows m0 .. m0+13 to f_out (the backward needs
+// them), and writes all 16 into its X slot as this conv's input: the front activation is never
+// re-read from HBM and the front launch disappears.  Every front row goes through the unfused
+// launch's MFMA sequence and epilogue, so stored and consumed values are the same bits as the
+// two-launch path (a halo row is computed by both tiles that touch it, identically).
+template <int NB, bool TAIL>
+struct C2fCfg {
+  using C = C2wCfg<NB, 4, 3>;  // this conv: 33 .. 64 input channels
+  using F = C2wCfg<4, 1, 3>;   // front: <= 16 -> <= 64 channels
+  static constexpr int TR = 14;  // output rows per tile
+  static constexpr size_t lds(int wpg) {
+    return (C::W_FLOATS + C::E_FLOATS + F::W_FLOATS + 64 + (size_t)wpg * (F::X_FLOATS + C::X_FLOATS)) * 4;
+  }
+};
+
+template <int NB, bool TAIL>
+__global__ __launch_bounds__(64 * 12) void conv2f_kernel(ConvArgs a, int64_t ntiles) {
+  using Q = C2fCfg<NB, TAIL>;
+  using C = typename Q::C;
+  using F = typename Q::F;
+  constexpr int TR = Q::TR;
+  extern __shared__ float4 smem4[];
+  float* Ws = reinterpret_cast<float*>(smem4);  // this conv's image [3][NW][LDX]
+  float* Es = Ws + C::W_FLOATS;                 // bias, tail weight, tail bias
+  float* Fs = Es + C::E_FLOATS;                 // front image [3][64][F::LDX]
+  float* Fb = Fs + F::W_FLOATS;                 // front bias [64]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nwv = blockDim.x >> 6;
+  float* X1 = Fb + 64 + wave * (F::X_FLOATS + C::X_FLOATS);  // front input rows m0-2 .. m0+15
+  float* Xs = X1 + F::X_FLOATS;                                // front output rows m0-1 .. m0+14
+  const int lg4 = lane >> 4, l16 = lane & 15;
+
+  {
+    const float4* src = reinterpret_cast<const float4*>(a.Wimg);
+    for (int i = tid; i < (int)(C::W_FLOATS / 4); i += blockDim.x) smem4[i] = src[i];
+    const float4* fsrc = reinterpret_cast<const float4*>(a.f_Wimg);
+    float4* fdst = reinterpret_cast<float4*>(Fs);
+    for (int i = tid; i < (int)(F::W_FLOATS / 4); i += blockDim.x) fdst[i] = fsrc[i];
+  }
+  for (int i = tid; i < (int)C::E_FLOATS; i += blockDim.x) {
+    float v = 0.f;
+    if (i < C::NW) {
+      v = (a.bias && i < a.N) ? a.bias[i] : 0.f;
+    } else if (i < 17 * C::NW) {
+      const int j = i - C::NW, c2 = j / C::NW, n = j - c2 * C::NW;
+      v = (TAIL && c2 < a.C2 && n < a.N) ? a.tW[(int64_t)c2 * a.N + n] : 0.f;
+    } else {
+      const int c2 = i - 17 * C::NW;
+      v = (TAIL && a.tb && c2 < a.C2) ? a.tb[c2] : 0.f;
+    }
+    Es[i] = v;
+  }
+  for (int i = tid; i < 64; i += blockDim.x) Fb[i] = i < a.Kc ? a.f_bias[i] : 0.f;
+  // the front conv as an ordinary ConvArgs (input = this launch's src)
+  ConvArgs fa = a;
+  fa.Kc = a.f_Kc; fa.N = a.Kc; fa.out = a.f_out; fa.out_cf = nullptr; fa.scale = nullptr;
+  const float sc = a.scale ? *a.scale : 1.0f;
+
+  const int64_t stride = (int64_t)gridDim.x * nwv;
+  int64_t tile = (int64_t)wave * gridDim.x + blockIdx.x;
+  float4 pf[F::PF];
+#pragma unroll
+  for (int k = 0; k < F::PF; ++k) {
+    const int s = lane + k * 64;
+    pf[k] = x_raw(fa, tile * TR - 1, s < F::XF4 ? s : 0, F::KCW);
+  }
+  __syncthreads();  // weights; from here on the waves never wait for each other
+  const float4 aux0[4][1] = {};
+  while (tile < ntiles) {
+    const int64_t m0 = tile * TR;
+#pragma unroll
+    for (int k = 0; k < F::PF; ++k) {
+      const int s = lane + k * 64;
+      if (s < F::XF4) {
+        const int row = s / (F::KCW / 4), c = (s - row * (F::KCW / 4)) * 4;
+        *reinterpret_cast<float4*>(X1 + row * F::LDX + c) = x_mask(fa, m0 - 1, s, F::KCW, pf[k]);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    const int64_t next = tile + stride;
+    {  // unconditional prefetch, as in conv2w_kernel
+      const int64_t pt = next < ntiles ? next : tile;
+#pragma unroll
+      for (int k = 0; k < F::PF; ++k) {
+        const int s = lane + k * 64;
+        pf[k] = x_raw(fa, pt * TR - 1, s < F::XF4 ? s : 0, F::KCW);
+      }
+    }
+    // ---- front conv: rows m0-1 .. m0+14
+    f32x4 acc1[4][1];
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) acc1[nb][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+    c2_mfma_tile<4, 1, 1, 3, F::LDX, F::NW>(Fs, X1, lg4, l16, acc1, a.pipe);
+    {
+      float b1[4][4], tw0[4][4] = {};
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        const float4 b4 = *reinterpret_cast<const float4*>(Fb + nb * 16 + 4 * lg4);
+        b1[nb][0] = b4.x; b1[nb][1] = b4.y; b1[nb][2] = b4.z; b1[nb][3] = b4.w;
+      }
+      conv2_epilogue<4, 1, 1>(fa, m0 - 1, 0, lg4, l16, acc1, aux0, b1, tw0, f32x4{0.f, 0.f, 0.f, 0.f}, 1.0f, false,
+                              1, TR + 1);
+    }
+    // activated rows (0 outside sequences) -> this conv's input slot
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) *reinterpret_cast<f32x4*>(Xs + l16 * C::LDX + nb * 16 + 4 * lg4) = acc1[nb][0];
+    __builtin_amdgcn_wave_barrier();
+    // ---- this conv: rows m0 .. m0+13 (block rows 14, 15 are the next tile's: not stored)
+    f32x4 acc[NB][1];
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) acc[nb][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+    c2_mfma_tile<NB, 1, 4, 3, C::LDX, C::NW>(Ws, Xs, lg4, l16, acc, a.pipe);
+    __builtin_amdgcn_wave_barrier();  // the slots' reads are done before the next tile overwrites them
+    float bias_r[NB][4], tw[NB][4];
+    f32x4 tb0 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      const float4 b4 = *reinterpret_cast<const float4*>(Es + nb * 16 + 4 * lg4);
+      bias_r[nb][0] = b4.x; bias_r[nb][1] = b4.y; bias_r[nb][2] = b4.z; bias_r[nb][3] = b4.w;
+      if constexpr (TAIL) {
+        const float4 t4 = *reinterpret_cast<const float4*>(Es + C::NW + l16 * C::NW + nb * 16 + 4 * lg4);
+        tw[nb][0] = t4.x; tw[nb][1] = t4.y; tw[nb][2] = t4.z; tw[nb][3] = t4.w;
+      }
+    }
+    if constexpr (TAIL) {
+      const float4 t4 = *reinterpret_cast<const float4*>(Es + 17 * C::NW + 4 * lg4);
+      tb0 = f32x4{t4.x, t4.y, t4.z, t4.w};
+    }
+    const float4 auxv[NB][1] = {};
+    conv2_epilogue<NB, 1, 1>(a, m0, 0, lg4, l16, acc, auxv, bias_r, tw, tb0, sc, TAIL, 0, TR);
+    tile = next;
+  }
+}
+
+template <int NB, bool TAIL>
+static int launch_c2f(const ConvArgs& a, hipStream_t s) {
+  using Q = C2fCfg<NB, TAIL>;
+  ConvArgs ap = a;
+  ap.pipe = 1;
+  const int64_t ntiles = cdiv(a.R, Q::TR);
+  int wmax = 12;
+  while (wmax > 1 && Q::lds(wmax) > 160 * 1024) --wmax;
+  if (Q::lds(wmax) > 160 * 1024) return VQHMM_EUNSUPPORTED;
+  const int64_t want = cdiv(ntiles, 256);
+  const int wpg = (int)(want < wmax ? (want > 0 ? want : 1) : wmax);
+  const int64_t grid = cdiv(ntiles, wpg) < 256 ? cdiv(ntiles, wpg) : 256;
+  conv2f_kernel<NB, TAIL><<<(unsigned)grid, 64 * wpg, Q::lds(wpg), s>>>(ap, ntiles);
+  VQHMM_LAUNCH_CHECK();
+  return VQHMM_OK;
+}
+
+bool conv2_fused_supported(const ConvArgs& a) {
+  return a.f_Wimg && a.Wimg && a.f_bias && a.f_out && !a.src_cf && a.ks == 3 && a.act == 1 && a.f_Kc >= 1 &&
+         a.f_Kc <= 16 && a.Kc > 32 && a.Kc <= 64 && a.N <= 64 && (a.tW == nullptr || a.C2 <= 16) && !a.out_cf;
+}
+
+int launch_conv2_fused(const ConvArgs& a, hipStream_t s) {
+  if (!conv2_fused_supported(a)) return VQHMM_EUNSUPPORTED;
+  if (a.R == 0) return VQHMM_OK;
+  const bool tail = a.tW != nullptr;
+  if (a.N <= 16) return tail ? launch_c2f<1, true>(a, s) : launch_c2f<1, false>(a, s);
+  if (a.N <= 32) return tail ? launch_c2f<2, true>(a, s) : launch_c2f<2, false>(a, s);
+  return tail ? launch_c2f<4, true>(a, s) : launch_c2f<4, false>(a, s);
 }
 
 // Kernel choice: VQHMM_CONV=wg | wave forces one (A/B), else the wave kernel below

@@ -49,6 +49,13 @@ struct ConvArgs {
   float* lb_dh;
   int lb_C;
   int pipe;          // conv2 kernels: software-pipelined operand reads (set by the launcher)
+  // fused front conv (conv2w only, f_Wimg set): src is the INPUT of a k=3 ReLU conv f_Kc -> Kc
+  // (f_Kc <= 16, Kc <= 64; weights packed in conv2w<4, 1, 3>'s image layout), whose output rows
+  // are written to f_out (PCL, ld4(Kc)) and feed this conv from LDS, never re-read from HBM
+  int f_Kc;
+  const float* f_Wimg;
+  const float* f_bias;
+  float* f_out;
 };
 
 // Loss normalisers of compute_loss (VQ_VAE_HMM_fixed.py:120 mask.sum()*C, :131/:135 B).
@@ -171,6 +178,9 @@ int launch_vq_argmin(const float* z, int64_t B, int64_t Dv, int64_t T, const flo
                      float* dmin, hipStream_t s);
 int launch_conv(const ConvArgs& a, hipStream_t s);
 bool conv2_supported(const ConvArgs& a);
+// front conv + this conv in one launch (conv2.hip conv2f_kernel; ConvArgs::f_*)
+bool conv2_fused_supported(const ConvArgs& a);
+int launch_conv2_fused(const ConvArgs& a, hipStream_t s);
 // Packed weight image of a conv2_kernel launch: img[(tap*NW + n)*LDX + c] = Weff(n, c, tap)
 // (zero past N / Kc), NW = 16*NB and LDX = 16*KCP + 4 for the launch's (NB, KCP) (c2_nb / c2_kcp).
 // Built once per step (prologue), so every workgroup stages its weights with float4 copies.
