@@ -475,12 +475,14 @@ int make_tail(const ElboPlan& p, const StepCtx& c, TailArgs& ta) {
   return dwc_seg;
 }
 
-// enc_conv1 -> enc_conv2 and the composed dec_conv1 -> dec_conv2 as one launch each
+// enc_conv1 -> enc_conv2, the composed dec_conv1 -> dec_conv2 and to_params_dgrad -> dec_conv2_dgrad
+// as one launch each
 // (conv2.hip conv2f_kernel); VQHMM_CONV_FUSE=0 keeps two launches (A/B), read once.
 ConvArgs fused_pair(const ElboPlan& p, const float* const* w, int st) {
   ConvArgs a = conv_of(p, w, st);
   const ConvArgs f = conv_of(p, w, st - 1);
-  a.src = f.src; a.f_Kc = f.Kc; a.f_Wimg = f.Wimg; a.f_bias = f.bias; a.f_out = f.out;
+  a.src = f.src; a.f_Kc = f.Kc; a.f_ks = f.ks; a.f_act = f.act; a.f_Wimg = f.Wimg; a.f_bias = f.bias;
+  a.f_aux = f.aux; a.f_out = f.out;
   return a;
 }
 bool front_fused(const ElboPlan& p, const float* const* w, int st) {
@@ -488,7 +490,7 @@ bool front_fused(const ElboPlan& p, const float* const* w, int st) {
     const char* e = getenv("VQHMM_CONV_FUSE");
     return !e || atoi(e) != 0;
   }();
-  return on && (st == S_ENC2 || st == S_DEC2) && conv2_fused_supported(fused_pair(p, w, st));
+  return on && (st == S_ENC2 || st == S_DEC2 || st == S_DEC2_DG) && conv2_fused_supported(fused_pair(p, w, st));
 }
 
 // VQHMM_TAIL_FUSED=0: grad_tail and compose_bwd / compose_adam as two launches (A/B); read once
@@ -526,7 +528,14 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
     case S_ENC2: case S_DEC2:
       if (front_fused(p, w, st)) return launch_conv2_fused(fused_pair(p, w, st), s);
       return launch_conv(conv_of(p, w, st), s);
-    case S_DEC2_DG: case S_ENC2_DG:
+    case S_DEC2_DG:
+      if (front_fused(p, w, st)) {
+        ConvArgs a = fused_pair(p, w, st);
+        a.f_scale = c.gscale;  // the front is S_PAR_DG
+        return launch_conv2_fused(a, s);
+      }
+      return launch_conv(conv_of(p, w, st), s);
+    case S_ENC2_DG:
       return launch_conv(conv_of(p, w, st), s);
     case S_LOGIT_DG:
       if (logits_dg_fused(p)) return VQHMM_OK;  // ran in S_DEC1_DG's epilogue
@@ -543,6 +552,7 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       return launch_conv(a, s);
     }
     case S_PAR_DG: {
+      if (front_fused(p, w, S_DEC2_DG)) return VQHMM_OK;  // runs inside S_DEC2_DG's launch
       ConvArgs a = conv_of(p, w, st);
       a.scale = c.gscale;  // dpar is the head's gradient for dloss = 1
       return launch_conv(a, s);

@@ -523,19 +523,19 @@ __global__ __launch_bounds__((64 * C2wOcc<NB, KCP>::MAXW)) void conv2w_kernel(Co
 // re-read from HBM and the front launch disappears.  Every front row goes through the unfused
 // launch's MFMA sequence and epilogue, so stored and consumed values are the same bits as the
 // two-launch path (a halo row is computed by both tiles that touch it, identically).
-template <int NB, bool TAIL>
+template <int NB, bool TAIL, int FKS>
 struct C2fCfg {
-  using C = C2wCfg<NB, 4, 3>;  // this conv: 33 .. 64 input channels
-  using F = C2wCfg<4, 1, 3>;   // front: <= 16 -> <= 64 channels
+  using C = C2wCfg<NB, 4, 3>;   // this conv: 33 .. 64 input channels
+  using F = C2wCfg<4, 1, FKS>;  // front: <= 16 -> <= 64 channels
   static constexpr int TR = 14;  // output rows per tile
   static constexpr size_t lds(int wpg) {
     return (C::W_FLOATS + C::E_FLOATS + F::W_FLOATS + 64 + (size_t)wpg * (F::X_FLOATS + C::X_FLOATS)) * 4;
   }
 };
 
-template <int NB, bool TAIL>
+template <int NB, bool TAIL, int FKS, int ACT>
 __global__ __launch_bounds__(64 * 12) void conv2f_kernel(ConvArgs a, int64_t ntiles) {
-  using Q = C2fCfg<NB, TAIL>;
+  using Q = C2fCfg<NB, TAIL, FKS>;
   using C = typename Q::C;
   using F = typename Q::F;
   constexpr int TR = Q::TR;
@@ -570,11 +570,13 @@ __global__ __launch_bounds__(64 * 12) void conv2f_kernel(ConvArgs a, int64_t nti
     }
     Es[i] = v;
   }
-  for (int i = tid; i < 64; i += blockDim.x) Fb[i] = i < a.Kc ? a.f_bias[i] : 0.f;
+  for (int i = tid; i < 64; i += blockDim.x) Fb[i] = (a.f_bias && i < a.Kc) ? a.f_bias[i] : 0.f;
   // the front conv as an ordinary ConvArgs (input = this launch's src)
   ConvArgs fa = a;
-  fa.Kc = a.f_Kc; fa.N = a.Kc; fa.out = a.f_out; fa.out_cf = nullptr; fa.scale = nullptr;
+  fa.Kc = a.f_Kc; fa.N = a.Kc; fa.out = a.f_out; fa.out_cf = nullptr; fa.scale = a.f_scale; fa.aux = a.f_aux;
   const float sc = a.scale ? *a.scale : 1.0f;
+  const float fsc = fa.scale ? *fa.scale : 1.0f;
+  const int ldn1 = ld4(fa.N), ldn = ld4(a.N);
 
   const int64_t stride = (int64_t)gridDim.x * nwv;
   int64_t tile = (int64_t)wave * gridDim.x + blockIdx.x;
@@ -585,9 +587,20 @@ __global__ __launch_bounds__(64 * 12) void conv2f_kernel(ConvArgs a, int64_t nti
     pf[k] = x_raw(fa, tile * TR - 1, s < F::XF4 ? s : 0, F::KCW);
   }
   __syncthreads();  // weights; from here on the waves never wait for each other
-  const float4 aux0[4][1] = {};
   while (tile < ntiles) {
     const int64_t m0 = tile * TR;
+    // ReLU masks of both epilogues (ACT = 2), older than the prefetch in the vmcnt order
+    float4 aux1[4][1] = {}, auxv[NB][1] = {};
+    if constexpr (ACT == 2) {
+      const int64_t r1 = m0 - 1 + l16, r = m0 + l16;
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb)
+        aux1[nb][0] = *reinterpret_cast<const float4*>(fa.aux + (r1 < 0 ? 0 : (r1 < a.R ? r1 : a.R - 1)) * ldn1 +
+                                                       min(nb * 16 + 4 * lg4, ldn1 - 4));
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb)
+        auxv[nb][0] = *reinterpret_cast<const float4*>(a.aux + (r < a.R ? r : a.R - 1) * ldn + min(nb * 16 + 4 * lg4, ldn - 4));
+    }
 #pragma unroll
     for (int k = 0; k < F::PF; ++k) {
       const int s = lane + k * 64;
@@ -610,7 +623,7 @@ __global__ __launch_bounds__(64 * 12) void conv2f_kernel(ConvArgs a, int64_t nti
     f32x4 acc1[4][1];
 #pragma unroll
     for (int nb = 0; nb < 4; ++nb) acc1[nb][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-    c2_mfma_tile<4, 1, 1, 3, F::LDX, F::NW>(Fs, X1, lg4, l16, acc1, a.pipe);
+    c2_mfma_tile<4, 1, 1, FKS, F::LDX, F::NW>(Fs, X1, lg4, l16, acc1, a.pipe);
     {
       float b1[4][4], tw0[4][4] = {};
 #pragma unroll
@@ -618,8 +631,8 @@ __global__ __launch_bounds__(64 * 12) void conv2f_kernel(ConvArgs a, int64_t nti
         const float4 b4 = *reinterpret_cast<const float4*>(Fb + nb * 16 + 4 * lg4);
         b1[nb][0] = b4.x; b1[nb][1] = b4.y; b1[nb][2] = b4.z; b1[nb][3] = b4.w;
       }
-      conv2_epilogue<4, 1, 1>(fa, m0 - 1, 0, lg4, l16, acc1, aux0, b1, tw0, f32x4{0.f, 0.f, 0.f, 0.f}, 1.0f, false,
-                              1, TR + 1);
+      conv2_epilogue<4, 1, ACT>(fa, m0 - 1, 0, lg4, l16, acc1, aux1, b1, tw0, f32x4{0.f, 0.f, 0.f, 0.f}, fsc, false,
+                                1, TR + 1);
     }
     // activated rows (0 outside sequences) -> this conv's input slot
 #pragma unroll
@@ -646,15 +659,14 @@ __global__ __launch_bounds__(64 * 12) void conv2f_kernel(ConvArgs a, int64_t nti
       const float4 t4 = *reinterpret_cast<const float4*>(Es + 17 * C::NW + 4 * lg4);
       tb0 = f32x4{t4.x, t4.y, t4.z, t4.w};
     }
-    const float4 auxv[NB][1] = {};
-    conv2_epilogue<NB, 1, 1>(a, m0, 0, lg4, l16, acc, auxv, bias_r, tw, tb0, sc, TAIL, 0, TR);
+    conv2_epilogue<NB, 1, ACT>(a, m0, 0, lg4, l16, acc, auxv, bias_r, tw, tb0, sc, TAIL, 0, TR);
     tile = next;
   }
 }
 
-template <int NB, bool TAIL>
+template <int NB, bool TAIL, int FKS, int ACT>
 static int launch_c2f(const ConvArgs& a, hipStream_t s) {
-  using Q = C2fCfg<NB, TAIL>;
+  using Q = C2fCfg<NB, TAIL, FKS>;
   ConvArgs ap = a;
   ap.pipe = 1;
   const int64_t ntiles = cdiv(a.R, Q::TR);
@@ -664,23 +676,27 @@ static int launch_c2f(const ConvArgs& a, hipStream_t s) {
   const int64_t want = cdiv(ntiles, 256);
   const int wpg = (int)(want < wmax ? (want > 0 ? want : 1) : wmax);
   const int64_t grid = cdiv(ntiles, wpg) < 256 ? cdiv(ntiles, wpg) : 256;
-  conv2f_kernel<NB, TAIL><<<(unsigned)grid, 64 * wpg, Q::lds(wpg), s>>>(ap, ntiles);
+  conv2f_kernel<NB, TAIL, FKS, ACT><<<(unsigned)grid, 64 * wpg, Q::lds(wpg), s>>>(ap, ntiles);
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
 }
 
 bool conv2_fused_supported(const ConvArgs& a) {
-  return a.f_Wimg && a.Wimg && a.f_bias && a.f_out && !a.src_cf && a.ks == 3 && a.act == 1 && a.f_Kc >= 1 &&
+  const bool relu_pair = a.act == 1 && a.f_act == 1 && a.f_ks == 3;                        // forward
+  const bool mask_pair = a.act == 2 && a.f_act == 2 && a.f_ks == 1 && a.aux && a.f_aux && !a.tW;  // data grad
+  return a.f_Wimg && a.Wimg && a.f_out && !a.src_cf && a.ks == 3 && (relu_pair || mask_pair) && a.f_Kc >= 1 &&
          a.f_Kc <= 16 && a.Kc > 32 && a.Kc <= 64 && a.N <= 64 && (a.tW == nullptr || a.C2 <= 16) && !a.out_cf;
 }
 
 int launch_conv2_fused(const ConvArgs& a, hipStream_t s) {
   if (!conv2_fused_supported(a)) return VQHMM_EUNSUPPORTED;
   if (a.R == 0) return VQHMM_OK;
+  if (a.act == 2) return a.N <= 64 && a.N > 32 ? launch_c2f<4, false, 1, 2>(a, s)
+                         : a.N > 16 ? launch_c2f<2, false, 1, 2>(a, s) : launch_c2f<1, false, 1, 2>(a, s);
   const bool tail = a.tW != nullptr;
-  if (a.N <= 16) return tail ? launch_c2f<1, true>(a, s) : launch_c2f<1, false>(a, s);
-  if (a.N <= 32) return tail ? launch_c2f<2, true>(a, s) : launch_c2f<2, false>(a, s);
-  return tail ? launch_c2f<4, true>(a, s) : launch_c2f<4, false>(a, s);
+  if (a.N <= 16) return tail ? launch_c2f<1, true, 3, 1>(a, s) : launch_c2f<1, false, 3, 1>(a, s);
+  if (a.N <= 32) return tail ? launch_c2f<2, true, 3, 1>(a, s) : launch_c2f<2, false, 3, 1>(a, s);
+  return tail ? launch_c2f<4, true, 3, 1>(a, s) : launch_c2f<4, false, 3, 1>(a, s);
 }
 
 // Kernel choice: VQHMM_CONV=wg | wave forces one (A/B), else the wave kernel below

@@ -49,12 +49,16 @@ struct ConvArgs {
   float* lb_dh;
   int lb_C;
   int pipe;          // conv2 kernels: software-pipelined operand reads (set by the launcher)
-  // fused front conv (conv2w only, f_Wimg set): src is the INPUT of a k=3 ReLU conv f_Kc -> Kc
+  // fused front conv (conv2f only, f_Wimg set): src is the INPUT of a k=3 ReLU conv f_Kc -> Kc
   // (f_Kc <= 16, Kc <= 64; weights packed in conv2w<4, 1, 3>'s image layout), whose output rows
   // are written to f_out (PCL, ld4(Kc)) and feed this conv from LDS, never re-read from HBM
-  int f_Kc;
+  // (or, f_ks = 1 / f_act = 2 with this conv's act = 2: a 1x1 data-gradient front with the ReLU
+  // mask f_aux, scaled by *f_scale, feeding a masked k=3 data gradient)
+  int f_Kc, f_ks, f_act;
   const float* f_Wimg;
   const float* f_bias;
+  const float* f_aux;
+  const float* f_scale;
   float* f_out;
 };
 
