@@ -718,10 +718,20 @@ int vqhmm_elbo_stage_info(const vqhmm_dims_t* d, int64_t B, int64_t T, int stage
                           double* flops, double* bytes, int* mfma_bound) {
   if (!dims_ok(d) || stage < 0 || stage >= S_COUNT || B <= 0 || T <= 0) return VQHMM_EINVAL;
   ElboPlan p = plan_elbo(d, B, T, nullptr);
+  // fused conv pairs: decided on a plan with (never dereferenced) workspace addresses
+  const int pair_of = stage == S_ENC1 ? S_ENC2 : stage == S_DEC1 ? S_DEC2 : stage == S_PAR_DG ? S_DEC2_DG : stage;
+  const bool fused_front = (pair_of == S_ENC2 || pair_of == S_DEC2 || pair_of == S_DEC2_DG) &&
+                           front_fused(plan_elbo(d, B, T, reinterpret_cast<void*>(4096)), nullptr, pair_of);
   if (name && name_len) {
     const char* nm = kStageNames[stage];
     if (p.wgroup && stage == S_W_ENC1) nm = "wgrad_group(all 6 weight gradients)";
     else if (p.wgroup && stage >= S_W_PAR && stage < S_W_ENC1) nm = "(wgrad: in wgrad_group)";
+    else if (fused_front && (stage == S_ENC1 || stage == S_DEC1 || stage == S_PAR_DG))
+      nm = stage == S_ENC1 ? "(enc_conv1: in enc_conv2's launch)"
+           : stage == S_DEC1 ? "(dec_conv1: in dec_conv2's launch)" : "(to_params_dgrad: in dec_conv2_dgrad's launch)";
+    else if (fused_front && stage == S_ENC2) nm = "enc_conv1+enc_conv2+to_logits";
+    else if (fused_front && stage == S_DEC2) nm = "dec_conv1+dec_conv2+to_params";
+    else if (fused_front && stage == S_DEC2_DG) nm = "to_params_dgrad+dec_conv2_dgrad";
     else if (tail_fused_on() && stage == S_REDUCE) nm = "(grad_tail: in the tail launch)";
     else if (tail_fused_on() && stage == S_COMPOSE_BWD) nm = "tail(grad_tail+compose_bwd[+adam])";
     strncpy(name, nm, name_len - 1);
@@ -730,6 +740,24 @@ int vqhmm_elbo_stage_info(const vqhmm_dims_t* d, int64_t B, int64_t T, int stage
   double f, b;
   int m;
   stage_work(p, stage, &f, &b, &m);
+  if (fused_front && pair_of != stage) {
+    f = 0; b = 0;  // counted with the launch it runs in
+  } else if (fused_front) {
+    double f1, b1;
+    int m1;
+    stage_work(p, stage == S_ENC2 ? S_ENC1 : stage == S_DEC2 ? S_DEC1 : S_PAR_DG, &f1, &b1, &m1);
+    f += f1;
+    b += b1;
+  }
+  if (tail_fused_on() && stage == S_REDUCE) {
+    f = 0; b = 0;
+  } else if (tail_fused_on() && stage == S_COMPOSE_BWD) {
+    double f1, b1;
+    int m1;
+    stage_work(p, S_REDUCE, &f1, &b1, &m1);
+    f += f1;
+    b += b1;
+  }
   if (flops) *flops = f;
   if (bytes) *bytes = b;
   if (mfma_bound) *mfma_bound = m;
