@@ -225,8 +225,10 @@ int launch_grad_tail(TailArgs& a, hipStream_t s) {
 // row k each, dE[k][h] with 4 thread groups splitting o (combined in a fixed order), then Adam.
 // composed decoder conv1: element block cb < cdiv(H*H*3, 256) of dW (256 elements), else row
 // k = cb - that of dE; gradient into g, then Adam (compose_adam_kernel / tail_adam_kernel)
+// pre: this thread's Adam element of a dW block, already loaded (or null)
 template <bool ADAM>
-__device__ void compose_adam_block(const ComposeAdamArgs& a, int64_t cb, int64_t tn, float (&part)[4][256]) {
+__device__ void compose_adam_block(const ComposeAdamArgs& a, int64_t cb, int64_t tn, float (&part)[4][256],
+                                   const AdamElem* pre = nullptr) {
   const AdamArgs& ad = a.adam;
   const int H = a.H, K = a.K;
   const int64_t nw = cdiv((int64_t)H * H * 3, 256);
@@ -235,7 +237,7 @@ __device__ void compose_adam_block(const ComposeAdamArgs& a, int64_t cb, int64_t
     if (j < (int64_t)H * H * 3) {
       const int64_t i = a.off_w + j;
       AdamElem e{};
-      if constexpr (ADAM) e = adam_load(ad, i, tn);
+      if constexpr (ADAM) e = pre ? *pre : adam_load(ad, i, tn);
       const int o = (int)(j / (3 * H)), rem = (int)(j - (int64_t)o * 3 * H), h = rem / 3, tap = rem - 3 * h;
       float sacc = 0.f;
 #pragma unroll 4
@@ -307,6 +309,13 @@ __global__ __launch_bounds__(256) void tail_kernel(TailArgs ta, ComposeAdamArgs 
   const int64_t b = blockIdx.x;
   const int64_t finb = nblk + (ta.q0slab ? 1 : 0), comp0 = finb + (ta.fin_loss ? 1 : 0);
   if (b < nblk) {
+    AdamElem e{};
+    if constexpr (ADAM) {  // this column's Adam operands in flight across the slab reduction
+      int sj = 0;
+      while (sj + 1 < ta.nseg && b >= ta.blk_start[sj + 1]) ++sj;
+      const int64_t c = (b - ta.blk_start[sj]) * 64 + threadIdx.x;
+      if (sj != dwc_seg && threadIdx.x < 64 && c < ta.s[sj].len) e = adam_load(ad, (ta.s[sj].out - a.g) + c, tn);
+    }
     float v = 0.f;
     int64_t col;
     const int si = tail_segment_block(ta, part, &v, &col);
@@ -318,8 +327,7 @@ __global__ __launch_bounds__(256) void tail_kernel(TailArgs ta, ComposeAdamArgs 
         atomicAdd(sync, 1ull);
       }
     } else if (ADAM && threadIdx.x < 64 && col < sg.len) {
-      const int64_t i = (sg.out - a.g) + col;
-      adam_apply(ad, i, v, adam_load(ad, i, tn));
+      adam_apply(ad, (sg.out - a.g) + col, v, e);
     }
   } else if (ta.q0slab && b == nblk) {
     tail_logprior_block(ta, red, scratch);
@@ -333,6 +341,10 @@ __global__ __launch_bounds__(256) void tail_kernel(TailArgs ta, ComposeAdamArgs 
     finalize_loss_block(ta.fin_part, ta.fin_nblk, nullptr, ta.lp.norm, ta.fin_B, ta.fin_T, ta.fin_D, ta.lp.beta,
                         ta.fin_loss, ta.fin_accum, ta.fin_pieces, fred, ta.fin_cnt);
   } else {
+    const int64_t cb = b - comp0, jw = cb * 256 + threadIdx.x;
+    const bool dw = cb < cdiv((int64_t)a.H * a.H * 3, 256) && jw < (int64_t)a.H * a.H * 3;
+    AdamElem e{};
+    if (ADAM && dw) e = adam_load(ad, a.off_w + jw, tn);  // in flight across the wait
     if (threadIdx.x == 0) {
       for (int spin = 0; spin < (1 << 22); ++spin) {
         // relaxed: an acquire load would invalidate this XCD's L2 on every poll
@@ -342,7 +354,7 @@ __global__ __launch_bounds__(256) void tail_kernel(TailArgs ta, ComposeAdamArgs 
     }
     __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    compose_adam_block<ADAM>(a, b - comp0, tn, cpart);
+    compose_adam_block<ADAM>(a, cb, tn, cpart, dw ? &e : nullptr);
   }
   if constexpr (ADAM) adam_ticket(ad.step, tn);
 }
