@@ -91,6 +91,45 @@ __device__ __forceinline__ bool argmax_beats(float v, int i, float bv, int bi) {
   return v > bv || (v == bv && i < bi);
 }
 
+// Sums over the 64 lanes on the VALU (DPP quad / half-row / row rotations, then the permlane
+// swaps): every lane ends with the same bits (each step adds a lane's value and its partner's,
+// and a + b == b + a), no LDS round trip.  A fixed order, different from wave_sum's.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v += __builtin_bit_cast(float, dpp_u32<0xB1>(__builtin_bit_cast(uint32_t, v)));   // quad_perm [1,0,3,2]
+  v += __builtin_bit_cast(float, dpp_u32<0x4E>(__builtin_bit_cast(uint32_t, v)));   // quad_perm [2,3,0,1]
+  v += __builtin_bit_cast(float, dpp_u32<0x141>(__builtin_bit_cast(uint32_t, v)));  // row_half_mirror
+  v += __builtin_bit_cast(float, dpp_u32<0x128>(__builtin_bit_cast(uint32_t, v)));  // row_ror:8
+  float2 r = pair16(v);
+  v = r.x + r.y;
+  r = pair32(v);
+  return r.x + r.y;
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint64_t lo = dpp_u32<CTRL>((uint32_t)u), hi = dpp_u32<CTRL>((uint32_t)(u >> 32));
+  return __builtin_bit_cast(double, (hi << 32) | lo);
+}
+__device__ __forceinline__ double xor_f64_16or32(double v, bool b32) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = b32 ? xor32<uint32_t>((uint32_t)u) : xor16<uint32_t>((uint32_t)u);
+  const uint32_t hi = b32 ? xor32<uint32_t>((uint32_t)(u >> 32)) : xor16<uint32_t>((uint32_t)(u >> 32));
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+  v += dpp_f64<0xB1>(v);
+  v += dpp_f64<0x4E>(v);
+  v += dpp_f64<0x141>(v);
+  v += dpp_f64<0x128>(v);
+  v += xor_f64_16or32(v, false);
+  v += xor_f64_16or32(v, true);
+  return v;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);

@@ -294,8 +294,10 @@ __global__ __launch_bounds__(256, (C2Occ<NB, KCP, TAIL>::W)) void conv2_kernel(C
   // ---- weights once: Ws[tap][n][c] = Weff(n, c, tap)
   if (a.Wimg) {  // the step's prologue packed them in exactly this layout: float4 copy
     const float4* src = reinterpret_cast<const float4*>(a.Wimg);
+#pragma unroll 8  // independent load -> store iterations: keep 8 loads in flight
     for (int i = tid; i < (int)(C::W_FLOATS / 4); i += 256) smem4[i] = src[i];
   } else {
+#pragma unroll 8  // independent load -> store iterations: keep 8 loads in flight
     for (int i = tid; i < KS * C::NW * C::KCW; i += 256) {
       const int c = i % C::KCW, n = (i / C::KCW) % C::NW, tap = i / (C::KCW * C::NW);
       float v = 0.f;
@@ -422,8 +424,10 @@ __global__ __launch_bounds__((64 * C2wOcc<NB, KCP>::MAXW)) void conv2w_kernel(Co
 
   if (a.Wimg) {
     const float4* src = reinterpret_cast<const float4*>(a.Wimg);
+#pragma unroll 8  // independent load -> store iterations: keep 8 loads in flight
     for (int i = tid; i < (int)(C::W_FLOATS / 4); i += blockDim.x) smem4[i] = src[i];
   } else {
+#pragma unroll 8  // independent load -> store iterations: keep 8 loads in flight
     for (int i = tid; i < KS * C::NW * C::KCW; i += blockDim.x) {
       const int c = i % C::KCW, n = (i / C::KCW) % C::NW, tap = i / (C::KCW * C::NW);
       float v = 0.f;
@@ -433,6 +437,7 @@ __global__ __launch_bounds__((64 * C2wOcc<NB, KCP>::MAXW)) void conv2w_kernel(Co
     }
   }
   // epilogue constants in LDS (read back per tile: registers go to the MFMA loop's prefetch)
+#pragma unroll 8  // independent load -> store iterations: keep 8 loads in flight
   for (int i = tid; i < (int)C::E_FLOATS; i += blockDim.x) {
     float v = 0.f;
     if (i < C::NW) {
@@ -552,11 +557,14 @@ __global__ __launch_bounds__(64 * 12) void conv2f_kernel(ConvArgs a, int64_t nti
 
   {
     const float4* src = reinterpret_cast<const float4*>(a.Wimg);
+#pragma unroll 8  // independent load -> store iterations: keep 8 loads in flight
     for (int i = tid; i < (int)(C::W_FLOATS / 4); i += blockDim.x) smem4[i] = src[i];
     const float4* fsrc = reinterpret_cast<const float4*>(a.f_Wimg);
     float4* fdst = reinterpret_cast<float4*>(Fs);
+#pragma unroll 8  // independent load -> store iterations: keep 8 loads in flight
     for (int i = tid; i < (int)(F::W_FLOATS / 4); i += blockDim.x) fdst[i] = fsrc[i];
   }
+#pragma unroll 8  // independent load -> store iterations: keep 8 loads in flight
   for (int i = tid; i < (int)C::E_FLOATS; i += blockDim.x) {
     float v = 0.f;
     if (i < C::NW) {

@@ -83,6 +83,7 @@ __global__ __launch_bounds__(256) void elbo_head_kernel(HeadArgs a) {
   __syncthreads();
   {
     unsigned long long c = 0;
+#pragma unroll 8  // independent load -> store iterations: keep 8 loads in flight
     for (int64_t b = tid; !a.norm && b < a.B; b += 256) {
       const int64_t L = a.lengths[b];
       c += (unsigned long long)(L <= 0 ? 0 : (L < a.T ? L : a.T));

@@ -93,6 +93,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_mfma_kernel(HeadArgs a) {
   const float cent = a.beta / Bn;   // d loss / d (sum q*log q)
 
   // ---- one-time: weights to LDS / registers, log_pi, valid count
+#pragma unroll 8  // independent load -> store iterations: keep 8 loads in flight
   for (int i = tid; i < 16 * S::LDW2; i += 256) {
     const int ij = i / S::LDW2, h = i - ij * S::LDW2;
     sh.W2S[i] = (ij < KK && h < TH) ? a.W2[ij * TH + h] : 0.f;
@@ -106,6 +107,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_mfma_kernel(HeadArgs a) {
     for (int k = 0; k < K; ++k) sh.lpS[k] = a.log_prior[k] - l;
     sh.cnt = a.norm ? (unsigned long long)a.norm[0] : 0ull;
   }
+#pragma unroll 8  // independent load -> store iterations: keep 8 loads in flight
   for (int i = tid; i < TH * 8; i += 256) {
     const int h = i >> 3, c = i & 7;
     sh.W1S[i] = c < U ? a.W1[h * U + c] : (c == U ? a.b1[h] : 0.f);
@@ -118,6 +120,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_mfma_kernel(HeadArgs a) {
   __syncthreads();
   {
     unsigned long long c = 0;
+#pragma unroll 8  // independent load -> store iterations: keep 8 loads in flight
     for (int64_t b = tid; !a.norm && b < a.B; b += 256) {
       const int64_t L = a.lengths[b];
       c += (unsigned long long)(L <= 0 ? 0 : (L < a.T ? L : a.T));

@@ -106,6 +106,7 @@ __global__ __launch_bounds__(256) void head_l2_kernel(StagedHeadArgs a) {
   __syncthreads();
   {  // valid positions (the recon normaliser mask.sum() * C, VQ_VAE_HMM_fixed.py:120)
     unsigned long long c = 0;
+#pragma unroll 8  // independent load -> store iterations: keep 8 loads in flight
     for (int64_t b = tid; !a.norm && b < a.B; b += 256) {
       const int64_t L = a.lengths[b];
       c += (unsigned long long)(L <= 0 ? 0 : (L < a.T ? L : a.T));

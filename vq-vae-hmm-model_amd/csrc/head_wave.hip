@@ -90,10 +90,12 @@ __global__ __launch_bounds__(256, 2) void elbo_head_wave_kernel(HeadArgs a) {
   auto& W = sh.wv[wave];
 
   // ---- one-time: weights to LDS, log_pi, valid count
-  for (int i = tid; i < 16 * S::LDW2; i += 256) {
+#pragma unroll 8  // independent load -> store iterations: keep 8 loads in flight
+  for (int i = tid; i < 16 * S::LDW2 && !(a.dbg & 16); i += 256) {
     const int ij = i / S::LDW2, h = i - ij * S::LDW2;
     sh.W2S[i] = (ij < KK && h < TH) ? a.W2[ij * TH + h] : 0.f;
   }
+#pragma unroll 8  // independent load -> store iterations: keep 8 loads in flight
   for (int i = tid; i < TH * 8; i += 256) {
     const int h = i >> 3, c = i & 7;
     sh.W1S[i] = c < U ? a.W1[h * U + c] : (c == U ? a.b1[h] : 0.f);
@@ -111,8 +113,9 @@ __global__ __launch_bounds__(256, 2) void elbo_head_wave_kernel(HeadArgs a) {
 #pragma unroll
   for (int v = 0; v < 4; ++v) b2f[v] = (4 * lg4 + v) < KK ? a.b2[4 * lg4 + v] : 0.f;
   __syncthreads();
-  if (!a.norm) {  // valid positions of the batch (mask.sum(), :120): one LDS atomic per wave
+  if (!a.norm && !(a.dbg & 64)) {  // valid positions of the batch (mask.sum(), :120): one LDS atomic per wave
     unsigned c = 0;
+#pragma unroll 8  // independent load -> store iterations: keep 8 loads in flight
     for (int64_t b = tid; b < a.B; b += 256) {
       const int64_t L = a.lengths[b];
       c += (unsigned)(L <= 0 ? 0 : (L < a.T ? L : a.T));
@@ -267,7 +270,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_wave_kernel(HeadArgs a) {
   int64_t w = (int64_t)((wave + blockIdx.x) & 3) * gridDim.x + blockIdx.x;
   // (a wave sees 1-2 windows at the cfg2 sizes, so rows are loaded at the window's start —
   // phase A waits only for u — rather than prefetched a window ahead in registers)
-  for (; w < nwin; w += stride) {
+  for (; w < nwin && !(a.dbg & 8); w += stride) {
     const int64_t r0 = w * WOWN;
     const int nown = (int)min<int64_t>(WOWN, a.R - r0);  // rows 0 .. nown-1 owned; row nown halo
     const int p = lane;
@@ -299,7 +302,8 @@ __global__ __launch_bounds__(256, 2) void elbo_head_wave_kernel(HeadArgs a) {
       }
     }
     // ---------------- A: MLP forward (MFMA), lg^T -> lgS
-    phase_a();
+    if (!(a.dbg & 1)) phase_a();
+    if (!(a.dbg & 2)) {
     // ---------------- B: lane = row
     float qv[4], lgv[4];
 #pragma unroll
@@ -443,29 +447,33 @@ __global__ __launch_bounds__(256, 2) void elbo_head_wave_kernel(HeadArgs a) {
         for (int ij = 0; ij < 16; ++ij) dl[ij] = 0.f;
       }
     }
+    }
     // ---------------- C: MLP backward (MFMA)
-    if (a.need_grad) {
+    if (a.need_grad && !(a.dbg & 4)) {
       phase_c();
     }
   }
 
   // ---------------- epilogue: loss partials, q0 / db2 sums, weight-gradient partials.  The
-  // whole LDS is scratch now: waves 1..3 park their accumulators side by side, one barrier,
-  // then wave 0 adds them in wave order (deterministic) and writes the workgroup's slab.
+  // whole LDS is scratch now: every wave parks its accumulators side by side, one barrier, then
+  // wave w adds hidden blocks [w HB/4, (w+1) HB/4) over the 4 waves in wave order (deterministic,
+  // the order wave 0 alone used) and writes that part of the workgroup's slab.
+  if (a.dbg & 32) return;
   constexpr int NV = 8 * HB;  // accumulator floats per lane: gW2 (4 HB) + gW1 (4 HB)
+  constexpr int HBW = HB / 4;  // hidden blocks per wave in the slab write
   float* xbuf = reinterpret_cast<float*>(smem4);
-  double* pw = reinterpret_cast<double*>(xbuf + 3 * NV * 64);  // [4 waves][4] loss partials
+  double* pw = reinterpret_cast<double*>(xbuf + 4 * NV * 64);  // [4 waves][4] loss partials
   float* qw = reinterpret_cast<float*>(pw + 16);                // [4 waves][4] q0 sums
   float* bw = qw + 16;                                          // [4 waves][16] db2 sums
   double dsum[4] = {(double)s_rec, (double)s_init, (double)s_tr, (double)s_ent};
+  if (!(a.dbg & 128)) {
 #pragma unroll
-  for (int k = 0; k < 4; ++k)
+    for (int k = 0; k < 4; ++k) dsum[k] = wave_sum_dpp(dsum[k]);
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) dsum[k] += __shfl_xor(dsum[k], o);
+    for (int k = 0; k < K; ++k) q0acc[k] = wave_sum_dpp(q0acc[k]);
 #pragma unroll
-  for (int k = 0; k < K; ++k) q0acc[k] = wave_sum(q0acc[k]);
-#pragma unroll
-  for (int ij = 0; ij < KK; ++ij) db2v[ij] = wave_sum(db2v[ij]);
+    for (int ij = 0; ij < KK; ++ij) db2v[ij] = wave_sum_dpp(db2v[ij]);
+  }
   lds_barrier();  // every wave is past its windows: W2S / W1S / wv[] are free (stores stay in flight)
   if (lane == 0) {
 #pragma unroll
@@ -475,8 +483,8 @@ __global__ __launch_bounds__(256, 2) void elbo_head_wave_kernel(HeadArgs a) {
 #pragma unroll
     for (int ij = 0; ij < KK; ++ij) bw[wave * 16 + ij] = db2v[ij];
   }
-  if (wave > 0 && a.need_grad) {
-    float* xb = xbuf + (wave - 1) * NV * 64;
+  if (a.need_grad) {
+    float* xb = xbuf + wave * NV * 64;
 #pragma unroll
     for (int hb = 0; hb < HB; ++hb) {
 #pragma unroll
@@ -486,42 +494,38 @@ __global__ __launch_bounds__(256, 2) void elbo_head_wave_kernel(HeadArgs a) {
     }
   }
   lds_barrier();
-  if (wave != 0) return;
-  if (lane < 4) a.part[blockIdx.x * 4 + lane] = ((pw[lane] + pw[4 + lane]) + pw[8 + lane]) + pw[12 + lane];
-  if (!a.need_grad) return;
-  if (lane < K) a.slab_q0[blockIdx.x * K + lane] = ((qw[lane] + qw[4 + lane]) + qw[8 + lane]) + qw[12 + lane];
-  if (lane < KK)
-    a.slab_b2[(int64_t)blockIdx.x * KK + lane] = ((bw[lane] + bw[16 + lane]) + bw[32 + lane]) + bw[48 + lane];
-#pragma unroll 1
-  for (int ww = 0; ww < 3; ++ww) {  // one wave's 8*HB partials at a time (registers)
-    const float* xb = xbuf + ww * NV * 64;
-#pragma unroll
-    for (int hb = 0; hb < HB; ++hb) {
-#pragma unroll
-      for (int v = 0; v < 4; ++v) gW2[hb][v] += xb[(hb * 4 + v) * 64 + lane];
-#pragma unroll
-      for (int v = 0; v < 4; ++v) gW1[hb][v] += xb[(4 * HB + hb * 4 + v) * 64 + lane];
+  if (a.dbg & 256) return;
+  if (wave == 0) {
+    if (lane < 4) a.part[blockIdx.x * 4 + lane] = ((pw[lane] + pw[4 + lane]) + pw[8 + lane]) + pw[12 + lane];
+    if (a.need_grad) {
+      if (lane < K) a.slab_q0[blockIdx.x * K + lane] = ((qw[lane] + qw[4 + lane]) + qw[8 + lane]) + qw[12 + lane];
+      if (lane < KK)
+        a.slab_b2[(int64_t)blockIdx.x * KK + lane] = ((bw[lane] + bw[16 + lane]) + bw[32 + lane]) + bw[48 + lane];
     }
   }
+  if (!a.need_grad) return;
+  auto sum4 = [&](int slot) {
+    const float* x = xbuf + slot * 64 + lane;
+    return ((x[0] + x[NV * 64]) + x[2 * NV * 64]) + x[3 * NV * 64];
+  };
   float* sW2 = a.slab_W2 + (int64_t)blockIdx.x * KK * TH;
-#pragma unroll
-  for (int hb = 0; hb < HB; ++hb)
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int ij = 4 * lg4 + v;
-      if (ij < KK) sW2[ij * TH + hb * 16 + l16] = gW2[hb][v];
-    }
-  // gW1' block hb: lane -> h = hb*16 + 4*lg4 + v, c' = l16 (c' == U is db1)
   float* sW1 = a.slab_W1 + (int64_t)blockIdx.x * TH * U;
   float* sb1 = a.slab_b1 + (int64_t)blockIdx.x * TH;
 #pragma unroll
-  for (int hb = 0; hb < HB; ++hb)
+  for (int k = 0; k < HBW; ++k) {
+    const int hb = wave * HBW + k;
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
+      const int ij = 4 * lg4 + v;
+      const float g2 = sum4(hb * 4 + v);
+      if (ij < KK) sW2[ij * TH + hb * 16 + l16] = g2;
+      // gW1' block hb: lane -> h = hb*16 + 4*lg4 + v, c' = l16 (c' == U is db1)
       const int h = hb * 16 + 4 * lg4 + v;
-      if (l16 < U) sW1[h * U + l16] = gW1[hb][v];
-      else if (l16 == U) sb1[h] = gW1[hb][v];
+      const float g1 = sum4(4 * HB + hb * 4 + v);
+      if (l16 < U) sW1[h * U + l16] = g1;
+      else if (l16 == U) sb1[h] = g1;
     }
+  }
 }
 
 // Blocks per window: 4 (63 owned rows) from ~256 sequences of T = 200 up, else 1 (15 owned rows): at small batches the per-window chain, not the work, sets the time,
@@ -542,12 +546,18 @@ int head_wave_grid(int64_t R) {
 
 template <int NBW>
 static size_t head_wave_lds(int HB) {
-  const size_t ex = (size_t)3 * 8 * HB * 64 * 4 + 512;  // epilogue exchange buffer
+  const size_t ex = (size_t)4 * 8 * HB * 64 * 4 + 512;  // epilogue exchange buffer
   const size_t st = HB == 4 ? sizeof(HwLds<4, NBW>) : sizeof(HwLds<8, NBW>);
   return ex > st ? ex : st;
 }
 
-int launch_head_wave(const HeadArgs& a, int grid, hipStream_t s) {
+int launch_head_wave(const HeadArgs& a0, int grid, hipStream_t s) {
+  static const int dbg = [] {
+    const char* e = getenv("VQHMM_HEAD_DBG");
+    return e ? atoi(e) : 0;
+  }();
+  HeadArgs a = a0;
+  a.dbg = dbg;
   if (a.R >= (1ll << 31)) return VQHMM_EUNSUPPORTED;  // 32-bit row arithmetic
   const int nbw = head_wave_nbw(a.R);
 #define VQHMM_HW(KV, HBV)                                                                              \

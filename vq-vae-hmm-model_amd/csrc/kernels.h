@@ -80,9 +80,11 @@ __device__ inline void finalize_loss_block(const double* part, int nblk, const i
                                            float* pieces, double* red, const int64_t* cnt = nullptr) {
   const int tid = threadIdx.x;
   double v[5] = {0, 0, 0, 0, 0};
+#pragma unroll 8  // independent load -> store iterations: keep 8 loads in flight
   for (int i = tid; i < nblk; i += 256)
     for (int k = 0; k < 4; ++k) v[k] += part[i * 4 + k];
   if (!norm && cnt && tid == 0) v[4] = (double)*cnt;
+#pragma unroll 8  // independent load -> store iterations: keep 8 loads in flight
   for (int64_t b = tid; !norm && !cnt && b < B; b += 256) {
     const int64_t L = lengths[b];
     v[4] += (double)(L <= 0 ? 0 : (L < T ? L : T));
@@ -122,6 +124,8 @@ struct WgradArgs {
 };
 
 struct HeadArgs {
+  int dbg;               // head_wave profiling switch (VQHMM_HEAD_DBG bits: 1 no A, 2 no B, 4 no C, 8 no
+                         // window loop); results then invalid.  0 in every product launch
   int64_t B;
   int T;
   int64_t R;

@@ -27,10 +27,12 @@ __device__ __forceinline__ void prior_stage_weights(PriorW<HB, KB>& w, const flo
   using S = PriorW<HB, KB>;
   constexpr int TH = S::TH;
   const int KK = K * K;
+#pragma unroll 8  // independent load -> store iterations: keep 8 loads in flight
   for (int i = tid; i < S::KP2 * S::LDW2; i += nthr) {
     const int ij = i / S::LDW2, h = i - ij * S::LDW2;
     w.W2S[i] = (ij < KK && h < TH) ? W2[(int64_t)ij * TH + h] : 0.f;
   }
+#pragma unroll 8  // independent load -> store iterations: keep 8 loads in flight
   for (int i = tid; i < TH * 8; i += nthr) {
     const int h = i >> 3, c = i & 7;
     w.W1S[i] = c < U ? W1[h * U + c] : (c == 4 ? b1[h] : 0.f);

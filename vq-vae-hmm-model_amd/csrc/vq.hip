@@ -192,6 +192,7 @@ __global__ __launch_bounds__(256, NBUF == 2 ? 2 : 1) void vq_rows_kernel(const f
     if (i < NC) cbS[i / (4 * DG)][i % (4 * DG)] = (i / (4 * DG)) < K ? cbv[k] : 0.0f;
   }
   lds_barrier();
+#pragma unroll 8  // independent load -> store iterations: keep 8 loads in flight
   for (int i = tid; i < CB * DG * 64; i += 256) {
     const int c = i / (DG * 64), dg = (i / 64) % DG, l = i & 63;
     aS[c][dg][l] = -2.0f * cbS[16 * c + (l & 15)][4 * dg + (l >> 4)];
@@ -312,6 +313,7 @@ __global__ __launch_bounds__(256) void vq_argmin_kernel(const float* __restrict_
   for (int kb = 0; kb < K; kb += KB) {
     const int kn = min(KB, K - kb);
     __syncthreads();
+#pragma unroll 8  // independent load -> store iterations: keep 8 loads in flight
     for (int i = threadIdx.x; i < KB * ldc; i += 256) {
       const int k = i / ldc, d = i - k * ldc;
       cbs[i] = (k < kn && d < Dv) ? -2.0f * cb[(int64_t)(kb + k) * Dv + d] : 0.0f;
