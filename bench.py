@@ -359,6 +359,7 @@ def main():
 
     roof = None
     kernels = None
+    stage_roof = None
     if rank == 0 and a.profile_steps > 0:
         stages = stage_timings(lib, st, x, u, L, B, T, beta, a.profile_steps)
         dom = max(stages, key=lambda s: s["us"])
@@ -374,6 +375,22 @@ def main():
         roof.update({"traffic": traffic_for(dom["name"], a.config), "kernel": dom["name"],
                      "avg_us": round(dom["us"], 2)})
         kernels = {s["name"]: round(s["us"], 2) for s in stages}
+        # every launch's own roofline (SURVEY 8d asks for the H->H convs' MFMA fraction, not only the
+        # dominant stage's): algorithmic flops (MFMA-bound) or bytes (HBM-bound) over the event-timed
+        # stage duration (which includes ~5 us of event overhead: an empty stage reads ~5 us)
+        stage_roof = {}
+        for sd in stages:
+            if sd["name"].startswith("(") or sd["us"] <= 0 or (sd["flops"] <= 0 and sd["bytes"] <= 0):
+                continue
+            dur = sd["us"] * 1e-6
+            if sd["mfma"]:
+                ach = sd["flops"] / dur / 1e12
+                stage_roof[sd["name"]] = {"bound": "mfma", "us": round(sd["us"], 2), "achieved": round(ach, 2),
+                                          "unit": "TFLOP/s", "frac": round(ach / MFMA_F32_PEAK_TFLOPS, 4)}
+            else:
+                ach = sd["bytes"] / dur / 1e9
+                stage_roof[sd["name"]] = {"bound": "hbm", "us": round(sd["us"], 2), "achieved": round(ach, 1),
+                                          "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4)}
     vq = vq_cfg3(lib) if rank == 0 and world == 1 else None
     hmm = hmm_kernels(lib) if rank == 0 and world == 1 and not a.no_hmm else {}
 
@@ -393,7 +410,7 @@ def main():
                        "parallelism": f"dp{world}" if world > 1 else "single", "hip_graph": use_graph,
                        "rccl_ranks": torch.distributed.get_world_size() if world > 1 else 0},
             "roofline": roof, "cpu_baseline": cpu,
-            "step_kernels_us": kernels, "vq_cfg3": vq, **hmm,
+            "step_kernels_us": kernels, "stage_roofline": stage_roof, "vq_cfg3": vq, **hmm,
         }
         if cpu:
             line["speedup_vs_cpu"] = round(value / cpu["value"], 1)

@@ -732,6 +732,8 @@ int vqhmm_elbo_stage_info(const vqhmm_dims_t* d, int64_t B, int64_t T, int stage
     else if (fused_front && stage == S_ENC2) nm = "enc_conv1+enc_conv2+to_logits";
     else if (fused_front && stage == S_DEC2) nm = "dec_conv1+dec_conv2+to_params";
     else if (fused_front && stage == S_DEC2_DG) nm = "to_params_dgrad+dec_conv2_dgrad";
+    else if (stage == S_LOGIT_BWD && logits_bwd_fused(p)) nm = "(logits_bwd: in dec_conv1_dgrad's epilogue)";
+    else if (stage == S_LOGIT_DG && logits_dg_fused(p)) nm = "(to_logits_dgrad: in dec_conv1_dgrad's epilogue)";
     else if (tail_fused_on() && stage == S_REDUCE) nm = "(grad_tail: in the tail launch)";
     else if (tail_fused_on() && stage == S_COMPOSE_BWD) nm = "tail(grad_tail+compose_bwd[+adam])";
     strncpy(name, nm, name_len - 1);
@@ -748,6 +750,21 @@ int vqhmm_elbo_stage_info(const vqhmm_dims_t* d, int64_t B, int64_t T, int stage
     stage_work(p, stage == S_ENC2 ? S_ENC1 : stage == S_DEC2 ? S_DEC1 : S_PAR_DG, &f1, &b1, &m1);
     f += f1;
     b += b1;
+  }
+  if ((stage == S_LOGIT_BWD && logits_bwd_fused(p)) || (stage == S_LOGIT_DG && logits_dg_fused(p))) {
+    f = 0; b = 0;
+  } else if (stage == S_DEC1_DG && logits_bwd_fused(p)) {  // its epilogue does the logits backward (+ dgrad)
+    double f1, b1;
+    int m1;
+    stage_work(p, S_LOGIT_BWD, &f1, &b1, &m1);
+    f += f1;
+    b += b1;
+    if (logits_dg_fused(p)) {
+      stage_work(p, S_LOGIT_DG, &f1, &b1, &m1);
+      f += f1;
+      b += b1;
+    }
+    m = 0;  // K output channels: bytes, not flops, bound it
   }
   if (tail_fused_on() && stage == S_REDUCE) {
     f = 0; b = 0;
