@@ -7,6 +7,6 @@ tail -1 $OUT/pytest.log
 for b in 1024 512 128; do
   for t in 1 0; do
     VQHMM_CONV_FUSE=$t timeout -k 10 200 python bench.py --batch $b --no-cpu-baseline --no-hmm --steps 200 > $OUT/b${b}_f$t.json 2>> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
-    python3 -c "import json; d=json.load(open('$OUT/b${b}_f$t.json')); k=d['step_kernels_us']; print('B=$b fuse=$t', d['ms_per_step'], 'enc2', k['enc_conv2+to_logits'], 'dec2', k['dec_conv2+to_params'], 'dec2dg', k['dec_conv2_dgrad'], 'pardg', k['to_params_dgrad'])"
+    python3 -c "import json; d=json.load(open('$OUT/b${b}_f$t.json')); k=d['step_kernels_us']; print('B=$b fuse=$t', d['ms_per_step'], {n: v for n, v in k.items() if 'conv' in n and not n.startswith('(')})"
   done
 done

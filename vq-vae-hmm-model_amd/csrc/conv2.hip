@@ -123,6 +123,35 @@ __device__ __forceinline__ void c2_mfma_tile(const float* Ws, const float* Xw, i
   }
 }
 
+// Packed taps for a narrow k = 3 layer (3 * Kc <= 16): k-column j = tap * Kc + c, so the three taps
+// share ONE 16-wide k-block — NB x 4 MFMAs per 16 rows instead of 3 x NB x 4.  Operands are per-lane
+// gathers from the standard weight image [tap][n][LDX] and X slot [row][LDX]; columns past 3 * Kc
+// read tap 0's zero pad column 15 (image and slot are zero past the layer's channels).
+template <int NB, int LDX, int NW>
+__device__ __forceinline__ void c2_mfma_pk(const float* Ws, const float* Xw, int lg4, int l16, int C,
+                                           f32x4 (&acc)[NB][1]) {
+  int wo[4], xo[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int k = 4 * lg4 + e;
+    const bool in = k < 3 * C;
+    const int tap = in ? k / C : 0, c = in ? k - tap * C : 15;
+    wo[e] = (tap * NW + l16) * LDX + c;
+    xo[e] = (l16 + tap) * LDX + c;
+  }
+  float b[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) b[e] = Xw[xo[e]];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    float a4[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) a4[e] = Ws[wo[e] + nb * 16 * LDX];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc[nb][0] = mfma16x16x4(a4[e], b[e], acc[nb][0]);
+  }
+}
+
 // Epilogue of one tile (ACT: 0 none, 1 ReLU, 2 ReLU-backward mask by aux, 3 none + the softmax
 // backward of the row, see ConvArgs::lb_*).
 // Rows of a 16-row block outside [rlo, rhi) get their values (acc) but no stores: the fused
@@ -411,7 +440,7 @@ struct C2wOcc {
   static constexpr int MAXW = NB * KCP >= 8 ? 12 : 16;
 };
 
-template <int NB, int KCP, int KS, int ACT, bool TAIL>
+template <int NB, int KCP, int KS, int ACT, bool TAIL, bool PK = false>
 __global__ __launch_bounds__((64 * C2wOcc<NB, KCP>::MAXW)) void conv2w_kernel(ConvArgs a, int64_t ntiles) {
   using C = C2wCfg<NB, KCP, KS>;
   extern __shared__ float4 smem4[];
@@ -497,7 +526,8 @@ __global__ __launch_bounds__((64 * C2wOcc<NB, KCP>::MAXW)) void conv2w_kernel(Co
     f32x4 acc[NB][1];
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) acc[nb][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-    c2_mfma_tile<NB, 1, KCP, KS, C::LDX, C::NW>(Ws, Xs, lg4, l16, acc, a.pipe);
+    if constexpr (PK) c2_mfma_pk<NB, C::LDX, C::NW>(Ws, Xs, lg4, l16, a.Kc, acc);
+    else c2_mfma_tile<NB, 1, KCP, KS, C::LDX, C::NW>(Ws, Xs, lg4, l16, acc, a.pipe);
     __builtin_amdgcn_wave_barrier();  // the slot's reads are done before the next tile overwrites it
     float bias_r[NB][4], tw[NB][4];
     f32x4 tb0 = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -538,7 +568,7 @@ struct C2fCfg {
   }
 };
 
-template <int NB, bool TAIL, int FKS, int ACT>
+template <int NB, bool TAIL, int FKS, int ACT, bool FPK>
 __global__ __launch_bounds__(64 * 12) void conv2f_kernel(ConvArgs a, int64_t ntiles) {
   using Q = C2fCfg<NB, TAIL, FKS>;
   using C = typename Q::C;
@@ -631,7 +661,8 @@ __global__ __launch_bounds__(64 * 12) void conv2f_kernel(ConvArgs a, int64_t nti
     f32x4 acc1[4][1];
 #pragma unroll
     for (int nb = 0; nb < 4; ++nb) acc1[nb][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-    c2_mfma_tile<4, 1, 1, FKS, F::LDX, F::NW>(Fs, X1, lg4, l16, acc1, a.pipe);
+    if constexpr (FPK) c2_mfma_pk<4, F::LDX, F::NW>(Fs, X1, lg4, l16, a.f_Kc, acc1);  // = the unfused front's
+    else c2_mfma_tile<4, 1, 1, FKS, F::LDX, F::NW>(Fs, X1, lg4, l16, acc1, a.pipe);
     {
       float b1[4][4], tw0[4][4] = {};
 #pragma unroll
@@ -684,7 +715,10 @@ static int launch_c2f(const ConvArgs& a, hipStream_t s) {
   const int64_t want = cdiv(ntiles, 256);
   const int wpg = (int)(want < wmax ? (want > 0 ? want : 1) : wmax);
   const int64_t grid = cdiv(ntiles, wpg) < 256 ? cdiv(ntiles, wpg) : 256;
-  conv2f_kernel<NB, TAIL, FKS, ACT><<<(unsigned)grid, 64 * wpg, Q::lds(wpg), s>>>(ap, ntiles);
+  if (FKS == 3 && 3 * a.f_Kc <= 16)  // packed front taps, as launch_c2w runs the unfused front
+    conv2f_kernel<NB, TAIL, FKS, ACT, true><<<(unsigned)grid, 64 * wpg, Q::lds(wpg), s>>>(ap, ntiles);
+  else
+    conv2f_kernel<NB, TAIL, FKS, ACT, false><<<(unsigned)grid, 64 * wpg, Q::lds(wpg), s>>>(ap, ntiles);
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
 }
@@ -739,6 +773,13 @@ static int launch_c2w(const ConvArgs& a, hipStream_t s) {
   const int64_t want = cdiv(ntiles, 256);
   const int wpg = (int)(want < wmax ? (want > 0 ? want : 1) : wmax);
   const int64_t grid = cdiv(ntiles, wpg) < 256 ? cdiv(ntiles, wpg) : 256;
+  if constexpr (KCP == 1 && KS == 3) {
+    if (3 * a.Kc <= 16) {  // packed taps (c2_mfma_pk)
+      conv2w_kernel<NB, KCP, KS, ACT, TAIL, true><<<(unsigned)grid, 64 * wpg, C::lds(wpg), s>>>(a, ntiles);
+      VQHMM_LAUNCH_CHECK();
+      return VQHMM_OK;
+    }
+  }
   conv2w_kernel<NB, KCP, KS, ACT, TAIL><<<(unsigned)grid, 64 * wpg, C::lds(wpg), s>>>(a, ntiles);
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
