@@ -493,6 +493,35 @@ bool front_fused(const ElboPlan& p, const float* const* w, int st) {
   return on && (st == S_ENC2 || st == S_DEC2 || st == S_DEC2_DG) && conv2_fused_supported(fused_pair(p, w, st));
 }
 
+// dec_conv1's data gradient with, for K <= 4, the softmax backward (+ to_logits' dgrad) in its epilogue
+ConvArgs dec1_dg_args(const ElboPlan& p, const float* const* w, const float* gscale) {
+  static const float* const kNull[VQHMM_NPARAMS] = {};
+  if (!w) w = kNull;
+  ConvArgs a = conv_of(p, w, S_DEC1_DG);
+  if (logits_bwd_fused(p)) {  // + logits_bwd in the epilogue
+    a.act = 3;
+    a.lb_q = p.q; a.lb_dqx = p.dqx; a.lb_dlx = p.dlx; a.lb_scale = gscale; a.lb_dlog = p.dlog;
+    if (logits_dg_fused(p)) {  // + to_logits_dgrad
+      a.lb_W = w[LOGIT_W]; a.lb_h = p.h2e; a.lb_dh = p.dh2; a.lb_C = p.H2;
+    }
+  }
+  return a;
+}
+// dec_conv1 dgrad -> enc_conv2 dgrad as one launch below 2^17 rows (conv2.hip conv2g_kernel);
+// VQHMM_CONV_FUSE=0 switches it off too
+bool bwd_pair_fused(const ElboPlan& p, const float* const* w, const float* gscale) {
+  static const bool on = [] {
+    const char* e = getenv("VQHMM_CONV_FUSE");
+    return !e || atoi(e) != 0;
+  }();
+  // measured: a launch fewer wins at small batches (B = 128: 22.3 -> 16.8 us), break-even at B = 512,
+  // and at cfg2 (207k rows) the two launches are 3 us faster (168 VGPRs + spills at 3 waves / SIMD)
+  if (!on || !logits_dg_fused(p) || p.R >= (1 << 17)) return false;
+  ConvArgs f = dec1_dg_args(p, w, gscale);
+  if (!w) f.lb_dh = p.dh2;  // stage_info's shape-only query (any non-null marks the fused dgrad)
+  return conv2_bwd_pair_supported(conv_of(p, w, S_ENC2_DG), f);
+}
+
 // VQHMM_TAIL_FUSED=0: grad_tail and compose_bwd / compose_adam as two launches (A/B); read once
 bool tail_fused_on() {
   static const bool v = [] {
@@ -536,20 +565,15 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       }
       return launch_conv(conv_of(p, w, st), s);
     case S_ENC2_DG:
+      if (bwd_pair_fused(p, w, c.gscale))
+        return launch_conv2_bwd_pair(conv_of(p, w, st), dec1_dg_args(p, w, c.gscale), s);
       return launch_conv(conv_of(p, w, st), s);
     case S_LOGIT_DG:
       if (logits_dg_fused(p)) return VQHMM_OK;  // ran in S_DEC1_DG's epilogue
       return launch_conv(conv_of(p, w, st), s);
     case S_DEC1_DG: {
-      ConvArgs a = conv_of(p, w, st);
-      if (logits_bwd_fused(p)) {  // + logits_bwd in the epilogue
-        a.act = 3;
-        a.lb_q = p.q; a.lb_dqx = p.dqx; a.lb_dlx = p.dlx; a.lb_scale = c.gscale; a.lb_dlog = p.dlog;
-        if (logits_dg_fused(p)) {  // + to_logits_dgrad
-          a.lb_W = w[LOGIT_W]; a.lb_h = p.h2e; a.lb_dh = p.dh2; a.lb_C = p.H2;
-        }
-      }
-      return launch_conv(a, s);
+      if (bwd_pair_fused(p, w, c.gscale)) return VQHMM_OK;  // runs inside S_ENC2_DG's launch
+      return launch_conv(dec1_dg_args(p, w, c.gscale), s);
     }
     case S_PAR_DG: {
       if (front_fused(p, w, S_DEC2_DG)) return VQHMM_OK;  // runs inside S_DEC2_DG's launch
@@ -722,6 +746,7 @@ int vqhmm_elbo_stage_info(const vqhmm_dims_t* d, int64_t B, int64_t T, int stage
   const int pair_of = stage == S_ENC1 ? S_ENC2 : stage == S_DEC1 ? S_DEC2 : stage == S_PAR_DG ? S_DEC2_DG : stage;
   const bool fused_front = (pair_of == S_ENC2 || pair_of == S_DEC2 || pair_of == S_DEC2_DG) &&
                            front_fused(plan_elbo(d, B, T, reinterpret_cast<void*>(4096)), nullptr, pair_of);
+  const bool bwd_pair = bwd_pair_fused(plan_elbo(d, B, T, reinterpret_cast<void*>(4096)), nullptr, nullptr);
   if (name && name_len) {
     const char* nm = kStageNames[stage];
     if (p.wgroup && stage == S_W_ENC1) nm = "wgrad_group(all 6 weight gradients)";
@@ -732,6 +757,8 @@ int vqhmm_elbo_stage_info(const vqhmm_dims_t* d, int64_t B, int64_t T, int stage
     else if (fused_front && stage == S_ENC2) nm = "enc_conv1+enc_conv2+to_logits";
     else if (fused_front && stage == S_DEC2) nm = "dec_conv1+dec_conv2+to_params";
     else if (fused_front && stage == S_DEC2_DG) nm = "to_params_dgrad+dec_conv2_dgrad";
+    else if (bwd_pair && stage == S_DEC1_DG) nm = "(dec_conv1_dgrad: in enc_conv2_dgrad's launch)";
+    else if (bwd_pair && stage == S_ENC2_DG) nm = "dec_conv1_dgrad+logits_bwd+to_logits_dgrad+enc_conv2_dgrad";
     else if (stage == S_LOGIT_BWD && logits_bwd_fused(p)) nm = "(logits_bwd: in dec_conv1_dgrad's epilogue)";
     else if (stage == S_LOGIT_DG && logits_dg_fused(p)) nm = "(to_logits_dgrad: in dec_conv1_dgrad's epilogue)";
     else if (tail_fused_on() && stage == S_REDUCE) nm = "(grad_tail: in the tail launch)";
@@ -765,6 +792,18 @@ int vqhmm_elbo_stage_info(const vqhmm_dims_t* d, int64_t B, int64_t T, int stage
       b += b1;
     }
     m = 0;  // K output channels: bytes, not flops, bound it
+  }
+  if (bwd_pair && stage == S_DEC1_DG) {
+    f = 0; b = 0;
+  } else if (bwd_pair && stage == S_ENC2_DG) {  // + dec_conv1 dgrad with its fused epilogue work
+    double f1, b1;
+    int m1;
+    stage_work(p, S_DEC1_DG, &f1, &b1, &m1);
+    f += f1; b += b1;
+    stage_work(p, S_LOGIT_BWD, &f1, &b1, &m1);
+    f += f1; b += b1;
+    stage_work(p, S_LOGIT_DG, &f1, &b1, &m1);
+    f += f1; b += b1;
   }
   if (tail_fused_on() && stage == S_REDUCE) {
     f = 0; b = 0;

@@ -160,7 +160,8 @@ template <int NB, int PB, int ACT>
 __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a, int64_t m0, int wave, int lg4, int l16,
                                                f32x4 (&acc)[NB][PB], const float4 (&auxv)[NB][PB],
                                                const float (&bias_r)[NB][4], const float (&tw)[NB][4],
-                                               f32x4 tb0, float sc, bool tail, int rlo = 0, int rhi = 16) {
+                                               f32x4 tb0, float sc, bool tail, int rlo = 0, int rhi = 16,
+                                               float* xs_dh = nullptr, int xs_ld = 0) {
   // lane (lg4, l16) holds channels nb*16 + 4*lg4 + v of row m0 + (wave*PB+pb)*16 + l16
   const bool own = l16 >= rlo && l16 < rhi;
 #pragma unroll
@@ -192,7 +193,9 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a, int64_t m0, in
             float yk[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) yk[k] = __shfl(y[k], l16);
-            if (st_r) {
+            // rows inside [0, R) are computed (a fused next conv's halo rows need them, xs_dh),
+            // only owned rows are stored
+            if (r >= 0 && r < a.R) {
               const float lsc = a.lb_scale ? *a.lb_scale : 1.f;
               const float4 q4 = *reinterpret_cast<const float4*>(a.lb_q + r * 4);
               const float4 x4 = *reinterpret_cast<const float4*>(a.lb_dqx + r * 4);
@@ -208,7 +211,7 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a, int64_t m0, in
               f32x4 dl;
 #pragma unroll
               for (int k = 0; k < 4; ++k) dl[k] = qk[k] * (dq[k] - sdot) + lsc * lk[k];
-              if (lg4 == 0) *reinterpret_cast<f32x4*>(a.lb_dlog + r * 4) = dl;
+              if (lg4 == 0 && st_r) *reinterpret_cast<f32x4*>(a.lb_dlog + r * 4) = dl;
               if (a.lb_dh) {
                 // dh[r][c] = (h[r][c] > 0) * sum_k W[k][c] dl[k]: to_logits (1x1, K -> C) dgrad with the
                 // ReLU mask of its input h, the same k-ordered fma chain as the MFMA path; lane group
@@ -226,9 +229,14 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a, int64_t m0, in
                     for (int k = 0; k < 4; ++k) sacc = fmaf(c < C && k < a.N ? a.lb_W[k * C + c] : 0.f, dl[k], sacc);
                     o[v] = hv[v] > 0.f ? sacc : 0.f;
                   }
-                  *reinterpret_cast<f32x4*>(a.lb_dh + r * L + c0) = o;
+                  if (st_r) *reinterpret_cast<f32x4*>(a.lb_dh + r * L + c0) = o;
+                  if (xs_dh) *reinterpret_cast<f32x4*>(xs_dh + l16 * xs_ld + c0) = o;
                 }
               }
+            } else if (xs_dh && a.lb_dh) {  // rows outside [0, R): the zero padding of the next conv
+              const int L = ld4(a.lb_C), per = L / 4;
+              for (int c0 = lg4 * per; c0 < (lg4 + 1) * per; c0 += 4)
+                *reinterpret_cast<f32x4*>(xs_dh + l16 * xs_ld + c0) = f32x4{0.f, 0.f, 0.f, 0.f};
             }
           }
         }
@@ -739,6 +747,132 @@ int launch_conv2_fused(const ConvArgs& a, hipStream_t s) {
   if (a.N <= 16) return tail ? launch_c2f<1, true, 3, 1>(a, s) : launch_c2f<1, false, 3, 1>(a, s);
   if (a.N <= 32) return tail ? launch_c2f<2, true, 3, 1>(a, s) : launch_c2f<2, false, 3, 1>(a, s);
   return tail ? launch_c2f<4, true, 3, 1>(a, s) : launch_c2f<4, false, 3, 1>(a, s);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Fused backward pair: dec_conv1 dgrad (H -> K, k = 3) whose epilogue runs the softmax backward and
+// to_logits' masked data gradient (ACT = 3 with lb_dh: dh2, H2 channels), feeding enc_conv2's
+// masked data gradient (H2 -> H, k = 3).  14-row tiles as conv2f_kernel: the front computes rows
+// m0-1 .. m0+14, stores its own rows' dqd / dlog / dh2 and writes all 16 dh2 rows into the X slot;
+// dh2 is never re-read from HBM.  Same arithmetic per row as the two launches (bit-identical).
+template <int NB, int KCP>
+struct C2gCfg {
+  using C = C2wCfg<NB, KCP, 3>;  // enc_conv2 dgrad: H2 -> H
+  using F = C2wCfg<1, 4, 3>;     // dec_conv1 dgrad: H (33 .. 64) -> K (<= 4)
+  static constexpr int TR = 14;
+  static constexpr size_t lds(int wpg) {
+    return (C::W_FLOATS + F::W_FLOATS + (size_t)wpg * (F::X_FLOATS + C::X_FLOATS)) * 4;
+  }
+};
+
+template <int NB, int KCP>
+__global__ __launch_bounds__(64 * 12) void conv2g_kernel(ConvArgs a, ConvArgs f, int64_t ntiles) {
+  using Q = C2gCfg<NB, KCP>;
+  using C = typename Q::C;
+  using F = typename Q::F;
+  constexpr int TR = Q::TR;
+  extern __shared__ float4 smem4[];
+  float* Ws = reinterpret_cast<float*>(smem4);  // enc_conv2 dgrad image
+  float* Fs = Ws + C::W_FLOATS;                 // dec_conv1 dgrad image
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nwv = blockDim.x >> 6;
+  float* X1 = Fs + F::W_FLOATS + wave * (F::X_FLOATS + C::X_FLOATS);  // dg1 rows m0-2 .. m0+15
+  float* Xs = X1 + F::X_FLOATS;                                         // dh2 rows m0-1 .. m0+14
+  const int lg4 = lane >> 4, l16 = lane & 15;
+  {
+    const float4* src = reinterpret_cast<const float4*>(a.Wimg);
+#pragma unroll 8
+    for (int i = tid; i < (int)(C::W_FLOATS / 4); i += blockDim.x) smem4[i] = src[i];
+    const float4* fsrc = reinterpret_cast<const float4*>(f.Wimg);
+    float4* fdst = reinterpret_cast<float4*>(Fs);
+#pragma unroll 8
+    for (int i = tid; i < (int)(F::W_FLOATS / 4); i += blockDim.x) fdst[i] = fsrc[i];
+  }
+  const float sc = a.scale ? *a.scale : 1.0f, fsc = f.scale ? *f.scale : 1.0f;
+  const int ldn = ld4(a.N);
+  const int64_t stride = (int64_t)gridDim.x * nwv;
+  int64_t tile = (int64_t)wave * gridDim.x + blockIdx.x;
+  float4 pf[F::PF];
+#pragma unroll
+  for (int k = 0; k < F::PF; ++k) {
+    const int s = lane + k * 64;
+    pf[k] = x_raw(f, tile * TR - 1, s < F::XF4 ? s : 0, F::KCW);
+  }
+  __syncthreads();  // weights; from here on the waves never wait for each other
+  const float zb1[1][4] = {}, zbN[NB][4] = {}, tw1[1][4] = {}, twN[NB][4] = {};
+  const float4 aux1[1][1] = {};
+  while (tile < ntiles) {
+    const int64_t m0 = tile * TR;
+    float4 auxv[NB][1];
+    {
+      const int64_t r = m0 + l16;
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb)
+        auxv[nb][0] = *reinterpret_cast<const float4*>(a.aux + (r < a.R ? r : a.R - 1) * ldn + min(nb * 16 + 4 * lg4, ldn - 4));
+    }
+#pragma unroll
+    for (int k = 0; k < F::PF; ++k) {
+      const int s = lane + k * 64;
+      if (s < F::XF4) {
+        const int row = s / (F::KCW / 4), c = (s - row * (F::KCW / 4)) * 4;
+        *reinterpret_cast<float4*>(X1 + row * F::LDX + c) = x_mask(f, m0 - 1, s, F::KCW, pf[k]);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    const int64_t next = tile + stride;
+    {
+      const int64_t pt = next < ntiles ? next : tile;
+#pragma unroll
+      for (int k = 0; k < F::PF; ++k) {
+        const int s = lane + k * 64;
+        pf[k] = x_raw(f, pt * TR - 1, s < F::XF4 ? s : 0, F::KCW);
+      }
+    }
+    f32x4 acc1[1][1] = {{f32x4{0.f, 0.f, 0.f, 0.f}}};
+    c2_mfma_tile<1, 1, 4, 3, F::LDX, F::NW>(Fs, X1, lg4, l16, acc1, 1);
+    conv2_epilogue<1, 1, 3>(f, m0 - 1, 0, lg4, l16, acc1, aux1, zb1, tw1, f32x4{0.f, 0.f, 0.f, 0.f}, fsc, false, 1,
+                            TR + 1, Xs, C::LDX);
+    __builtin_amdgcn_wave_barrier();
+    f32x4 acc[NB][1];
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) acc[nb][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+    c2_mfma_tile<NB, 1, KCP, 3, C::LDX, C::NW>(Ws, Xs, lg4, l16, acc, 1);
+    __builtin_amdgcn_wave_barrier();  // the slots' reads are done before the next tile overwrites them
+    conv2_epilogue<NB, 1, 2>(a, m0, 0, lg4, l16, acc, auxv, zbN, twN, f32x4{0.f, 0.f, 0.f, 0.f}, sc, false, 0, TR);
+    tile = next;
+  }
+}
+
+template <int NB, int KCP>
+static int launch_c2g(const ConvArgs& a, const ConvArgs& f, hipStream_t s) {
+  using Q = C2gCfg<NB, KCP>;
+  const int64_t ntiles = cdiv(a.R, Q::TR);
+  int wmax = 12;
+  while (wmax > 1 && Q::lds(wmax) > 160 * 1024) --wmax;
+  if (Q::lds(wmax) > 160 * 1024) return VQHMM_EUNSUPPORTED;
+  const int64_t want = cdiv(ntiles, 256);
+  const int wpg = (int)(want < wmax ? (want > 0 ? want : 1) : wmax);
+  const int64_t grid = cdiv(ntiles, wpg) < 256 ? cdiv(ntiles, wpg) : 256;
+  conv2g_kernel<NB, KCP><<<(unsigned)grid, 64 * wpg, Q::lds(wpg), s>>>(a, f, ntiles);
+  VQHMM_LAUNCH_CHECK();
+  return VQHMM_OK;
+}
+
+// a: enc_conv2 dgrad (act 2), f: dec_conv1 dgrad with the fused logits backward + to_logits dgrad
+bool conv2_bwd_pair_supported(const ConvArgs& a, const ConvArgs& f) {
+  const int L = ld4(f.lb_C);
+  const int kcw = a.Kc <= 16 ? 16 : a.Kc <= 32 ? 32 : 64;
+  return a.Wimg && f.Wimg && f.act == 3 && f.lb_dh && f.N <= 4 && f.Kc > 32 && f.Kc <= 64 && f.ks == 3 &&
+         a.ks == 3 && a.act == 2 && a.aux && a.N <= 64 && a.N > 32 && a.Kc == f.lb_C && L == kcw && !a.src_cf &&
+         !f.src_cf && !a.out_cf && !f.out_cf && !a.tW && a.R == f.R;
+}
+
+int launch_conv2_bwd_pair(const ConvArgs& a, const ConvArgs& f, hipStream_t s) {
+  if (!conv2_bwd_pair_supported(a, f)) return VQHMM_EUNSUPPORTED;
+  if (a.R == 0) return VQHMM_OK;
+  if (a.Kc <= 16) return launch_c2g<4, 1>(a, f, s);
+  if (a.Kc <= 32) return launch_c2g<4, 2>(a, f, s);
+  return launch_c2g<4, 4>(a, f, s);
 }
 
 // Kernel choice: VQHMM_CONV=wg | wave forces one (A/B), else the wave kernel below

@@ -189,6 +189,9 @@ bool conv2_supported(const ConvArgs& a);
 // front conv + this conv in one launch (conv2.hip conv2f_kernel; ConvArgs::f_*)
 bool conv2_fused_supported(const ConvArgs& a);
 int launch_conv2_fused(const ConvArgs& a, hipStream_t s);
+// dec_conv1 dgrad (+ logits backward, to_logits dgrad: f) -> enc_conv2 dgrad (a) in one launch
+bool conv2_bwd_pair_supported(const ConvArgs& a, const ConvArgs& f);
+int launch_conv2_bwd_pair(const ConvArgs& a, const ConvArgs& f, hipStream_t s);
 // Packed weight image of a conv2_kernel launch: img[(tap*NW + n)*LDX + c] = Weff(n, c, tap)
 // (zero past N / Kc), NW = 16*NB and LDX = 16*KCP + 4 for the launch's (NB, KCP) (c2_nb / c2_kcp).
 // Built once per step (prologue), so every workgroup stages its weights with float4 copies.
