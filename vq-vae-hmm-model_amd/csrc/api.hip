@@ -515,8 +515,13 @@ bool bwd_pair_fused(const ElboPlan& p, const float* const* w, const float* gscal
     return !e || atoi(e) != 0;
   }();
   // measured: a launch fewer wins at small batches (B = 128: 22.3 -> 16.8 us), break-even at B = 512,
-  // and at cfg2 (207k rows) the two launches are 3 us faster (168 VGPRs + spills at 3 waves / SIMD)
-  if (!on || !logits_dg_fused(p) || p.R >= (1 << 17)) return false;
+  // and at cfg2 (207k rows) the two launches are 3 us faster (168 VGPRs + spills at 3 waves / SIMD;
+  // 2 waves without spills: slower still).  VQHMM_BWD_PAIR_ROWS moves the threshold (A/B)
+  static const int64_t max_rows = [] {
+    const char* e = getenv("VQHMM_BWD_PAIR_ROWS");
+    return e ? (int64_t)atoll(e) : (int64_t)1 << 17;
+  }();
+  if (!on || !logits_dg_fused(p) || p.R >= max_rows) return false;
   ConvArgs f = dec1_dg_args(p, w, gscale);
   if (!w) f.lb_dh = p.dh2;  // stage_info's shape-only query (any non-null marks the fused dgrad)
   return conv2_bwd_pair_supported(conv_of(p, w, S_ENC2_DG), f);
