@@ -55,8 +55,10 @@ bool wgroup_enabled() {
 int64_t wgroup_min_rows() {
   static const int64_t v = [] {
     const char* e = getenv("VQHMM_WGRAD_MINROWS");
-    const long r = e ? atol(e) : 128;  // 2 stages: fewer, fuller slabs at small batches (B = 128: 0.165 -> 0.158 ms)
-    return (int64_t)(r >= 64 && r <= 65536 && r % 64 == 0 ? r : 128);
+    // 3 stages: fewer, fuller slabs at small batches (B = 128: 64 / 128 / 192 / 256 rows 0.1463 / 0.1381 /
+    // 0.1369 / 0.1377 ms; B = 256: 128 -> 192 rows 0.1953 -> 0.1921 ms)
+    const long r = e ? atol(e) : 192;
+    return (int64_t)(r >= 64 && r <= 65536 && r % 64 == 0 ? r : 192);
   }();
   return v;
 }

@@ -351,12 +351,14 @@ int launch_wgrad2_group(const WgradArgs* jobs, int n, hipStream_t s) {
 
 bool wgrad2_supported(const WgradArgs& a) { return !a.x_cf && a.N <= 64 && a.C <= 64; }
 
-// chunks per launch for big outputs (tuning override VQHMM_WGRAD_BIG_CHUNKS, read once)
+// chunks per launch for big outputs (tuning override VQHMM_WGRAD_BIG_CHUNKS, read once).  192: with
+// the grouped launch the small jobs fill the CUs, and fewer, longer chunks mean less slab traffic and a
+// shorter tail (cfg2 step 128 / 192 / 256 / 512 chunks: 0.4735 / 0.4728 / 0.4817 / 0.485 ms)
 static int64_t big_chunks() {
   static const int64_t n = [] {
     const char* e = getenv("VQHMM_WGRAD_BIG_CHUNKS");
     const long v = e ? atol(e) : 0;
-    return (int64_t)(v >= 64 && v <= 4096 ? v : 512);
+    return (int64_t)(v >= 64 && v <= 4096 ? v : 192);
   }();
   return n;
 }
@@ -371,9 +373,18 @@ static int64_t all_chunks() {
   return n;
 }
 
+// chunks for small outputs (N * C * ks < 4096; override VQHMM_WGRAD_SMALL_CHUNKS, read once)
+static int64_t small_chunks() {
+  static const int64_t n = [] {
+    const char* e = getenv("VQHMM_WGRAD_SMALL_CHUNKS");
+    const long v = e ? atol(e) : 0;
+    return (int64_t)(v >= 64 && v <= 4096 ? v : 512);
+  }();
+  return n;
+}
+
 int64_t wgrad2_rows(int64_t R, int N, int C, int ks) {
-  // 2 chunks per CU (measured: 63.5 vs 66.2 us on dec_conv2_wgrad at cfg2, 2 waves/SIMD)
-  int64_t chunks = ((int64_t)N * C * ks >= 4096) ? big_chunks() : 512;
+  int64_t chunks = ((int64_t)N * C * ks >= 4096) ? big_chunks() : small_chunks();
   if (all_chunks()) chunks = all_chunks();
   int64_t rows = cdiv(R, chunks);
   return cdiv(rows, RT) * RT;
