@@ -528,15 +528,18 @@ __global__ __launch_bounds__(256, 2) void elbo_head_wave_kernel(HeadArgs a) {
   }
 }
 
-// Blocks per window: 4 (63 owned rows) from ~256 sequences of T = 200 up, else 1 (15 owned rows): at small batches the per-window chain, not the work, sets the time,
-// so shorter windows on more waves finish sooner.  VQHMM_HEAD_NBW=1|4 overrides (A/B).
+// Blocks per window: 4 (63 owned rows) from ~500 sequences of T = 200 up, 2 (31) from ~160, else 1 (15
+// owned rows): at small batches the per-window chain, not the work, sets the time, so shorter windows on
+// more waves finish sooner.  VQHMM_HEAD_NBW=1|4 overrides (A/B).
 static int head_wave_nbw(int64_t R) {
   static const int force = [] {
     const char* e = getenv("VQHMM_HEAD_NBW");
     return e ? atoi(e) : 0;
   }();
   if (force == 1 || force == 2 || force == 4) return force;
-  return cdiv(R, 63) >= 512 ? 4 : 1;
+  // measured (step ms, NBW 1 / 2 / 4): B = 1024 0.489 / 0.478 / 0.473, B = 512 0.293 / 0.282 / 0.280,
+  // B = 256 0.187 / 0.181 / 0.191, B = 128 0.136 / 0.139 / 0.139 (T = 200)
+  return R >= 98304 ? 4 : R >= 32768 ? 2 : 1;
 }
 
 int head_wave_grid(int64_t R) {
