@@ -557,6 +557,15 @@ __global__ __launch_bounds__((64 * C2wOcc<NB, KCP>::MAXW)) void conv2w_kernel(Co
   }
 }
 
+// waves per workgroup cap for the wave-independent conv kernels (VQHMM_CONV_WMAX, A/B; read once)
+static int conv_wmax(int dflt) {
+  static const int v = [] {
+    const char* e = getenv("VQHMM_CONV_WMAX");
+    return e ? atoi(e) : 0;
+  }();
+  return v >= 1 && v < dflt ? v : dflt;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Fused pair: a k=3 ReLU "front" conv (<= 16 -> Kc channels, Kc <= 64) feeding this k=3 conv
 // (enc_conv1 -> enc_conv2 + to_logits, composed dec_conv1 -> dec_conv2 + to_params).  Tiles of 14
@@ -717,7 +726,7 @@ static int launch_c2f(const ConvArgs& a, hipStream_t s) {
   ConvArgs ap = a;
   ap.pipe = 1;
   const int64_t ntiles = cdiv(a.R, Q::TR);
-  int wmax = 12;
+  int wmax = conv_wmax(12);
   while (wmax > 1 && Q::lds(wmax) > 160 * 1024) --wmax;
   if (Q::lds(wmax) > 160 * 1024) return VQHMM_EUNSUPPORTED;
   const int64_t want = cdiv(ntiles, 256);
@@ -847,7 +856,7 @@ template <int NB, int KCP>
 static int launch_c2g(const ConvArgs& a, const ConvArgs& f, hipStream_t s) {
   using Q = C2gCfg<NB, KCP>;
   const int64_t ntiles = cdiv(a.R, Q::TR);
-  int wmax = 12;  // 3 waves / SIMD (a few bytes of spill) measured faster than 2 without (cfg2 72 vs 78 us)
+  int wmax = conv_wmax(12);  // 3 waves / SIMD (a few bytes of spill) measured faster than 2 without (cfg2 72 vs 78 us)
   while (wmax > 1 && Q::lds(wmax) > 160 * 1024) --wmax;
   if (Q::lds(wmax) > 160 * 1024) return VQHMM_EUNSUPPORTED;
   const int64_t want = cdiv(ntiles, 256);
@@ -900,7 +909,7 @@ template <int NB, int KCP, int KS, int ACT, bool TAIL>
 static int launch_c2w(const ConvArgs& a, hipStream_t s) {
   using C = C2wCfg<NB, KCP, KS>;
   const int64_t ntiles = cdiv(a.R, 16);
-  int wmax = C2wOcc<NB, KCP>::MAXW;
+  int wmax = conv_wmax(C2wOcc<NB, KCP>::MAXW);
   while (wmax > 1 && C::lds(wmax) > 160 * 1024) --wmax;
   if (C::lds(wmax) > 160 * 1024) return VQHMM_EUNSUPPORTED;
   // one workgroup per CU: as many waves as it takes to give every CU work, up to wmax
