@@ -596,6 +596,7 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       h.lengths = c.lengths; h.par = p.par; h.logits = p.logits; h.q = p.q;
       h.W1 = w[TN0_W]; h.b1 = w[TN0_B]; h.W2 = w[TN2_W]; h.b2 = w[TN2_B]; h.log_prior = w[LOG_PRIOR];
       h.beta = c.beta; h.norm = c.norm; h.need_grad = c.need_grad;
+      if (c.need_grad == 2 && !c.norm) h.cnt_in = p.cnt;  // the prologue counted the batch (S_TOPCL)
       h.dpar = p.dpar; h.dqx = p.dqx; h.dlx = p.dlx; h.part = p.part;
       h.slab_W1 = p.sW1; h.slab_b1 = p.sb1; h.slab_W2 = p.sW2; h.slab_b2 = p.sb2; h.slab_q0 = p.sq0;
       if (p.wave_head) return launch_head_wave(h, p.hgrid, s);

@@ -107,13 +107,13 @@ __global__ __launch_bounds__(256, 2) void elbo_head_wave_kernel(HeadArgs a) {
     for (int k = 0; k < K; ++k) s += __expf(a.log_prior[k] - m);
     const float l = m + __logf(s);
     for (int k = 0; k < 4; ++k) sh.lpS[k] = k < K ? a.log_prior[k] - l : 0.f;
-    sh.cnt = a.norm ? (unsigned long long)a.norm[0] : 0ull;
+    sh.cnt = a.norm ? (unsigned long long)a.norm[0] : a.cnt_in ? (unsigned long long)*a.cnt_in : 0ull;
   }
   f32x4 b2f;
 #pragma unroll
   for (int v = 0; v < 4; ++v) b2f[v] = (4 * lg4 + v) < KK ? a.b2[4 * lg4 + v] : 0.f;
   __syncthreads();
-  if (!a.norm && !(a.dbg & 64)) {  // valid positions of the batch (mask.sum(), :120): one LDS atomic per wave
+  if (!a.norm && !a.cnt_in && !(a.dbg & 64)) {  // valid positions of the batch (mask.sum(), :120): one LDS atomic per wave
     unsigned c = 0;
 #pragma unroll 8  // independent load -> store iterations: keep 8 loads in flight
     for (int64_t b = tid; b < a.B; b += 256) {

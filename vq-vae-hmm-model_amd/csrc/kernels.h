@@ -143,6 +143,7 @@ struct HeadArgs {
   const float* log_prior;// (K)
   float beta;
   const int64_t* norm;   // null, or device {valid_count, batch}: global normalisers (see loss_norm)
+  const int64_t* cnt_in; // without norm: the batch's valid count if the prologue already wrote it (else counted)
   int need_grad;
   float* dpar;           // PCL (R, ld4(2D))
   float* dqx;            // PCL (R, ld4(K))  dL/dq from the prior term
