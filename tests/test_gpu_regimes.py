@@ -164,3 +164,29 @@ def test_prior_viterbi_outside_fused_range_falls_back():
     prior = vqhmm.Prior(3, u_dim=4, trans_hidden=32).cuda()
     em = torch.log_softmax(torch.randn(3, 40, 3, device="cuda"), dim=2)
     assert vqhmm.prior_viterbi(prior, u, em) is None
+
+
+def test_prior_viterbi_fused_cfg5_length():
+    """cfg5's sequence length (T = 4096, K = 8, trans_hidden 128) on a 192-sequence slice of a shard:
+    fused path and score bit-identical to Prior.forward + Viterbi, and the C oracle on that log_A."""
+    import vqhmm
+    torch.manual_seed(5)
+    B, T, K = 192, 4096, 8
+    prior = vqhmm.Prior(K, u_dim=4, trans_hidden=128)
+    with torch.no_grad():
+        prior.transition_net[2].weight.mul_(3.0)
+    prior = prior.cuda()
+    g = torch.Generator(device="cuda").manual_seed(11)
+    u = torch.randn(B, 4, T, device="cuda", generator=g)
+    em = torch.log_softmax(2.0 * torch.randn(B, T, K, device="cuda", generator=g), dim=2)
+    L = torch.randint(T // 2, T + 1, (B,), generator=torch.Generator().manual_seed(3))
+    L[0] = T
+    got = vqhmm.prior_viterbi(prior, u, em, L)
+    with torch.no_grad():
+        log_pi, log_A = prior(u)
+    ref = vqhmm.viterbi(log_pi, log_A, em, L)
+    assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1])
+    sl = slice(0, 24)  # the C oracle on a slice (same tables)
+    rp, rs = c_oracle.viterbi(log_pi.cpu().numpy(), log_A[sl].cpu().numpy(), em[sl].cpu().numpy(), L[sl].numpy())
+    assert np.array_equal(got[0][sl].cpu().numpy(), rp)
+    assert np.array_equal(got[1][sl].cpu().numpy().view(np.uint32), rs.view(np.uint32))
