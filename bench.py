@@ -189,6 +189,34 @@ def hmm_kernels(lib):
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(gbps / HBM_PEAK_GBPS, 4),
                      "traffic": traffic_for(name, name), "shape": f"B{B} T{T} K{K}"}
         del log_A, em, ws
+    # the fused Prior-MLP -> Viterbi at the same cfg5 shard: log_A is built on the chip
+    # from u, so the kernel is bound by the MLP on the f32 MFMA: 2 (U + K^2) TH flops per position
+    import vqhmm
+    B, T, K, U, TH = 1024, 4096, 8, 4, 128
+    torch.manual_seed(0)
+    prior = vqhmm.Prior(K, u_dim=U, trans_hidden=TH).cuda()
+    g = torch.Generator(device="cuda").manual_seed(9)
+    u = torch.randn(B, U, T, device="cuda", generator=g)
+    em = torch.log_softmax(torch.randn(B, T, K, device="cuda", generator=g), -1)
+    L = torch.full((B,), T, dtype=torch.int64, device="cuda")
+    run = lambda: vqhmm.prior_viterbi(prior, u, em, L)  # noqa: E731
+    for _ in range(2):
+        run()
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(5):
+        run()
+    e1.record(s)
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) / 5 * 1e3
+    tf = B * T * 2.0 * (U + K * K) * TH / (us * 1e-6) / 1e12
+    out["prior_viterbi_cfg5"] = {"kernel": "prior_viterbi_kernel<8, 8, 8, 32> (vqhmm_prior_viterbi_f32)",
+                                 "bound": "mfma", "avg_us": round(us, 2), "achieved": round(tf, 2),
+                                 "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                 "frac": round(tf / MFMA_F32_PEAK_TFLOPS, 4), "shape": f"B{B} T{T} K{K} TH{TH} U{U}",
+                                 "note": "per call incl. log_pi + workspace allocation; the unfused Prior.forward "
+                                         "+ Viterbi writes and reads the 1.07 GB log_A"}
     return out
 
 
