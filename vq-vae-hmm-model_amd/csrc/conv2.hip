@@ -732,10 +732,16 @@ static int launch_c2f(const ConvArgs& a, hipStream_t s) {
   const int64_t want = cdiv(ntiles, 256);
   const int wpg = (int)(want < wmax ? (want > 0 ? want : 1) : wmax);
   const int64_t grid = cdiv(ntiles, wpg) < 256 ? cdiv(ntiles, wpg) : 256;
-  if (FKS == 3 && 3 * a.f_Kc <= 16)  // packed front taps, as launch_c2w runs the unfused front
-    conv2f_kernel<NB, TAIL, FKS, ACT, true><<<(unsigned)grid, 64 * wpg, Q::lds(wpg), s>>>(ap, ntiles);
-  else
-    conv2f_kernel<NB, TAIL, FKS, ACT, false><<<(unsigned)grid, 64 * wpg, Q::lds(wpg), s>>>(ap, ntiles);
+  bool pk = false;
+  if constexpr (FKS == 3) pk = 3 * a.f_Kc <= 16;  // packed front taps, as launch_c2w runs the unfused front
+  if constexpr (FKS == 3) {
+    if (pk) {
+      conv2f_kernel<NB, TAIL, FKS, ACT, true><<<(unsigned)grid, 64 * wpg, Q::lds(wpg), s>>>(ap, ntiles);
+      VQHMM_LAUNCH_CHECK();
+      return VQHMM_OK;
+    }
+  }
+  conv2f_kernel<NB, TAIL, FKS, ACT, false><<<(unsigned)grid, 64 * wpg, Q::lds(wpg), s>>>(ap, ntiles);
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
 }
