@@ -68,6 +68,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--profile-steps", type=int, default=5)
     ap.add_argument("--no-hmm", action="store_true", help="skip the Viterbi / forward-backward kernel lines")
+    ap.add_argument("--dp-form", action="store_true",
+                    help="N=1: run the data-parallel step form (fwd+bwd graph, RCCL all-reduce over a 1-rank "
+                         "process group, Adam graph) instead of the fused single-process step")
     return ap.parse_args()
 
 
@@ -294,7 +297,9 @@ def cpu_baseline(cfg, B, seconds):
 
 def spawn_ranks(n):
     """`python bench.py --gpus N` without torchrun: start N fresh rank processes (this
-    parent never touches the GPU) on 127.0.0.1 and return the worst exit code."""
+    parent never touches the GPU) on 127.0.0.1; report every rank's exit code or signal
+    and return the worst one."""
+    import signal
     import socket
     import subprocess
     with socket.socket() as so:
@@ -307,7 +312,15 @@ def spawn_ranks(n):
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
     codes = [p.wait() for p in procs]
     if any(codes):
-        print(f"bench.py: rank exit codes {codes}", file=sys.stderr)
+        def describe(c):
+            if c < 0:
+                try:
+                    return f"signal {signal.Signals(-c).name}"
+                except ValueError:
+                    return f"signal {-c}"
+            return f"exit {c}"
+        print("bench.py: rank exits: " + ", ".join(f"rank {r}: {describe(c)}" for r, c in enumerate(codes)),
+              file=sys.stderr)
     return max(abs(c) for c in codes)
 
 
@@ -336,6 +349,9 @@ def main():
             sys.exit("bench.py: process group size disagrees with WORLD_SIZE")
     else:
         torch.cuda.set_device(0)
+        if a.dp_form:  # a 1-rank RCCL group: the DP step's collective runs for real, on one GPU
+            torch.distributed.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % _free_port(),
+                                                 world_size=1, rank=0, device_id=torch.device("cuda", 0))
     import vqhmm
     from vqhmm import _ext
     lib = _ext.load()
@@ -353,7 +369,7 @@ def main():
         Bglob = B * world
     torch.manual_seed(0)
     model = vqhmm.VAE_HMM(D, H, K, H2, u_dim=U, trans_hidden=TH).cuda()
-    st = vqhmm.TrainState(model, lr=1e-3)
+    st = vqhmm.TrainState(model, lr=1e-3, dp_form=True if a.dp_form else None)
     g = torch.Generator(device="cuda").manual_seed(1234 + rank)
     x = torch.randn(B, D, T, device="cuda", generator=g)
     u = torch.randn(B, U, T, device="cuda", generator=g)
@@ -384,6 +400,7 @@ def main():
         elapsed = t.item()
     ms_per_step = elapsed / a.steps * 1e3
     value = Bglob * a.steps / elapsed
+    st.check_status()  # any device-side error word set during the timed steps raises here
 
     roof = None
     kernels = None
@@ -436,20 +453,46 @@ def main():
                        "global_batch": Bglob, "per_gpu_batch": B, "seq_len": T, "K": K, "input_dim": D,
                        "hidden_dim": H, "hidden_dim2": H2, "u_dim": U, "trans_hidden": TH,
                        "parallelism": f"dp{world}" if world > 1 else "single", "hip_graph": use_graph,
-                       "rccl_ranks": torch.distributed.get_world_size() if world > 1 else 0},
+                       "step_form": _step_form(st, use_graph),
+                       "collective": ({"backend": _backend_name(), "ranks": torch.distributed.get_world_size()}
+                                      if torch.distributed.is_initialized() else None)},
             "roofline": roof, "cpu_baseline": cpu,
             "step_kernels_us": kernels, "stage_roofline": stage_roof, "vq_cfg3": vq, **hmm,
         }
         if cpu:
             line["speedup_vs_cpu"] = round(value / cpu["value"], 1)
         print(json.dumps(line), flush=True)
-    if world > 1:
+    # ordered teardown: drop the captured graphs (and with them their memory pools) while the
+    # device and the communicator are alive, drain the device, then leave the process group
+    del step, st, model
+    torch.cuda.synchronize()
+    if torch.distributed.is_initialized():
+        torch.distributed.barrier()
         torch.distributed.destroy_process_group()
-        # a rank's result is already out; skip interpreter / runtime teardown (an intermittent
-        # nonzero exit of one rank there was seen in the 2-rank rehearsal, with no error text)
-        sys.stdout.flush()
-        sys.stderr.flush()
-        os._exit(0)
+
+
+def _step_form(st, use_graph):
+    if not st.dp_form:
+        return "fused (Adam in the backward's tail launch)" + (", one graph" if use_graph else ", eager")
+    if not use_graph:
+        return "dp, eager (fwd+bwd, all-reduce, Adam)"
+    if getattr(st, "step_graphs", 2) == 1:
+        return "dp, one graph (fwd+bwd, RCCL all-reduce and Adam captured together)"
+    return "dp, split graphs (fwd+bwd graph, host-issued all-reduce, Adam graph)"
+
+
+def _free_port():
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def _backend_name():
+    """The collective library the step's all-reduce actually runs on ("rccl" for the nccl backend
+    on ROCm; "gloo" in the CPU-side rehearsal)."""
+    b = str(torch.distributed.get_backend())
+    return "rccl" if b == "nccl" else b
 
 
 if __name__ == "__main__":

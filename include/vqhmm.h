@@ -37,6 +37,11 @@ extern "C" {
 #define VQHMM_EWORKSPACE -3
 #define VQHMM_EUNSUPPORTED -4
 
+/* Bits of the training step's device status word (vqhmm_elbo_status_offset).  Kernels only
+ * ever OR bits in; the caller zeroes the word when it allocates the workspace and reads it
+ * after a synchronisation (TrainState.check_status raises RuntimeError on any bit). */
+#define VQHMM_STATUS_TAIL_TIMEOUT 1ull /* the backward tail's in-launch wait for the reduced dWc ran out */
+
 /* Number of parameter tensors of a VAE_HMM, in nn.Module.parameters() order
  * (VQ_VAE_HMM_fixed.py:92-98 -> encoder :32-36, prior :44-57, decoder :74-79). */
 #define VQHMM_NPARAMS 18
@@ -148,6 +153,11 @@ int vqhmm_elbo_bwd_adam_f32(const vqhmm_dims_t* dims, const float* const* params
  * pieces [recon, prior, entropy] (for tests).  Host-only, no GPU access. */
 int vqhmm_elbo_pieces(const vqhmm_dims_t* dims, int64_t B, int64_t T, const void* workspace,
                       const float** loss, const float** pieces);
+
+/* Byte offset, inside an elbo workspace of this (dims, B, T), of the step's 8-byte device
+ * status word (VQHMM_STATUS_* bits).  The caller zeroes it once after allocating the
+ * workspace; the step's kernels never clear it.  Host-only. */
+int vqhmm_elbo_status_offset(const vqhmm_dims_t* dims, int64_t B, int64_t T, size_t* offset);
 
 /* Device addresses (inside the workspace) of the step's PCL activation and gradient
  * buffers, in this order: x, h1, h2, logits, q, g1, g2, par (mu|logvar), dpar, dg2, dg1,

@@ -58,3 +58,18 @@ def test_cpu_tensors_fail_loudly():
     import vqhmm
     with pytest.raises(RuntimeError, match="HIP"):
         vqhmm.vq_argmin(torch.zeros(1, 2, 3), torch.zeros(4, 2))
+
+
+@pytest.mark.parametrize("dims,B,T", [((5, 64, 3, 32, 4, 128), 1024, 200), ((16, 64, 8, 32, 4, 128), 512, 512),
+                                      ((64, 256, 32, 128, 4, 128), 8, 50)])
+def test_status_word_inside_workspace(dims, B, T):
+    """The step's device status word (vqhmm_elbo_status_offset) lies inside the workspace, 8-byte
+    aligned, for the configs' shapes (host-only query)."""
+    from vqhmm import _ext
+    lib = _ext.load()
+    d = _ext.Dims(*dims)
+    nb, off = ctypes.c_size_t(), ctypes.c_size_t()
+    assert lib.vqhmm_elbo_workspace_size(ctypes.byref(d), B, T, ctypes.byref(nb)) == 0
+    assert lib.vqhmm_elbo_status_offset(ctypes.byref(d), B, T, ctypes.byref(off)) == 0
+    assert off.value % 8 == 0 and off.value + 8 <= nb.value
+    assert lib.vqhmm_elbo_status_offset(ctypes.byref(d), 0, T, ctypes.byref(off)) == -1

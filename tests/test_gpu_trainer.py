@@ -116,7 +116,8 @@ def test_trainer_custom_loss_fn_matches_default():
 
 
 @pytest.mark.parametrize("B,K,D,H,H2,T", [(128, 3, 5, 64, 32, 200), (1024, 3, 5, 64, 32, 200),
-                                          (64, 8, 16, 64, 32, 96), (40, 32, 64, 80, 72, 50)])
+                                          (64, 8, 16, 64, 32, 96), (40, 32, 64, 80, 72, 50),
+                                          (24, 32, 64, 256, 128, 60)])  # cfg3 dims: thousands of tail blocks
 def test_fused_tail_adam_bit_identical(B, K, D, H, H2, T):
     """The single-process step's backward tail in one launch (tail_adam_kernel: slab reduction +
     composed dW / dE + Adam, with the in-launch wait for the dWc segment) against the split path
@@ -198,3 +199,72 @@ def test_fused_conv_pairs_match_separate_launches(tmp_path, dims):
     """enc_conv1 -> enc_conv2 and dec_conv1 -> dec_conv2 fused into one launch each (conv2f_kernel:
     14-row tiles, the front rows computed in-tile) against the two-launch path (VQHMM_CONV_FUSE=0)."""
     _run_both(tmp_path, "VQHMM_CONV_FUSE", dims)
+
+
+def test_tail_rerun_after_one_forward_is_identical():
+    """The backward (its one-launch tail included) run twice after ONE forward gives the same bits:
+    the tail re-arms its own dWc counters, so the second launch waits for its own reduction
+    (the counters used to be zeroed only by the forward's prologue)."""
+    import vqhmm
+    gen = torch.Generator().manual_seed(11)
+    B, D, T = 64, 5, 120
+    x = torch.randn(B, D, T, generator=gen).cuda()
+    u = torch.randn(B, 4, T, generator=gen).cuda()
+    L = torch.randint(20, T + 1, (B,), generator=gen)
+    torch.manual_seed(4)
+    m = vqhmm.VAE_HMM(D, 64, 3, 32, u_dim=4, trans_hidden=128).cuda()
+    st = vqhmm.TrainState(m, lr=1e-3)
+    xs, us, Ls = st.prepare(x, u, L)
+    st.forward_backward(xs, us, Ls, 0.5)
+    g1 = st.grad.clone()
+    ws = st.workspace(B, T)
+    d = __import__("ctypes").byref(st.dims)
+    from vqhmm import _ext
+    for _ in range(2):  # the backward alone, twice more, on the same forward
+        _ext.check(st.lib.vqhmm_elbo_bwd_f32(d, st.ptrs, _ext.ptr(xs), None, B, T, 0.5, None, _ext.ptr(ws),
+                                             ws.numel(), _ext.ptr(st.grad), _ext.stream_ptr()), "bwd")
+        torch.cuda.synchronize()
+        assert torch.equal(st.grad, g1)
+    st.check_status()
+
+
+_TIMEOUT_RUN = r"""
+import sys, torch
+sys.path.insert(0, sys.argv[1])
+import vqhmm
+gen = torch.Generator().manual_seed(5)
+x = torch.randn(32, 5, 80, generator=gen).cuda()
+u = torch.randn(32, 4, 80, generator=gen).cuda()
+L = torch.full((32,), 80, dtype=torch.int64)
+torch.manual_seed(3)
+m = vqhmm.VAE_HMM(5, 64, 3, 32, u_dim=4, trans_hidden=128).cuda()
+st = vqhmm.TrainState(m, lr=1e-3)
+st.step(x, u, L, 1.0)
+torch.cuda.synchronize()
+try:
+    st.check_status()
+except RuntimeError as e:
+    print("STATUS-RAISED:", e)
+    sys.exit(0)
+print("STATUS-CLEAN")
+"""
+
+
+@pytest.mark.parametrize("force", ["1", "0"])
+def test_tail_wait_timeout_is_reported(force):
+    """The backward tail's bounded in-launch wait (misc.hip tail_kernel) reports a timeout in the
+    step's device status word instead of falling through silently: VQHMM_TAIL_TEST_TIMEOUT=1 makes
+    the wait target unreachable with a short poll budget; TrainState.check_status must raise.
+    Without the switch the same step leaves the word clear."""
+    import os
+    import subprocess
+    import sys
+    from conftest import ROOT
+    pkg = os.path.join(ROOT, "vq-vae-hmm-model_amd")
+    r = subprocess.run([sys.executable, "-c", _TIMEOUT_RUN, pkg], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, VQHMM_TAIL_TEST_TIMEOUT=force))
+    assert r.returncode == 0, r.stderr[-2000:]
+    if force == "1":
+        assert "STATUS-RAISED" in r.stdout and "timed out" in r.stdout, r.stdout
+    else:
+        assert "STATUS-CLEAN" in r.stdout, r.stdout

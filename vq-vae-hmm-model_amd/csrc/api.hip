@@ -89,7 +89,8 @@ struct ElboPlan {
   float *sW1, *sb1, *sW2, *sb2, *sq0;
   float *loss, *pieces;
   int64_t* cnt;  // valid count written by the prologue (loss finalized in the backward)
-  unsigned long long* sync;  // the backward tail's in-launch dWc counter, zeroed by the prologue
+  unsigned long long* sync;  // [0] / [1] the backward tail's arrival / departure counters (zeroed by the
+                             // prologue and re-armed by the tail itself), [2] the status word, [3] spare
   // staged head (shapes the fused heads do not cover): Prior MLP as 1x1 convs
   bool staged;
   bool wave_head;  // head_wave.hip (else head_mfma / head.hip)
@@ -157,7 +158,7 @@ ElboPlan plan_elbo(const vqhmm_dims_t* d, int64_t B, int64_t T, void* ws) {
   p.loss = c.take<float>(1);
   p.pieces = c.take<float>(4);
   p.cnt = c.take<int64_t>(1);
-  p.sync = c.take<unsigned long long>(1);
+  p.sync = c.take<unsigned long long>(4);
   p.dg2 = c.take<float>(R * ld4(H));
   p.dg1 = c.take<float>(R * ld4(H));
   p.dqd = c.take<float>(R * ld4(K));
@@ -844,6 +845,15 @@ int vqhmm_elbo_pieces(const vqhmm_dims_t* d, int64_t B, int64_t T, const void* w
   ElboPlan p = plan_elbo(d, B, T, const_cast<void*>(ws));
   if (loss) *loss = p.loss;
   if (pieces) *pieces = p.pieces;
+  return VQHMM_OK;
+}
+
+int vqhmm_elbo_status_offset(const vqhmm_dims_t* d, int64_t B, int64_t T, size_t* offset) {
+  if (!dims_ok(d) || B <= 0 || T <= 0 || !offset) return VQHMM_EINVAL;
+  // a plan on a non-null base: only the carved offsets are used, nothing is dereferenced
+  char* const base = reinterpret_cast<char*>(4096);
+  const ElboPlan p = plan_elbo(d, B, T, base);
+  *offset = (size_t)(reinterpret_cast<char*>(p.sync + 2) - base);
   return VQHMM_OK;
 }
 

@@ -22,6 +22,7 @@
 #define VQHMM_ELAUNCH -2
 #define VQHMM_EWORKSPACE -3
 #define VQHMM_EUNSUPPORTED -4
+#define VQHMM_STATUS_TAIL_TIMEOUT 1ull
 
 namespace vqhmm {
 

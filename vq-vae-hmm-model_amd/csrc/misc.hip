@@ -292,13 +292,22 @@ __global__ __launch_bounds__(256) void compose_adam_kernel(ComposeAdamArgs a) {
 // columns it has just reduced), then the composed decoder conv1's dW / dE blocks
 // (compose_adam_block; ADAM: + their Adam).  Block order: [segment blocks][log_prior][loss
 // finalize][composed].  The composed blocks need the whole reduced dWc: every block of the dWc
-// segment releases its columns (device-scope fence) and adds 1 to *sync (zeroed by the step's
-// prologue); a composed block spins (bounded, relaxed polls, one acquire fence after) until *sync
-// reaches the segment's block count.  All blocks are co-resident (a few hundred 256-thread blocks)
-// and the dWc blocks precede the waiting ones in dispatch order.
+// segment drains its stores, releases them (agent fence) and adds 1 to sync[0]; a composed block
+// polls sync[0] (bounded, relaxed loads, one acquire fence after) until it reaches the segment's
+// block count.
+// Progress relies on IN-ORDER workgroup dispatch, not on co-residency: every dWc block has a lower
+// block index than every waiting block, so it is dispatched (and, never waiting itself, finishes)
+// before any waiting block can hold a CU slot it needs.  At cfg3 dims (H = 256) the grid is a few
+// thousand blocks, more than are resident at once; the H = 256 case of
+// tests/test_gpu_trainer.py::test_fused_tail_adam_bit_identical runs that shape.
+// sync[0] arrivals, sync[1] departures: the last composed block to depart zeroes both, so the next
+// launch (a re-run of the backward alone included) starts from 0 (the prologue zeroes them too).
+// sync[2] is the status word (VQHMM_STATUS_*): a wait that runs out of polls ORs in
+// VQHMM_STATUS_TAIL_TIMEOUT and its block skips the composed gradient; the host reads the word
+// (vqhmm_elbo_status_offset) and raises.  It is only ever set here, never cleared.
 template <bool ADAM>
 __global__ __launch_bounds__(256) void tail_kernel(TailArgs ta, ComposeAdamArgs a, int dwc_seg, int dwc_blocks,
-                                                   unsigned long long* sync) {
+                                                   unsigned long long* sync, int spin_limit, int ncomp) {
   __shared__ float part[16][64];
   __shared__ float red[256];
   __shared__ float scratch[256];
@@ -321,10 +330,15 @@ __global__ __launch_bounds__(256) void tail_kernel(TailArgs ta, ComposeAdamArgs 
     const int si = tail_segment_block(ta, part, &v, &col);
     const SlabSeg& sg = ta.s[si];
     if (si == dwc_seg) {
+      // producer hand-off (MI355X_MICROARCH.md, inter-workgroup visibility): every storing wave
+      // drains, barrier, one release, drain again (the compiler may drop the fence's own wait),
+      // then the relaxed agent-scope arrival
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (threadIdx.x == 0) {
-        __threadfence();
-        atomicAdd(sync, 1ull);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(sync, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     } else if (ADAM && threadIdx.x < 64 && col < sg.len) {
       adam_apply(ad, (sg.out - a.g) + col, v, e);
@@ -345,18 +359,45 @@ __global__ __launch_bounds__(256) void tail_kernel(TailArgs ta, ComposeAdamArgs 
     const bool dw = cb < cdiv((int64_t)a.H * a.H * 3, 256) && jw < (int64_t)a.H * a.H * 3;
     AdamElem e{};
     if (ADAM && dw) e = adam_load(ad, a.off_w + jw, tn);  // in flight across the wait
+    __shared__ int arrived;
     if (threadIdx.x == 0) {
-      for (int spin = 0; spin < (1 << 22); ++spin) {
+      int got = 0;
+      for (int spin = 0; spin < spin_limit; ++spin) {
         // relaxed: an acquire load would invalidate this XCD's L2 on every poll
-        if (__hip_atomic_load(sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned long long)dwc_blocks) break;
+        if (__hip_atomic_load(sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned long long)dwc_blocks) {
+          got = 1;
+          break;
+        }
         __builtin_amdgcn_s_sleep(1);
       }
+      if (!got)
+        __hip_atomic_fetch_or(sync + 2, (unsigned long long)VQHMM_STATUS_TAIL_TIMEOUT, __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT);
+      arrived = got;
     }
     __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    compose_adam_block<ADAM>(a, cb, tn, cpart, dw ? &e : nullptr);
+    if (arrived) compose_adam_block<ADAM>(a, cb, tn, cpart, dw ? &e : nullptr);
+    __syncthreads();
+    if (threadIdx.x == 0) {  // departure; the last one re-arms the counters for the next launch
+      const unsigned long long d = __hip_atomic_fetch_add(sync + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (d == (unsigned long long)(ncomp - 1)) {
+        __hip_atomic_store(sync, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(sync + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
   }
   if constexpr (ADAM) adam_ticket(ad.step, tn);
+}
+
+// Test hook, read once: VQHMM_TAIL_TEST_TIMEOUT=1 makes the composed blocks wait for a count that
+// never arrives, with a short poll budget, so a test can see the status word raised.
+static bool tail_test_timeout() {
+  static const bool v = [] {
+    const char* e = getenv("VQHMM_TAIL_TEST_TIMEOUT");
+    return e && e[0] == '1';
+  }();
+  return v;
 }
 
 int launch_tail(TailArgs& ta, const ComposeAdamArgs& ca, int dwc_seg, unsigned long long* sync, bool adam,
@@ -367,9 +408,16 @@ int launch_tail(TailArgs& ta, const ComposeAdamArgs& ca, int dwc_seg, unsigned l
   for (int i = 0; i < ta.nseg; ++i) ta.blk_start[i + 1] = ta.blk_start[i] + cdiv(ta.s[i].len, 64);
   const int64_t ncomp = cdiv((int64_t)ca.H * ca.H * 3, 256) + ca.K;
   const int64_t nb = ta.blk_start[ta.nseg] + (ta.q0slab ? 1 : 0) + (ta.fin_loss ? 1 : 0) + ncomp;
-  const int dwc_blocks = (int)cdiv(ta.s[dwc_seg].len, 64);
-  if (adam) tail_kernel<true><<<(unsigned)nb, 256, 0, s>>>(ta, ca, dwc_seg, dwc_blocks, sync);
-  else tail_kernel<false><<<(unsigned)nb, 256, 0, s>>>(ta, ca, dwc_seg, dwc_blocks, sync);
+  int dwc_blocks = (int)cdiv(ta.s[dwc_seg].len, 64);
+  int spin_limit = 1 << 22;  // x ~s_sleep(1): about 0.2 s before the wait gives up
+  if (tail_test_timeout()) {
+    dwc_blocks += 1 << 30;
+    spin_limit = 1 << 10;
+  }
+  if (adam)
+    tail_kernel<true><<<(unsigned)nb, 256, 0, s>>>(ta, ca, dwc_seg, dwc_blocks, sync, spin_limit, (int)ncomp);
+  else
+    tail_kernel<false><<<(unsigned)nb, 256, 0, s>>>(ta, ca, dwc_seg, dwc_blocks, sync, spin_limit, (int)ncomp);
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
 }
@@ -669,7 +717,7 @@ __device__ __forceinline__ void wimg_slice(const WImgJob& j, int64_t i0) {
 __global__ __launch_bounds__(256) void prologue_kernel(PrologueArgs a) {
   extern __shared__ float cs[];
   const unsigned bx = blockIdx.x;
-  if (bx == 0 && threadIdx.x == 0 && a.sync) *a.sync = 0ull;  // the backward tail's dWc counter
+  if (bx == 0 && threadIdx.x < 2 && a.sync) a.sync[threadIdx.x] = 0ull;  // the backward tail's counters
   if (bx < a.nbx) {
     to_pcl_slot(a.x, a.D, a.B, a.T, a.xsc, a.xst, a.xp, (int64_t)bx * 256 + threadIdx.x);
   } else if (bx < a.nbx + a.nbu) {

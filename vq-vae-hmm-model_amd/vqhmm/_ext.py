@@ -81,7 +81,11 @@ _SIGS = {
                                          c_vp, c_vp, c_sz, c_vp]),
     "vqhmm_argmax_f32": (ctypes.c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "vqhmm_elbo_debug_buffers": (ctypes.c_int, [ctypes.POINTER(Dims), c_i64, c_i64, c_vp, ctypes.POINTER(c_vp)]),
+    "vqhmm_elbo_status_offset": (ctypes.c_int, [ctypes.POINTER(Dims), c_i64, c_i64, ctypes.POINTER(c_sz)]),
 }
+
+# bits of the step's device status word (include/vqhmm.h VQHMM_STATUS_*)
+STATUS_BITS = {1: "the backward tail's in-launch wait for the reduced decoder-conv1 gradient timed out"}
 
 
 def load():

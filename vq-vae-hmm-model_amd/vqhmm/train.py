@@ -23,6 +23,7 @@ chain (`_backward_overlapped`).
 """
 import ctypes
 import os
+import sys
 
 import torch
 
@@ -49,7 +50,7 @@ def _overlap_default():
 
 class TrainState:
     def __init__(self, model, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, process_group=None, distributed=None,
-                 overlap_bwd=None):
+                 overlap_bwd=None, dp_form=None):
         params = model.ordered_parameters()
         dev = params[0].device
         if dev.type != "cuda":
@@ -73,12 +74,18 @@ class TrainState:
         self.loss = torch.zeros((), device=dev)
         self.epoch_acc = torch.zeros((), dtype=torch.float64, device=dev)
         self._ws = {}
+        self._status = {}
         self.lib = _ext.load()
         if distributed is None:
             distributed = torch.distributed.is_available() and torch.distributed.is_initialized()
         self.distributed = bool(distributed)
         self.pg = process_group
         self.world = torch.distributed.get_world_size(process_group) if self.distributed else 1
+        # the data-parallel step form (forward+backward, gradient all-reduce, Adam as its own launch):
+        # needed with more than one rank; dp_form=True forces it on a 1-rank group (bench --dp-form)
+        self.dp_form = (self.distributed and self.world > 1) if dp_form is None else bool(dp_form)
+        if self.dp_form and not self.distributed:
+            raise RuntimeError("vqhmm: dp_form needs an initialised torch.distributed process group")
         self.overlap_bwd = _overlap_default() if overlap_bwd is None else bool(overlap_bwd)
         self._side = None
         self._bwd_events = None
@@ -92,8 +99,23 @@ class TrainState:
             _ext.check(self.lib.vqhmm_elbo_workspace_size(ctypes.byref(self.dims), B, T, ctypes.byref(nb)),
                        "workspace")
             ws = torch.empty(nb.value, dtype=torch.uint8, device=self.device)
+            off = ctypes.c_size_t()
+            _ext.check(self.lib.vqhmm_elbo_status_offset(ctypes.byref(self.dims), B, T, ctypes.byref(off)),
+                       "status offset")
+            ws[off.value:off.value + 8].zero_()  # the kernels only ever set bits of it
             self._ws[key] = ws
+            self._status[key] = ws[off.value:off.value + 8].view(torch.int64)
         return ws
+
+    def check_status(self):
+        """Raise if any step since the workspaces were made set a bit of the device status word
+        (VQHMM_STATUS_*, e.g. the backward tail's bounded in-launch wait ran out).  Reads one
+        8-byte word per workspace: call it where the host syncs anyway (once per epoch)."""
+        for key, word in self._status.items():
+            v = int(word.item())
+            if v:
+                what = "; ".join(m for b, m in _ext.STATUS_BITS.items() if v & b) or f"status 0x{v:x}"
+                raise RuntimeError(f"vqhmm: training step (B, T) = {key} reported a device error: {what}")
 
     def prepare(self, x, u, lengths):
         dev = self.device
@@ -182,7 +204,7 @@ class TrainState:
         _ext.check(rc, "elbo backward + adam")
 
     def _fused_adam_ok(self, max_norm=None):
-        return not (self.distributed and self.world > 1) and max_norm is None and not self.overlap_bwd
+        return not self.dp_form and max_norm is None and not self.overlap_bwd
 
     def _step_device(self, x, u, lengths, beta, norm=None, max_norm=None):
         """One step on device tensors (no host sync)."""
@@ -198,7 +220,7 @@ class TrainState:
             self.apply_adam(scale=1.0)
 
     def reduce_gradients(self):
-        if self.distributed and self.world > 1:
+        if self.dp_form:
             torch.distributed.all_reduce(self.grad, op=torch.distributed.ReduceOp.SUM, group=self.pg)
 
     def grad_scale(self, global_norm=False):
@@ -246,12 +268,13 @@ class TrainState:
     def capture(self, x, u, lengths, beta, warmup=2, norm=None):
         """Capture one fixed-shape step into HIP graphs; returns a replay callable.
 
-        Single process: the whole step is one graph.  Multi-rank: forward+backward
-        and Adam are two graphs and the gradient all-reduce runs between them on
-        the same stream (the collective stays outside the graphs, so no
-        graph-capture support is required of the communicator)."""
+        Single process: the whole step is one graph.  Data-parallel form over RCCL:
+        forward+backward, the gradient all-reduce and Adam captured as ONE graph; with
+        gloo (which cannot be captured), a communicator that refuses capture, or
+        VQHMM_DP_GRAPH=0: forward+backward and Adam are two graphs and the all-reduce
+        runs between them from the host.  self.step_graphs says which (1 or 2)."""
         x, u, lengths = self.prepare(x, u, lengths)
-        split = self.distributed and self.world > 1
+        split = self.dp_form
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
@@ -262,7 +285,26 @@ class TrainState:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 self._step_device(x, u, lengths, beta, norm)
+            self.step_graphs = 1
             return g.replay
+        backend = str(torch.distributed.get_backend(self.pg))
+        if backend == "nccl" and _dp_graph_default():
+            # the whole DP step, RCCL all-reduce included, as ONE graph: no host hop between the
+            # backward, the collective and Adam (B = 128 on one GPU, 1-rank RCCL group: 0.159 ->
+            # 0.142 ms/step).  A communicator that refuses capture falls back to the split form.
+            g = torch.cuda.CUDAGraph()
+            try:
+                with torch.cuda.graph(g):
+                    self.forward_backward(x, u, lengths, beta, norm)
+                    self.reduce_gradients()
+                    self.apply_adam(norm is not None)
+            except RuntimeError as e:  # pragma: no cover - depends on the RCCL build
+                print(f"vqhmm: all-reduce could not be captured in the step graph ({e}); using split graphs",
+                      file=sys.stderr)
+            else:
+                self.step_graphs = 1
+                return g.replay
+        self.step_graphs = 2
         g_fb, g_adam = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         with torch.cuda.graph(g_fb):
             self.forward_backward(x, u, lengths, beta, norm)
@@ -276,6 +318,11 @@ class TrainState:
         return replay
 
 
+def _dp_graph_default():
+    # VQHMM_DP_GRAPH=0: the split form (fwd+bwd graph, all-reduce issued from the host, Adam graph), A/B
+    return os.environ.get("VQHMM_DP_GRAPH", "1") != "0"
+
+
 def train_model(model, dataloader, num_epochs=10, lr=1e-3):
     """Drop-in for VQ_VAE_HMM_fixed.train_model (:145-162): Adam(lr) with
     default betas/eps, beta warm-up min(1, 2(ep+1)/E), same epoch print."""
@@ -287,6 +334,7 @@ def train_model(model, dataloader, num_epochs=10, lr=1e-3):
         for x, u, lengths in dataloader:
             state.step(x, u, lengths, beta)
         epoch_loss = state.epoch_acc.item()
+        state.check_status()
         print(f"Epoch {ep+1}/{num_epochs}, Loss: {epoch_loss/len(dataloader):.4f}")
     state.publish_grads()
     return model
@@ -343,7 +391,9 @@ class Trainer:
                 st.step(x, u, lengths, beta, max_norm=self.max_norm)
             else:
                 self._custom_step(loss_fn, x, u, lengths)
-        return st.epoch_acc.item() / len(dataloader)
+        avg = st.epoch_acc.item() / len(dataloader)
+        st.check_status()
+        return avg
 
     def train(self, dataloader, num_epochs=100, use_beta_warmup=True):
         for ep in range(num_epochs):
