@@ -1,0 +1,56 @@
+"""The fused ELBO heads across the shapes that select them (csrc/api.hip plan_elbo):
+
+  head_wave.hip  K <= 4, U <= 4, TH in {64, 128}      (cfg1 / cfg2)
+  head_k8.hip    5 <= K <= 8, U <= 4, TH 64/128/256   (cfg4: K = 8, D = 16)
+  head_mfma.hip  K <= 4, U in 5..7, TH in {64, 128}
+  staged         everything else (cfg3: K = 32)
+
+Each case is one training step's loss (1e-5 relative vs the fp32 CPU oracle) and all 18
+gradients (normwise vs the fp64 oracle on the device forward's ReLU branch), through
+check_step_vs_oracle; U < 4 covers the bias column of u' = [u, 1] (VQ_VAE_HMM_fixed.py:53-57)."""
+import pytest
+import torch
+
+from test_gpu_configs import check_step_vs_oracle
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    # (D, H, K, H2, U, TH), B, T
+    ((16, 32, 8, 16, 4, 128), 24, 70),
+    ((16, 32, 8, 16, 4, 128), 96, 200),    # > 512 windows: workgroups loop over windows
+    ((5, 32, 5, 16, 4, 64), 24, 70),
+    ((7, 32, 6, 16, 3, 256), 16, 60),
+    ((16, 32, 7, 16, 2, 128), 20, 45),
+    ((16, 32, 8, 16, 1, 64), 12, 33),
+    ((5, 32, 3, 16, 2, 64), 24, 70),       # head_wave, U < 4
+    ((5, 32, 3, 16, 3, 128), 24, 70),
+    ((5, 32, 4, 16, 5, 64), 24, 70),       # head_mfma, U = 5..7
+    ((5, 32, 2, 16, 6, 128), 24, 70),
+    ((5, 32, 3, 16, 7, 64), 24, 70),
+]
+
+
+@pytest.mark.parametrize("dims,B,T", CASES)
+def test_head_shapes_vs_oracle(dims, B, T):
+    check_step_vs_oracle(dims, B, T, seed=B * 100 + T, rtol_norm=1e-5)
+
+
+@pytest.mark.parametrize("dims", [(16, 64, 8, 32, 4, 128), (5, 64, 3, 32, 4, 128)])
+def test_head_forward_only_matches_training_loss(dims):
+    """compute_loss without autograd (need_grad = 0: no gradient buffers or slabs written) gives
+    the same loss bits as the training forward."""
+    import vqhmm
+    D, H, K, H2, U, TH = dims
+    torch.manual_seed(1)
+    m = vqhmm.VAE_HMM(D, H, K, H2, u_dim=U, trans_hidden=TH).cuda()
+    gen = torch.Generator().manual_seed(3)
+    B, T = 40, 90
+    x = torch.randn(B, D, T, generator=gen).cuda()
+    u = torch.randn(B, U, T, generator=gen).cuda()
+    L = torch.randint(10, T + 1, (B,), generator=gen)
+    with torch.no_grad():
+        l0 = m.compute_loss(x, u, L, 0.8).item()
+    l1 = m.compute_loss(x, u, L, 0.8)
+    l1.backward()
+    assert l0 == l1.item()

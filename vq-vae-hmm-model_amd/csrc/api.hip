@@ -93,7 +93,8 @@ struct ElboPlan {
                              // prologue and re-armed by the tail itself), [2] the status word, [3] spare
   // staged head (shapes the fused heads do not cover): Prior MLP as 1x1 convs
   bool staged;
-  bool wave_head;  // head_wave.hip (else head_mfma / head.hip)
+  bool wave_head;  // head_wave.hip (K <= 4)
+  bool k8_head;    // head_k8.hip (5 <= K <= 8); else head_mfma / head.hip
   float *hid, *lgA, *dhid, *nx, *dqc, *trw, *logpi;
   // backward
   float *dg2, *dg1, *dqd, *dlog, *dh2, *dh1, *dWc;
@@ -127,9 +128,11 @@ ElboPlan plan_elbo(const vqhmm_dims_t* d, int64_t B, int64_t T, void* ws) {
   {
     HeadArgs hc{};
     hc.K = K; hc.U = p.U; hc.TH = p.TH; hc.D = D;
+    hc.R = R;
     p.wave_head = head_mfma_supported(hc) && p.U <= 4 && !head_legacy();
+    p.k8_head = !p.wave_head && head_k8_supported(hc) && !head_legacy();
   }
-  p.hgrid = p.wave_head ? head_wave_grid(R) : head_grid(R);
+  p.hgrid = p.wave_head ? head_wave_grid(R) : p.k8_head ? head_k8_grid(R) : head_grid(R);
   p.dpar = c.take<float>(R * ld4(2 * D));
   p.dqx = c.take<float>(R * ld4(K));
   p.dlx = c.take<float>(R * ld4(K));
@@ -601,6 +604,7 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       h.dpar = p.dpar; h.dqx = p.dqx; h.dlx = p.dlx; h.part = p.part;
       h.slab_W1 = p.sW1; h.slab_b1 = p.sb1; h.slab_W2 = p.sW2; h.slab_b2 = p.sb2; h.slab_q0 = p.sq0;
       if (p.wave_head) return launch_head_wave(h, p.hgrid, s);
+      if (p.k8_head) return launch_head_k8(h, p.hgrid, s);
       return launch_head(h, p.hgrid, s);
     }
     case S_FINAL:
@@ -678,8 +682,8 @@ void stage_work(const ElboPlan& p, int st, double* flops, double* bytes, int* mf
     *flops = N * (4.0 * p.TH * p.U + 6.0 * p.TH * KK + 20.0 * p.D + 12.0 * KK);
     *bytes = 4.0 * R * (2 * p.D + p.D + p.U + 2 * p.K + 2 * p.D + 2 * p.K);
     HeadArgs h{};
-    h.K = p.K; h.U = p.U; h.TH = p.TH; h.D = p.D;
-    *mfma = head_mfma_supported(h) ? 1 : 0;
+    h.K = p.K; h.U = p.U; h.TH = p.TH; h.D = p.D; h.R = p.R;
+    *mfma = (head_mfma_supported(h) || head_k8_supported(h)) ? 1 : 0;
   } else if (st == S_TOPCL) {
     *bytes = 4.0 * (N * (p.D + p.U) + R * (ld4(p.D) + ld4(p.U)));
   } else if (st == S_LOGIT_BWD) {

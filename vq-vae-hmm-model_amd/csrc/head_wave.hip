@@ -161,7 +161,9 @@ __global__ __launch_bounds__(256, 2) void elbo_head_wave_kernel(HeadArgs a) {
       f32x4 b, w2v;
     };
     auto ldw = [&](int hb, AW& w) {  // u' = [u, 1]: the bias column is the accumulator's start
-      w.w1a = sh.W1S[(hb * 16 + l16) * 8 + lg4];
+      // only u' columns c < U: column U holds the bias (1), which starts the accumulator instead
+      // (with U < 4 the k = 4 contraction would otherwise add b1 a second time)
+      w.w1a = lg4 < U ? sh.W1S[(hb * 16 + l16) * 8 + lg4] : 0.f;
 #pragma unroll
       for (int v = 0; v < 4; ++v) w.b[v] = sh.W1S[(hb * 16 + 4 * lg4 + v) * 8 + U];
       w.w2v = *reinterpret_cast<const f32x4*>(&sh.W2S[l16 * S::LDW2 + hb * 16 + 4 * lg4]);
@@ -205,7 +207,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_wave_kernel(HeadArgs a) {
     float ua[NBW], dla[NBW][SD], dlt[NBW][4], ub[NBW][4];
 #pragma unroll
     for (int i = 0; i < NBW; ++i) {
-      ua[i] = W.uS[(i * 16 + l16) * 8 + lg4];                                                      // u'[row l16][c lg4]
+      ua[i] = lg4 < U ? W.uS[(i * 16 + l16) * 8 + lg4] : 0.f;                                      // u'[row l16][c lg4], c < U
 #pragma unroll
       for (int s = 0; s < SD; ++s) dla[i][s] = W.dlgS[(i * 16 + l16) * LGS + 4 * s + lg4];         // dlg[row l16][ij 4s+lg4]
 #pragma unroll

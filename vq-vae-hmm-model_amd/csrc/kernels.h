@@ -260,6 +260,10 @@ int head_wave_grid(int64_t R);
 int launch_head_wave(const HeadArgs& a, int grid, hipStream_t s);
 bool head_mfma_supported(const HeadArgs& a);
 int launch_head_mfma(const HeadArgs& a, int grid, hipStream_t s);
+// 5 <= K <= 8 MFMA head (head_k8.hip): U <= 4, TH in {64, 128, 256}, D <= 16; its grid / slab count
+bool head_k8_supported(const HeadArgs& a);
+int head_k8_grid(int64_t R);
+int launch_head_k8(const HeadArgs& a, int grid, hipStream_t s);
 int launch_head(const HeadArgs& a, int grid, hipStream_t s);
 int launch_prior_fwd(const PriorArgs& p, hipStream_t s);
 // Prior.forward on MFMA (prior.hip): K*K <= 64, U <= 4, TH in {64, 128, 256}
