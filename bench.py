@@ -275,24 +275,31 @@ def _oracle_step_times(cfg, B, threads, seconds, min_steps, warmup):
 
 def cpu_baseline(cfg, B, seconds):
     """CPU oracle (oracle/ref_model.py, pinned bit-exact to the reference) train step on the
-    same shape: all the host threads this process may use (>= 3 warm-up steps, ~`seconds`
-    of timed steps), plus a 1-thread figure on a 256-sequence sample of the same workload."""
+    same shape.  First a thread sweep (1, 2, 4, ... up to the host threads this process may
+    use; 1 warm-up + 2 timed full-batch steps each), then ~`seconds` of full-batch steps
+    (>= 3 warm-up) at the sweep's fastest thread count, which is what `cores` states."""
     nthr, n_aff = host_threads()
     saved = torch.get_num_threads()
+    counts = sorted({c for c in (1, 2, 4, 8, 16, 32, 64) if c <= nthr} | {nthr})
+    sweep = {}
     try:
-        med, n = _oracle_step_times(cfg, B, nthr, seconds, 3, 3)
-        B1 = min(B, 256)
-        med1, n1 = _oracle_step_times(cfg, B1, 1, 0.0, 3, 1)
+        for c in counts:
+            med, _ = _oracle_step_times(cfg, B, c, 0.0, 2, 1)
+            sweep[c] = B / med
+        best = max(sweep, key=sweep.get)
+        med, n = _oracle_step_times(cfg, B, best, seconds, 3, 3)
     finally:
         torch.set_num_threads(saved)
     _, T = cfg[0], cfg[1]
-    return {"value": round(B / med, 1), "unit": "sequences/s", "cores": nthr, "kind": "port",
-            "sample": f"{n} full train steps (B={B}, T={T}) of the torch-CPU oracle after 3 warm-up steps, "
-                      f"median {med*1e3:.1f} ms/step, {nthr} threads ({n_aff} CPUs in the affinity mask, "
-                      f"capped by the cgroup quota / OMP_NUM_THREADS)",
-            "one_thread": {"value": round(B1 / med1, 1), "unit": "sequences/s", "cores": 1,
-                           "sample": f"{n1} train steps of B={B1}, T={T} after 1 warm-up, "
-                                     f"median {med1*1e3:.1f} ms/step"}}
+    scales = sweep[best] >= 1.2 * sweep[1]
+    return {"value": round(B / med, 1), "unit": "sequences/s", "cores": best, "kind": "port",
+            "sample": f"{n} full train steps (B={B}, T={T}) of the torch-CPU oracle after 3 warm-up steps at "
+                      f"the thread sweep's fastest count ({best} of {nthr} usable threads; {n_aff} CPUs in the "
+                      f"affinity mask, capped by the cgroup quota / OMP_NUM_THREADS), median {med*1e3:.1f} ms/step",
+            "thread_sweep": {"batch": B, "seq_per_s": {str(c): round(v, 1) for c, v in sweep.items()},
+                             "interop_threads": torch.get_num_interop_threads()},
+            "note": None if scales else
+            f"the host does not scale this workload: {best} threads give {sweep[best] / sweep[1]:.2f}x one thread"}
 
 
 def spawn_ranks(n):

@@ -44,10 +44,10 @@ def vq_argmin_np(z, codebook):
 def quantize_f32(z, codebook, idx, beta=0.25):
     """pseudocode.txt:11-18 in fp32 numpy on channels-first z (B, Dv, T), given the
     argmin indices idx (B, T) (c_oracle.vq_argmin: the kernel contract):
-      z_q      = codebook[idx]                         (quantize, :11)
-      z_q_st   = z + (z_q - z)   [value of z_e + (z_q - z_e).detach(), :12]
-      commit   = beta * mean((z - z_q)^2)               (:16)
-      cb_loss  = mean((z_q - z)^2)                      (:17)
+      z_q      = codebook[idx]                         (quantize, :12)
+      z_q_st   = z + (z_q - z)   [value of z_e + (z_q - z_e).detach(), :13]
+      commit   = beta * mean((z - z_q)^2)               (:17)
+      cb_loss  = mean((z_q - z)^2)                      (:18)
     and the gradients autograd gives them for a loss sum(w * z_q_st) + commit + cb_loss:
       dz        = w + beta * 2 (z - z_q) / N            (ST passes w straight through)
       dcodebook = sum over positions n with idx = k of 2 (z_q - z)_n / N

@@ -99,6 +99,22 @@ def decoder_params(p, q, masks=None):
     return out[:, :half, :], out[:, half:, :]
 
 
+def preactivations(p, x):
+    """The four conv pre-activations whose sign is a ReLU decision, on this oracle's own
+    branch: encoder conv1 / conv2 (:39-40) and decoder conv1 / conv2 (:85-86), each (B, C, T).
+    Test infrastructure: bounds how far a device forward's ReLU patterns may differ from the
+    oracle's (tests/test_gpu_configs.py)."""
+    with torch.no_grad():
+        z1 = F.conv1d(x, p["encoder.conv1.weight"], p["encoder.conv1.bias"], padding=1)
+        z2 = F.conv1d(F.relu(z1), p["encoder.conv2.weight"], p["encoder.conv2.bias"], padding=1)
+        logits = F.conv1d(F.relu(z2), p["encoder.to_logits.weight"], p["encoder.to_logits.bias"])
+        q = F.softmax(logits, dim=1)
+        emb = torch.matmul(q.transpose(1, 2), p["decoder.embeddings.weight"]).transpose(1, 2)
+        y1 = F.conv1d(emb, p["decoder.conv1.weight"], p["decoder.conv1.bias"], padding=1)
+        y2 = F.conv1d(F.relu(y1), p["decoder.conv2.weight"], p["decoder.conv2.bias"], padding=1)
+    return z1, z2, y1, y2
+
+
 def elbo_terms(p, x, u, lengths, K, u_dim, norm=None, relu_masks=None):
     """Returns the named pieces of the mean-field ELBO (reference :106-135).
 

@@ -39,7 +39,7 @@ def relu_masks(st, B, T):
     return out
 
 
-def check_step_vs_oracle(dims, B, T, seed, full_frac=0.5, rtol_norm=2e-6):
+def check_step_vs_oracle(dims, B, T, seed, full_frac=0.5, rtol_norm=2e-6, independent=False):
     """The training step (loss + 18 grads) at (B, T) vs the oracle:
       loss   within 1e-5 relative of the fp32 CPU oracle (the reference's arithmetic);
       grads  within 2e-6 normwise of the fp64 oracle evaluated on the device forward's own
@@ -48,6 +48,12 @@ def check_step_vs_oracle(dims, B, T, seed, full_frac=0.5, rtol_norm=2e-6):
              ~1e-5 (tools/stage_accuracy.py: 1-2 flips per layer, cpu-fp32 has its own);
              on a fixed branch the device grads sit ~2e-7 from fp64 (64-channel layers;
              the 256-channel layers' 768-term fp32 chains are held to 1e-5).
+      masks  the device's ReLU patterns against the fp64 oracle's OWN decisions: at most
+             max(4, 1e-6 of the elements) differ per layer, each at a pre-activation within
+             1e-4 of 0 relative to the layer's largest |pre-activation| (a forward bug that
+             flips or zeroes activations cannot hide behind the branch-conditioned oracle).
+      independent=True: also every gradient against the fp32 CPU oracle's autograd on ITS
+             own branch, 1e-5 normwise (round 1's check, no device information used).
     The autograd surface (compute_loss + backward) must give the same bits as TrainState."""
     import vqhmm
     D, H, K, H2, U, TH = dims
@@ -60,7 +66,10 @@ def check_step_vs_oracle(dims, B, T, seed, full_frac=0.5, rtol_norm=2e-6):
     L = torch.randint(20 if T > 20 else 1, T + 1, (B,), generator=gen)
     L[:int(B * full_frac)] = T
     p32 = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
-    ref_loss = RM.elbo(p32, x, u, L, 1.0, K, U).item()
+    ref = RM.elbo(p32, x, u, L, 1.0, K, U)
+    ref_loss = ref.item()
+    if independent:
+        ref.backward()
 
     mg = m.cuda()
     loss = mg.compute_loss(x.cuda(), u.cuda(), L, 1.0)
@@ -74,11 +83,22 @@ def check_step_vs_oracle(dims, B, T, seed, full_frac=0.5, rtol_norm=2e-6):
     assert st.loss.item() == loss.item()
     masks = relu_masks(st, B, T)
     p64 = {k: v.double().requires_grad_(True) for k, v in sd.items()}
+    for name, mk, pre in zip(("enc conv1", "enc conv2", "dec conv1", "dec conv2"), masks,
+                             RM.preactivations({k: v.detach() for k, v in p64.items()}, x.double())):
+        diff = mk != (pre > 0)
+        nd = int(diff.sum())
+        assert nd <= max(4, int(1e-6 * pre.numel())), f"{name}: {nd} ReLU decisions differ from the oracle's"
+        if nd:
+            worst = pre[diff].abs().max().item() / max(pre.abs().max().item(), 1e-30)
+            assert worst <= 1e-4, f"{name}: a flipped ReLU decision at |pre| = {worst:.2e} of the layer max"
     RM.elbo(p64, x.double(), u.double(), L, 1.0, K, U, relu_masks=masks).backward()
     for i, name in enumerate(vqhmm.PARAM_ORDER):
         g = st.grad[st.off[i]:st.off[i + 1]].view_as(auto[name])
         assert torch.equal(g, auto[name]), name
         assert_grad_close(g.cpu().numpy(), p64[name].grad.numpy(), name, rtol_norm=rtol_norm, rtol_max=10 * rtol_norm)
+        if independent:
+            assert_grad_close(g.cpu().numpy(), p32[name].grad.numpy(), name + " (fp32 oracle, own branch)",
+                              rtol_norm=1e-5, rtol_max=1.0)
 
 
 def test_cfg4_shard_train_step_vs_oracle():

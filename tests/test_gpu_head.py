@@ -54,3 +54,39 @@ def test_head_forward_only_matches_training_loss(dims):
     l1 = m.compute_loss(x, u, L, 0.8)
     l1.backward()
     assert l0 == l1.item()
+
+
+@pytest.mark.parametrize("dims", [(5, 64, 3, 32, 4, 128), (16, 64, 8, 32, 4, 128)])
+@pytest.mark.parametrize("where", ["u", "logvar_bias", "transition_w2"])
+def test_head_propagates_nan_like_the_reference(dims, where):
+    """A NaN input or parameter gives a NaN loss, as the reference's torch arithmetic does
+    (relu(NaN) = NaN, exp(NaN) = NaN): the head's ReLU / max / clamp must not swallow it
+    (head kernels built with -fno-honor-nans)."""
+    import vqhmm
+    from oracle import ref_model as RM
+    D, H, K, H2, U, TH = dims
+    torch.manual_seed(2)
+    m = vqhmm.VAE_HMM(D, H, K, H2, u_dim=U, trans_hidden=TH)
+    gen = torch.Generator().manual_seed(7)
+    B, T = 8, 40
+    x = torch.randn(B, D, T, generator=gen)
+    u = torch.randn(B, U, T, generator=gen)
+    L = torch.full((B,), T)
+    with torch.no_grad():
+        if where == "u":
+            u[3, 1, 17] = float("nan")
+        elif where == "logvar_bias":
+            m.decoder.to_params.bias[D] = float("nan")
+        else:
+            m.prior.transition_net[2].weight[0, 5] = float("nan")
+    p = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    ref = RM.elbo(p, x, u, L, 1.0, K, U).item()
+    assert ref != ref  # the reference's arithmetic: NaN
+    mg = m.cuda()
+    with torch.no_grad():
+        got = mg.compute_loss(x.cuda(), u.cuda(), L, 1.0).item()
+    assert got != got, got
+    st = vqhmm.TrainState(mg, lr=1e-3)
+    xs, us, Ls = st.prepare(x, u, L)
+    st.forward_backward(xs, us, Ls, 1.0)
+    assert st.loss.item() != st.loss.item()

@@ -162,11 +162,12 @@ def test_train_model_lines(case):
 
 
 def test_cfg2_full_size_vs_oracle():
-    """BASELINE cfg2 (B=1024, T=200, K=3, D=5, H=64): loss vs the fp32 CPU oracle and all
-    gradients vs the fp64 oracle on the device forward's ReLU branch, variable lengths
-    (tests/test_gpu_configs.py:check_step_vs_oracle)."""
+    """BASELINE cfg2 (B=1024, T=200, K=3, D=5, H=64): loss vs the fp32 CPU oracle; all
+    gradients vs the fp64 oracle on the device forward's ReLU branch AND, independently, vs the
+    fp32 CPU oracle's autograd on its own branch (1e-5 normwise); the device's ReLU decisions
+    vs the oracle's own (tests/test_gpu_configs.py:check_step_vs_oracle), variable lengths."""
     from test_gpu_configs import check_step_vs_oracle
-    check_step_vs_oracle((5, 64, 3, 32, 4, 128), 1024, 200, seed=1234)
+    check_step_vs_oracle((5, 64, 3, 32, 4, 128), 1024, 200, seed=1234, independent=True)
 
 
 @pytest.mark.parametrize("B", [256, 128])

@@ -35,6 +35,9 @@ __device__ __forceinline__ f32x4 mfma16x16x4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// torch.relu: a NaN input stays NaN (fmaxf / v_max_f32 return the other operand, 0, for it)
+__device__ __forceinline__ float relu_f(float x) { return x <= 0.f ? 0.f : x; }
+
 __host__ __device__ __forceinline__ int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 __host__ __device__ __forceinline__ int ld4(int c) { return (c + 3) & ~3; }
 

@@ -147,7 +147,7 @@ __global__ __launch_bounds__(256) void conv_mm_kernel(ConvArgs a) {
     if (n < a.N && row_bt(r, a.R, a.T, b, t)) {
       y = Ys[row * LDY + col] * sc;
       if (a.bias) y += a.bias[n];
-      if (a.act == 1) y = fmaxf(y, 0.f);
+      if (a.act == 1) y = relu_f(y);
       else if (a.act == 2) y = a.aux[r * ld4(a.N) + n] > 0.f ? y : 0.f;
     }
     Ys[row * LDY + col] = y;

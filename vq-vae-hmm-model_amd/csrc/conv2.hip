@@ -178,7 +178,7 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a, int64_t m0, in
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
           float yy = acc[nb][pb][v] * sc + bias_r[nb][v];
-          if (ACT == 1) yy = fmaxf(yy, 0.f);
+          if (ACT == 1) yy = relu_f(yy);
           if (ACT == 2) {
             const float av = v == 0 ? auxv[nb][pb].x : v == 1 ? auxv[nb][pb].y : v == 2 ? auxv[nb][pb].z : auxv[nb][pb].w;
             yy = av > 0.f ? yy : 0.f;

@@ -31,7 +31,7 @@ __device__ __forceinline__ void prior_row(const HeadArgs& a, const float* uv, fl
 #pragma unroll
     for (int c = 0; c < UM; ++c)
       if (c < a.U) hv = fmaf(a.W1[h * a.U + c], uv[c], hv);
-    hv = fmaxf(hv, 0.f);
+    hv = relu_f(hv);
 #pragma unroll
     for (int ij = 0; ij < KM * KM; ++ij)
       if (ij < KK) la[ij] = fmaf(a.W2[(int64_t)ij * a.TH + h], hv, la[ij]);
@@ -156,7 +156,7 @@ __global__ __launch_bounds__(256) void elbo_head_kernel(HeadArgs a) {
             const float lv = a.par[r * ld4(2 * D) + D + c];
             const float xv = a.x[r * ld4(D) + c];
             const float ev = __expf(lv);
-            const float var = fmaxf(ev, 1e-8f);
+            const float var = (ev < 1e-8f ? 1e-8f : ev)  /* clamp(min=1e-8), NaN stays NaN */;
             const float df = mu - xv;
             const float r2 = df * df / var;
             s_rec += 0.5f * (__logf(6.2831855f * var) + r2);
@@ -286,7 +286,7 @@ __global__ __launch_bounds__(256) void elbo_head_kernel(HeadArgs a) {
         float pre = b1h;
 #pragma unroll
         for (int c = 0; c < UM; ++c) pre = fmaf(w1r[c], uv[c], pre);
-        const float hv = fmaxf(pre, 0.f);
+        const float hv = relu_f(pre);
         float dh = 0.f;
 #pragma unroll
         for (int ij = 0; ij < KM * KM; ++ij) {
@@ -434,7 +434,7 @@ __global__ __launch_bounds__(256) void prior_fwd_wave_kernel(PriorArgs p) {
     for (int h = lane; h < p.TH; h += 64) {
       float v = p.b1[h];
       for (int c = 0; c < p.U; ++c) v = fmaf(p.W1[(int64_t)h * p.U + c], u[(int64_t)c * p.u_sc], v);
-      hS[wave][h] = fmaxf(v, 0.f);
+      hS[wave][h] = relu_f(v);
     }
     __builtin_amdgcn_wave_barrier();
     for (int ij = lane; ij < KK; ij += 64) {

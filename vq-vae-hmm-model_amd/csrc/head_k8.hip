@@ -230,7 +230,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_k8_kernel(HeadArgs a) {
 #pragma unroll
         for (int v = 0; v < 4; ++v)
 #pragma unroll
-          for (int rb = 0; rb < 2; ++rb) lg[rb] = mfma16x16x4(w2v[v], fmaxf(hc[rb][v], 0.f), lg[rb]);
+          for (int rb = 0; rb < 2; ++rb) lg[rb] = mfma16x16x4(w2v[v], relu_f(hc[rb][v]), lg[rb]);
       }
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb)
@@ -283,7 +283,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_k8_kernel(HeadArgs a) {
       float dmu = 0.f, dlv = 0.f;
       if (own && m && ch < D) {
         const float ev = __expf(cur.lv[k]);
-        const float var = fmaxf(ev, 1e-8f);
+        const float var = (ev < 1e-8f ? 1e-8f : ev)  /* clamp(min=1e-8), NaN stays NaN */;
         const float df = cur.mu[k] - cur.x[k];
         const float r2 = df * df / var;
         s_rec += 0.5f * (__logf(6.2831855f * var) + r2);
@@ -350,7 +350,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_k8_kernel(HeadArgs a) {
         f32x4 hr, dm;
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-          hr[v] = fmaxf(h[v], 0.f);
+          hr[v] = relu_f(h[v]);
           dm[v] = h[v] > 0.f ? dh[v] : 0.f;
         }
 #pragma unroll

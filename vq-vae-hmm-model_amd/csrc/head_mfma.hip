@@ -170,7 +170,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_mfma_kernel(HeadArgs a) {
 #pragma unroll
       for (int i = 0; i < NP; ++i)
 #pragma unroll
-        for (int v = 0; v < 4; ++v) h[i][v] = fmaxf(h[i][v], 0.f);
+        for (int v = 0; v < 4; ++v) h[i][v] = relu_f(h[i][v]);
 #pragma unroll
       for (int v = 0; v < 4; ++v)
 #pragma unroll
@@ -231,7 +231,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_mfma_kernel(HeadArgs a) {
         f32x4 hr, dm;
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-          hr[v] = fmaxf(h[i][v], 0.f);
+          hr[v] = relu_f(h[i][v]);
           dm[v] = h[i][v] > 0.f ? dh[i][v] : 0.f;
         }
 #pragma unroll
@@ -321,7 +321,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_mfma_kernel(HeadArgs a) {
             const float lv = cur.par[DM + c];
             const float xv = cur.x[c];
             const float ev = __expf(lv);
-            const float var = fmaxf(ev, 1e-8f);
+            const float var = (ev < 1e-8f ? 1e-8f : ev)  /* clamp(min=1e-8), NaN stays NaN */;
             const float df = mu - xv;
             const float r2 = df * df / var;
             s_rec += 0.5f * (__logf(6.2831855f * var) + r2);

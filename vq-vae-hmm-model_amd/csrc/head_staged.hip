@@ -130,7 +130,7 @@ __global__ __launch_bounds__(256) void head_l2_kernel(StagedHeadArgs a) {
       if (!m) break;
       const float mu = a.par[r * LP + c], lv = a.par[r * LP + D + c], xv = a.x[r * LX + c];
       const float ev = __expf(lv);
-      const float var = fmaxf(ev, 1e-8f);
+      const float var = (ev < 1e-8f ? 1e-8f : ev)  /* clamp(min=1e-8), NaN stays NaN */;
       const float df = mu - xv;
       const float r2 = df * df / var;
       s_rec += 0.5f * (__logf(6.2831855f * var) + r2);

@@ -184,7 +184,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_wave_kernel(HeadArgs a) {
 #pragma unroll
       for (int i = 0; i < NBW; ++i)
 #pragma unroll
-        for (int v = 0; v < 4; ++v) hc[cb][i][v] = fmaxf(hc[cb][i][v], 0.f);
+        for (int v = 0; v < 4; ++v) hc[cb][i][v] = relu_f(hc[cb][i][v]);
 #pragma unroll
       for (int v = 0; v < 4; ++v)
 #pragma unroll
@@ -251,7 +251,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_wave_kernel(HeadArgs a) {
         f32x4 hr, dm;
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-          hr[v] = fmaxf(h[cb][i][v], 0.f);
+          hr[v] = relu_f(h[cb][i][v]);
           dm[v] = h[cb][i][v] > 0.f ? dh[cb][i][v] : 0.f;
         }
 #pragma unroll
@@ -343,7 +343,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_wave_kernel(HeadArgs a) {
         const float lv = cur.par[DM + c];
         const float xv = cur.x[c];
         const float ev = __expf(lv);
-        const float var = fmaxf(ev, 1e-8f);
+        const float var = (ev < 1e-8f ? 1e-8f : ev)  /* clamp(min=1e-8), NaN stays NaN */;
         const float df = mu - xv;
         const float r2 = df * df / var;
         s_rec += 0.5f * (__logf(6.2831855f * var) + r2);

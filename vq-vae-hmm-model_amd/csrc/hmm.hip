@@ -1178,17 +1178,42 @@ static int fb_lin_tier() {  // VQHMM_FB_LIN=0: log tier only (A/B switch)
 }
 
 // the resident kernel when its LDS fits (VQHMM_FB_RES=0: always the streaming kernel)
+// CU count and LDS bytes per workgroup of the current device, queried once per device
+// (the kernel choice below sizes one round of resident workgroups from them).
+struct DevShape {
+  int cus = 0;
+  size_t lds = 0;
+};
+static DevShape dev_shape() {
+  static DevShape cache[16];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) dev = 0;
+  DevShape& d = cache[dev];
+  if (d.cus == 0) {
+    int cus = 0, lds = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    if (hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess || lds <= 0)
+      lds = 64 * 1024;
+    d.lds = (size_t)lds;
+    d.cus = cus;
+  }
+  return d;
+}
+
 static bool fwdbwd_resident_ok(int64_t B, int64_t K, int64_t T) {
-  const char* env = getenv("VQHMM_FB_RES");  // read per call: the tests switch kernels between calls
+  // VQHMM_FB_RES=0 forces the streaming kernel: a test switch, read per call because the tests
+  // run both kernels in one process
+  const char* env = getenv("VQHMM_FB_RES");
   if ((env && env[0] == '0') || K < 1 || K > 8 || T > 4096) return false;
   const int kp = K <= 2 ? 2 : K <= 4 ? 4 : 8;
   const size_t bytes = kp == 2 ? FbRes<2>::lds_bytes((int)T) : kp == 4 ? FbRes<4>::lds_bytes((int)T)
                                                                      : FbRes<8>::lds_bytes((int)T);
-  if (bytes > 160 * 1024) return false;
+  const DevShape dv = dev_shape();
+  if (bytes > dv.lds) return false;
   // one round of workgroups only: a second round doubles the chain time, and the streaming
   // kernel (two reads of the table, twice the workgroups per CU) is then faster
-  const int64_t spw = 64 / (kp * kp), per_cu = (160 * 1024) / (int64_t)bytes;
-  return cdiv(B, spw) <= 256 * per_cu;
+  const int64_t spw = 64 / (kp * kp), per_cu = (int64_t)(dv.lds / bytes);
+  return cdiv(B, spw) <= (int64_t)dv.cus * per_cu;
 }
 
 template <int K>
