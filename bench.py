@@ -139,10 +139,32 @@ def vq_cfg3(lib):
     us = e0.elapsed_time(e1) / 20 * 1e3
     byts = 4.0 * B * T * Dv + 4.0 * K * Dv + 4.0 * B * T
     gbps = byts / (us * 1e-6) / 1e9
-    del z
-    return {"kernel": "vq_rows_kernel (vqhmm_vq_argmin_f32)", "bound": "hbm", "avg_us": round(us, 2), "achieved": round(gbps, 1),
-            "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(gbps / HBM_PEAK_GBPS, 4),
-            "traffic": traffic_for("vq_argmin", "vq_cfg3"), "shape": "B2048 Dv64 T200 K32"}
+    out = {"kernel": "vq_rows_kernel (vqhmm_vq_argmin_f32)", "bound": "hbm", "avg_us": round(us, 2),
+           "achieved": round(gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(gbps / HBM_PEAK_GBPS, 4),
+           "traffic": traffic_for("vq_argmin", "vq_cfg3"), "shape": "B2048 Dv64 T200 K32"}
+    # the fused quantize (pseudocode.txt:12-18): argmin + z_q gather + straight-through value written +
+    # squared-error partials, then the fixed-order partial sum: z read once, z_q_st and idx written
+    zq = torch.empty_like(z)
+    sse = torch.zeros((), dtype=torch.float64, device="cuda")
+    nb = lib.vqhmm_vq_quantize_workspace_size(B, Dv, T, K)
+    ws = torch.empty(max(nb, 8), dtype=torch.uint8, device="cuda")
+    runq = lambda: lib.vqhmm_vq_quantize_f32(_ext.ptr(z), B, Dv, T, _ext.ptr(cb), K, _ext.ptr(idx), _ext.ptr(zq),  # noqa: E731
+                                             _ext.ptr(sse), _ext.ptr(ws), ws.numel(), sp)
+    for _ in range(5):
+        runq()
+    e0.record(s)
+    for _ in range(20):
+        runq()
+    e1.record(s)
+    torch.cuda.synchronize()
+    usq = e0.elapsed_time(e1) / 20 * 1e3
+    byq = 8.0 * B * T * Dv + 4.0 * K * Dv + 4.0 * B * T
+    gq = byq / (usq * 1e-6) / 1e9
+    out["quantize"] = {"kernel": "vq_rows_kernel<.., QUANT> + vq_sse_finalize_kernel (vqhmm_vq_quantize_f32)",
+                       "bound": "hbm", "avg_us": round(usq, 2), "achieved": round(gq, 1), "peak": HBM_PEAK_GBPS,
+                       "unit": "GB/s", "frac": round(gq / HBM_PEAK_GBPS, 4)}
+    del z, zq
+    return out
 
 
 def hmm_kernels(lib):

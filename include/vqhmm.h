@@ -78,6 +78,21 @@ int vqhmm_vq_argmin_f32(const float* z, int64_t B, int64_t Dv, int64_t T,
                         int32_t* idx, float* dmin, void* stream);
 
 
+/* VQ-VAE quantizer (pseudocode.txt:12-18: `z_q, idx = quantize(z_e, codebook)`, the
+ * straight-through z_e + (z_q - z_e).detach() of :13 and the commit / codebook MSEs of :17-18)
+ * on channels-first z (B, Dv, T): idx as vqhmm_vq_argmin_f32 (same bit-exact contract),
+ * z_q_st[b][d][t] = z + (c[idx][d] - z) in fp32 (the forward value of the straight-through
+ * tensor), and *sse = sum over (b, d, t) of (z - c[idx][d])^2 in the direct-difference form,
+ * accumulated in fp64 (commit = beta * sse / (B Dv T), codebook loss = sse / (B Dv T)).  Fused in
+ * the argmin kernel's epilogue where its row-load path runs (Dv in {4,8,16,32,64}, T % 4 == 0,
+ * K <= 32), else argmin + one gather launch; then one fixed-order partial-sum launch (the result
+ * is deterministic).  Replaces the reference's `quantize` + two MSEs.
+ * Workspace: vqhmm_vq_quantize_workspace_size(B, Dv, T, K) bytes. */
+size_t vqhmm_vq_quantize_workspace_size(int64_t B, int64_t Dv, int64_t T, int64_t K);
+int vqhmm_vq_quantize_f32(const float* z, int64_t B, int64_t Dv, int64_t T, const float* codebook, int64_t K,
+                          int32_t* idx, float* z_q_st, double* sse, void* workspace, size_t ws_bytes,
+                          void* stream);
+
 /* ------------------------------------------------------------ Viterbi ----
  * MAP state path (semantics math.md:23-67 over Prior.forward's
  * tables VQ_VAE_HMM_fixed.py:59-71 — no reference code).  log_pi (K),

@@ -234,6 +234,17 @@ int vqhmm_vq_argmin_f32(const float* z, int64_t B, int64_t Dv, int64_t T, const 
   return launch_vq_argmin(z, B, Dv, T, codebook, K, idx, dmin, (hipStream_t)stream);
 }
 
+size_t vqhmm_vq_quantize_workspace_size(int64_t B, int64_t Dv, int64_t T, int64_t K) {
+  return (B < 0 || T < 0 || Dv < 1 || K < 1) ? 0 : vq_quantize_ws_bytes(B, Dv, T, K);
+}
+
+int vqhmm_vq_quantize_f32(const float* z, int64_t B, int64_t Dv, int64_t T, const float* codebook, int64_t K,
+                          int32_t* idx, float* z_q_st, double* sse, void* ws, size_t ws_bytes, void* stream) {
+  if (B < 0 || T < 0 || Dv < 1 || K < 1 || !sse || !ws || (B * T > 0 && (!z || !codebook || !idx || !z_q_st)))
+    return VQHMM_EINVAL;
+  return launch_vq_quantize(z, B, Dv, T, codebook, K, idx, z_q_st, sse, ws, ws_bytes, (hipStream_t)stream);
+}
+
 size_t vqhmm_viterbi_workspace_size(int64_t B, int64_t T, int64_t K) {
   return (B < 0 || T < 0 || K < 1) ? 0 : viterbi_ws_bytes(B, T, K);
 }

@@ -185,6 +185,10 @@ struct SlabSeg {
 
 int launch_vq_argmin(const float* z, int64_t B, int64_t Dv, int64_t T, const float* cb, int64_t K, int32_t* idx,
                      float* dmin, hipStream_t s);
+// quantize (pseudocode.txt:12-18): argmin + z_q gather + straight-through value + sum (z - z_q)^2
+size_t vq_quantize_ws_bytes(int64_t B, int64_t Dv, int64_t T, int64_t K);
+int launch_vq_quantize(const float* z, int64_t B, int64_t Dv, int64_t T, const float* cb, int64_t K, int32_t* idx,
+                       float* zq_st, double* sse, void* ws, size_t ws_bytes, hipStream_t s);
 int launch_conv(const ConvArgs& a, hipStream_t s);
 bool conv2_supported(const ConvArgs& a);
 // front conv + this conv in one launch (conv2.hip conv2f_kernel; ConvArgs::f_*)

@@ -130,11 +130,16 @@ __global__ __launch_bounds__(256) void vq_mfma_kernel(const float* __restrict__ 
 // read the registers and the wave drains its loads at the top of every tile).
 // ||z||^2 (only for dmin) is formed after the MFMAs, so it never pulls a wait
 // forward.
-template <int DG, int CB, bool DMIN, int NBUF>  // Dv == 4 DG, K <= 16 CB; DMIN: dmin requested; NBUF register sets
+// QUANT (quantize, pseudocode.txt:12-18): the epilogue also gathers z_q = c[idx] from an LDS copy of
+// the codebook, writes the straight-through value z + (z_q - z) channels-first (float4 stores at the
+// z load addresses) and accumulates sum (z - z_q)^2 in the direct-difference form, in fp64, per lane;
+// every wave writes one partial (part[global wave]), summed in a fixed order by vq_sse_finalize.
+template <int DG, int CB, bool DMIN, int NBUF, bool QUANT = false>  // Dv == 4 DG, K <= 16 CB; DMIN: dmin requested; NBUF register sets
 __global__ __launch_bounds__(256, NBUF == 2 ? 2 : 1) void vq_rows_kernel(const float* __restrict__ z, int64_t B, int Dv, int T,
                                                          const float* __restrict__ cb, int K,
                                                          int32_t* __restrict__ idx, float* __restrict__ dmin,
-                                                         int64_t tiles, int64_t nwaves) {
+                                                         int64_t tiles, int64_t nwaves, float* __restrict__ zq_st = nullptr,
+                                                         double* __restrict__ part = nullptr) {
   constexpr int LDSC = 16 * CB + 4;  // score rows [position][code]
   struct Prologue {
     float cbS[16 * CB][4 * DG + 1];  // codebook, +1 pad: conflict-free per-code rows
@@ -149,6 +154,8 @@ __global__ __launch_bounds__(256, NBUF == 2 ? 2 : 1) void vq_rows_kernel(const f
   } u;
   __shared__ float aS[CB][DG][64];
   __shared__ float cnS[16 * CB];
+  __shared__ float cbQ[QUANT ? 16 * CB : 1][QUANT ? 4 * DG : 1];  // QUANT: the codebook, [code][dim]
+  __shared__ int argS[QUANT ? 4 : 1][QUANT ? 64 : 1];               // QUANT: the wave's argmins per position
   auto& cbS = u.pro.cbS;
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, j = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -197,6 +204,8 @@ __global__ __launch_bounds__(256, NBUF == 2 ? 2 : 1) void vq_rows_kernel(const f
     const int c = i / (DG * 64), dg = (i / 64) % DG, l = i & 63;
     aS[c][dg][l] = -2.0f * cbS[16 * c + (l & 15)][4 * dg + (l >> 4)];
   }
+  if constexpr (QUANT)
+    for (int i = tid; i < 16 * CB * 4 * DG; i += 256) cbQ[i / (4 * DG)][i % (4 * DG)] = cbS[i / (4 * DG)][i % (4 * DG)];
   if (tid < 16 * CB) {
     float cn = 0.0f;
 #pragma unroll
@@ -210,6 +219,7 @@ __global__ __launch_bounds__(256, NBUF == 2 ? 2 : 1) void vq_rows_kernel(const f
   for (int c = 0; c < CB; ++c)
 #pragma unroll
     for (int v = 0; v < 4; ++v) init[c][v] = cnS[16 * c + 4 * g + v];
+  double sse = 0.0;  // QUANT: sum (z - z_q)^2 of this lane's (position, dim) entries
 
   // one tile on zc while the loads of tile + NBUF - 1 land in zn
   auto run_tile = [&](int64_t tile, const f32x4* zc, f32x4* zn) {
@@ -268,6 +278,30 @@ __global__ __launch_bounds__(256, NBUF == 2 ? 2 : 1) void vq_rows_kernel(const f
         dmin[n] = best + ((qq[0] + qq[1]) + (qq[2] + qq[3]));
       }
     }
+    if constexpr (QUANT) {
+      // lane (g, j) holds z[d = 4 dg + g][positions 4j .. 4j+3]: their codes from the wave's argmins
+      argS[wave][lane] = arg;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+      int code[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) code[m] = argS[wave][4 * j + m];
+      const bool live = tile < t1 && tile * 64 + 4 * j < N;  // T % 4 == 0: a quad is all in or all out
+      const uint32_t o = tile_off(tile);
+#pragma unroll
+      for (int dg = 0; dg < DG; ++dg) {
+        f32x4 st;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const float zv = zc[dg][m], qv = cbQ[code[m]][4 * dg + g];
+          st[m] = zv + (qv - zv);  // z_e + (z_q - z_e).detach(), :13 (built without contraction)
+          const double dd = (double)zv - (double)qv;
+          if (live) sse = __builtin_fma(dd, dd, sse);
+        }
+        if (live) *reinterpret_cast<f32x4*>(reinterpret_cast<char*>(zq_st) + o + (uint32_t)dg * (uint32_t)gstep) = st;
+      }
+    }
     __builtin_amdgcn_wave_barrier();  // the next tile's writes must not pass this tile's reads
   };
   int64_t tile = t0;
@@ -285,6 +319,10 @@ __global__ __launch_bounds__(256, NBUF == 2 ? 2 : 1) void vq_rows_kernel(const f
     }
     if (tile < t1) run_tile(tile, za, zc3);
     if (tile + 1 < t1) run_tile(tile + 1, zb, za);
+  }
+  if constexpr (QUANT) {
+    sse = wave_sum_dpp(sse);
+    if (lane == 0 && gw < nwaves) part[gw] = sse;
   }
 }
 
@@ -362,6 +400,54 @@ __global__ __launch_bounds__(256) void vq_argmin_kernel(const float* __restrict_
   if (vb) { idx[nb] = arg_b; if (dmin) dmin[nb] = best_b + ((qb[0] + qb[1]) + (qb[2] + qb[3])); }
 }
 
+// ------------------------------------------------- quantize epilogue for the other argmin kernels
+// One thread per position (consecutive t: coalesced CF reads / writes): z_q = c[idx], the
+// straight-through value z + (z_q - z), and sum (z - z_q)^2 (fp64, direct difference); the block's
+// sum goes to part[blockIdx.x] (fixed-order tree).
+__global__ __launch_bounds__(256) void vq_quantize_gather_kernel(const float* __restrict__ z, int64_t B, int Dv, int T,
+                                                                 const float* __restrict__ cb,
+                                                                 const int32_t* __restrict__ idx,
+                                                                 float* __restrict__ zq_st, double* __restrict__ part) {
+  __shared__ double red[256];
+  const int64_t N = B * (int64_t)T;
+  const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  double sse = 0.0;
+  if (n < N) {
+    const int64_t b = n / T, t = n - b * T;
+    const int k = idx[n];
+    const float* zr = z + b * (int64_t)Dv * T + t;
+    float* zo = zq_st + b * (int64_t)Dv * T + t;
+    for (int d = 0; d < Dv; ++d) {
+      const float zv = zr[(int64_t)d * T], qv = cb[(int64_t)k * Dv + d];
+      zo[(int64_t)d * T] = zv + (qv - zv);
+      const double dd = (double)zv - (double)qv;
+      sse = __builtin_fma(dd, dd, sse);
+    }
+  }
+  red[threadIdx.x] = sse;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if ((int)threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+// *sse = sum of part[0, np) in a fixed order (one workgroup)
+__global__ __launch_bounds__(256) void vq_sse_finalize_kernel(const double* __restrict__ part, int64_t np,
+                                                              double* __restrict__ sse) {
+  __shared__ double red[256];
+  double v = 0.0;
+  for (int64_t i = threadIdx.x; i < np; i += 256) v += part[i];
+  red[threadIdx.x] = v;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if ((int)threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *sse = red[0];
+}
+
 static int env_int(const char* name, int dflt, int lo, int hi) {
   const char* e = getenv(name);
   const int v = e ? atoi(e) : dflt;
@@ -380,13 +466,22 @@ static void launch_mfma(const float* z, int64_t B, int Dv, int T, const float* c
   vq_mfma_kernel<S><<<(unsigned)cdiv(persistent_waves(tiles), 4), 256, 0, s>>>(z, B, Dv, T, cb, K, idx, dmin, tiles);
 }
 
+static int64_t rows_waves(int64_t N) {  // one wave per SIMD measured best (cfg3)
+  return cdiv(persistent_waves(cdiv(N, 64), 4), 4) * 4;
+}
+
 template <int DG, int CB>
 static void launch_rows(const float* z, int64_t B, int Dv, int T, const float* cb, int K, int32_t* idx, float* dmin,
-                        hipStream_t s) {
+                        hipStream_t s, float* zq_st = nullptr, double* part = nullptr) {
   static const int nbuf = env_int("VQHMM_VQ_NBUF", 2, 2, 3);  // tuning knob: register sets in flight
   const int64_t tiles = cdiv(B * (int64_t)T, 64);
-  const int64_t waves = cdiv(persistent_waves(tiles, 4), 4) * 4;  // one wave per SIMD measured best (cfg3)
+  const int64_t waves = rows_waves(B * (int64_t)T);
   const unsigned grid = (unsigned)(waves / 4);
+  if (zq_st) {
+    vq_rows_kernel<DG, CB, false, 2, true><<<grid, 256, 0, s>>>(z, B, Dv, T, cb, K, idx, nullptr, tiles, waves, zq_st,
+                                                                part);
+    return;
+  }
   if (nbuf == 3) {
     if (dmin) vq_rows_kernel<DG, CB, true, 3><<<grid, 256, 0, s>>>(z, B, Dv, T, cb, K, idx, dmin, tiles, waves);
     else vq_rows_kernel<DG, CB, false, 3><<<grid, 256, 0, s>>>(z, B, Dv, T, cb, K, idx, dmin, tiles, waves);
@@ -399,15 +494,53 @@ static void launch_rows(const float* z, int64_t B, int Dv, int T, const float* c
 // Dv % 4 == 0 only (whole dim groups)
 template <int CB>
 static bool dispatch_rows(const float* z, int64_t B, int Dv, int T, const float* cb, int K, int32_t* idx,
-                          float* dmin, hipStream_t s) {
+                          float* dmin, hipStream_t s, float* zq_st = nullptr, double* part = nullptr) {
   switch (Dv) {
-    case 4: launch_rows<1, CB>(z, B, Dv, T, cb, K, idx, dmin, s); return true;
-    case 8: launch_rows<2, CB>(z, B, Dv, T, cb, K, idx, dmin, s); return true;
-    case 16: launch_rows<4, CB>(z, B, Dv, T, cb, K, idx, dmin, s); return true;
-    case 32: launch_rows<8, CB>(z, B, Dv, T, cb, K, idx, dmin, s); return true;
-    case 64: launch_rows<16, CB>(z, B, Dv, T, cb, K, idx, dmin, s); return true;
+    case 4: launch_rows<1, CB>(z, B, Dv, T, cb, K, idx, dmin, s, zq_st, part); return true;
+    case 8: launch_rows<2, CB>(z, B, Dv, T, cb, K, idx, dmin, s, zq_st, part); return true;
+    case 16: launch_rows<4, CB>(z, B, Dv, T, cb, K, idx, dmin, s, zq_st, part); return true;
+    case 32: launch_rows<8, CB>(z, B, Dv, T, cb, K, idx, dmin, s, zq_st, part); return true;
+    case 64: launch_rows<16, CB>(z, B, Dv, T, cb, K, idx, dmin, s, zq_st, part); return true;
     default: return false;
   }
+}
+
+static bool rows_path(const float* z, int64_t B, int64_t Dv, int64_t T, int64_t K) {
+  static const int impl = env_int("VQHMM_VQ_IMPL", 0, 0, 2);  // 0 auto, 1 tile-32, 2 rows
+  const int64_t N = B * T;
+  const bool rows_ok = T % 4 == 0 && (reinterpret_cast<uintptr_t>(z) & 15) == 0 && N * Dv < (int64_t(1) << 30);
+  return K <= 32 && rows_ok && impl != 1 && (Dv == 4 || Dv == 8 || Dv == 16 || Dv == 32 || Dv == 64);
+}
+
+size_t vq_quantize_ws_bytes(int64_t B, int64_t Dv, int64_t T, int64_t K) {
+  (void)Dv; (void)K;
+  const int64_t N = B * T;
+  const int64_t np = std::max<int64_t>(rows_waves(N), cdiv(N, 256));
+  return (size_t)std::max<int64_t>(np, 1) * sizeof(double);
+}
+
+int launch_vq_quantize(const float* z, int64_t B, int64_t Dv, int64_t T, const float* cb, int64_t K, int32_t* idx,
+                       float* zq_st, double* sse, void* ws, size_t ws_bytes, hipStream_t s) {
+  const int64_t N = B * T;
+  if (K <= 0 || Dv <= 0 || Dv > 2048 || T <= 0 || T > INT32_MAX) return VQHMM_EINVAL;
+  if (ws_bytes < vq_quantize_ws_bytes(B, Dv, T, K)) return VQHMM_EWORKSPACE;
+  double* part = reinterpret_cast<double*>(ws);
+  int64_t np;
+  if (N > 0 && rows_path(z, B, Dv, T, K)) {
+    const bool done = K <= 16 ? dispatch_rows<1>(z, B, (int)Dv, (int)T, cb, (int)K, idx, nullptr, s, zq_st, part)
+                              : dispatch_rows<2>(z, B, (int)Dv, (int)T, cb, (int)K, idx, nullptr, s, zq_st, part);
+    if (!done) return VQHMM_EUNSUPPORTED;
+    np = rows_waves(N);
+  } else {
+    if (int rc = launch_vq_argmin(z, B, Dv, T, cb, K, idx, nullptr, s)) return rc;
+    np = cdiv(N, 256);
+    if (np > 0)
+      vq_quantize_gather_kernel<<<(unsigned)np, 256, 0, s>>>(z, B, (int)Dv, (int)T, cb, idx, zq_st, part);
+  }
+  VQHMM_LAUNCH_CHECK();
+  vq_sse_finalize_kernel<<<1, 256, 0, s>>>(part, np, sse);
+  VQHMM_LAUNCH_CHECK();
+  return VQHMM_OK;
 }
 
 int launch_vq_argmin(const float* z, int64_t B, int64_t Dv, int64_t T, const float* cb, int64_t K,

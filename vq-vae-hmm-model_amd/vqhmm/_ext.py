@@ -39,6 +39,9 @@ _SIGS = {
     "vqhmm_abi_version": (c_i32, []),
     "vqhmm_param_layout": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(c_i64)]),
     "vqhmm_vq_argmin_f32": (ctypes.c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "vqhmm_vq_quantize_workspace_size": (c_sz, [c_i64, c_i64, c_i64, c_i64]),
+    "vqhmm_vq_quantize_f32": (ctypes.c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_sz,
+                                             c_vp]),
     "vqhmm_viterbi_workspace_size": (c_sz, [c_i64, c_i64, c_i64]),
     "vqhmm_viterbi_f32": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "vqhmm_fwdbwd_workspace_size": (c_sz, [c_i64, c_i64, c_i64]),

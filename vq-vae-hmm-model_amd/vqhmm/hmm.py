@@ -46,21 +46,65 @@ def regime_argmax(q):
     return idx.long()
 
 
+class _Quantize(torch.autograd.Function):
+    """Forward: ONE fused kernel pass (vqhmm_vq_quantize_f32: argmin, z_q gather, straight-through
+    value, sum (z - z_q)^2 in fp64) + a fixed-order partial sum.  Backward (autograd of
+    pseudocode.txt:13,17-18): the straight-through output passes its gradient to z unchanged;
+    commit = beta * sse / n adds beta * 2 (z - z_q) / n to dz; the codebook loss sse / n gives
+    dcodebook[k] = sum over positions with idx = k of 2 (z_q - z) / n."""
+
+    @staticmethod
+    def forward(ctx, z, codebook, beta):
+        B, Dv, T = z.shape
+        K = codebook.shape[0]
+        idx = torch.empty((B, T), dtype=torch.int32, device=z.device)
+        zq_st = torch.empty_like(z)
+        sse = torch.zeros((), dtype=torch.float64, device=z.device)
+        lib = _ext.load()
+        nb = lib.vqhmm_vq_quantize_workspace_size(B, Dv, T, K)
+        ws = torch.empty(max(nb, 8), dtype=torch.uint8, device=z.device)
+        _ext.check(lib.vqhmm_vq_quantize_f32(_ext.ptr(z), B, Dv, T, _ext.ptr(codebook), K, _ext.ptr(idx),
+                                             _ext.ptr(zq_st), _ext.ptr(sse), _ext.ptr(ws), ws.numel(),
+                                             _ext.stream_ptr(z.device)), "quantize")
+        n = float(max(z.numel(), 1))
+        mse = (sse / n).float()
+        ctx.save_for_backward(z, codebook, idx)
+        ctx.beta, ctx.n = float(beta), n
+        ctx.mark_non_differentiable(idx)
+        return zq_st, idx, beta * mse, mse
+
+    @staticmethod
+    def backward(ctx, g_zq, g_idx, g_commit, g_cb):
+        z, codebook, idx = ctx.saved_tensors
+        dz = dcb = None
+        zq = codebook[idx.long()].permute(0, 2, 1)  # (B, Dv, T)
+        diff = z - zq
+        if ctx.needs_input_grad[0]:
+            dz = g_zq if g_zq is not None else torch.zeros_like(z)
+            if g_commit is not None:
+                dz = dz + g_commit * (ctx.beta * 2.0 / ctx.n) * diff
+        if ctx.needs_input_grad[1] and g_cb is not None:
+            w = (g_cb * (-2.0 / ctx.n)) * diff  # d cb_loss / d z_q
+            dcb = torch.zeros_like(codebook).index_add_(0, idx.long().reshape(-1),
+                                                        w.permute(0, 2, 1).reshape(-1, codebook.shape[1]))
+        return dz, dcb, None
+
+
 def quantize(z, codebook, beta=0.25):
     """VQ-VAE quantizer of pseudocode.txt:11-18 on channels-first z (B, Dv, T).
 
     Returns (z_q_st, idx, commit_loss, codebook_loss):
-      z_q = codebook[idx] (B, Dv, T); z_q_st = z + (z_q - z).detach() (straight-through, :12);
-      commit = beta * MSE(z, sg(z_q)) (:16); codebook = MSE(z_q, sg(z)) (:17).
-    The argmin is the HIP kernel; the gather/MSE are small elementwise ops on
-    its output.
+      idx = argmin_k ||z - c_k||^2 (the vq_argmin contract); z_q = codebook[idx];
+      z_q_st = z + (z_q - z).detach() (straight-through, :13); commit = beta * MSE(z, sg(z_q)) (:17);
+      codebook = MSE(z_q, sg(z)) (:18).
+    The forward is one HIP pass (argmin + gather + straight-through value + the squared-error
+    partial sums in the kernel's epilogue); the gradients follow the reference's autograd.
     """
-    idx = vq_argmin(z.detach(), codebook.detach())
-    z_q = codebook[idx.long()].permute(0, 2, 1)
-    z_q_st = z + (z_q - z).detach()
-    commit = beta * torch.mean((z - z_q.detach()) ** 2)
-    cb_loss = torch.mean((z_q - z.detach()) ** 2)
-    return z_q_st, idx, commit, cb_loss
+    _ext.require_device(z, codebook)
+    if z.dim() != 3 or codebook.dim() != 2 or z.shape[1] != codebook.shape[1]:
+        raise ValueError(f"quantize: expected z (B,Dv,T) and codebook (K,Dv), got {tuple(z.shape)} "
+                         f"{tuple(codebook.shape)}")
+    return _Quantize.apply(z.contiguous().float(), codebook.contiguous().float(), float(beta))
 
 
 def _hmm_inputs(log_pi, log_A, em, lengths):
