@@ -99,8 +99,9 @@ int vqhmm_vq_quantize_f32(const float* z, int64_t B, int64_t Dv, int64_t T, cons
  * log_A (B,T,K,K) [t = transition t-1 -> t], em (B,T,K) emission log-potentials,
  * lengths (B) int64 -> path (B,T) int32 (-1 at t >= length), score (B) fp32.
  * d_t[j] = (max_i d_{t-1}[i] + log_A[t,i,j]) + em[t,j] in fp32, ties -> lowest i;
- * last state = first argmax.  Bit-exact vs oracle/c/hmm_oracle.c.  K <= 32 (K <= 8: packed lane
- * groups, hmm.hip; 8 < K <= 32: one sequence per wave, hmm_wide.hip); larger K -> VQHMM_EUNSUPPORTED.
+ * last state = first argmax.  Bit-exact vs oracle/c/hmm_oracle.c.  K <= 256 (K <= 8: packed lane
+ * groups, hmm.hip; 8 < K <= 32: one sequence per wave, hmm_wide.hip; 32 < K <= 256: one workgroup
+ * per sequence, thread = state, hmm_generic.hip); larger K -> VQHMM_EUNSUPPORTED.
  * Workspace: vqhmm_viterbi_workspace_size(B, T, K) bytes (backpointers as one
  * 64-bit lane ballot per step per wave of 64 / KP^2 sequences, KP = K rounded
  * up to a power of two; T rounded up to 64). */
@@ -115,7 +116,7 @@ int vqhmm_viterbi_f32(const float* log_pi, const float* log_A, const float* em, 
  * Base-2 log-space alpha/beta with per-step shifts; a chunk whose fast step
  * leaves float range is recomputed with the max-shifted log-sum-exp.
  * Workspace: vqhmm_fwdbwd_workspace_size(B, T, K) = 2 * B * T * K * 4 bytes.
- * Accuracy target vs the fp64 oracle: |gamma| abs 1e-5, logZ rel 1e-5.  K <= 32 (as Viterbi). */
+ * Accuracy target vs the fp64 oracle: |gamma| abs 1e-5, logZ rel 1e-5.  K <= 256 (as Viterbi). */
 size_t vqhmm_fwdbwd_workspace_size(int64_t B, int64_t T, int64_t K);
 int vqhmm_fwdbwd_f32(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths,
                      int64_t B, int64_t T, int64_t K, float* gamma, float* logZ, void* workspace,

@@ -256,9 +256,50 @@ def test_viterbi_wide_ties():
     assert np.array_equal(score.cpu().numpy(), rs)
 
 
-def test_hmm_k_over_32_rejected():
+@pytest.mark.parametrize("K,B,T", [(33, 4, 60), (48, 3, 41), (64, 5, 130), (100, 2, 33), (256, 2, 20)])
+def test_hmm_generic_k_over_32(K, B, T):
+    """32 < K <= 256 (hmm_generic.hip: one workgroup per sequence, thread = state): Viterbi path and
+    score bit-exact vs the C oracle, gamma / logZ vs the fp64 oracle, ragged lengths incl. 0 and 1."""
     import vqhmm
-    K, B, T = 33, 1, 4
+    log_pi, log_A, em = random_hmm(K + B + T, B, T, K)
+    L = np.random.default_rng(K).integers(1, T + 1, B).astype(np.int64)
+    L[0] = T
+    if B > 2:
+        L[1] = 0
+    path, score = vqhmm.viterbi(*gpu(log_pi, log_A, em), torch.from_numpy(L))
+    rp, rs = c_oracle.viterbi(log_pi, log_A, em, L)
+    assert np.array_equal(path.cpu().numpy(), rp)
+    assert np.array_equal(score.cpu().numpy().view(np.uint32), rs.view(np.uint32))
+    gamma, logZ = vqhmm.forward_backward(*gpu(log_pi, log_A, em), torch.from_numpy(L))
+    rg, rz = hmm_ref.forward_backward_f64(log_pi, log_A, em, L)
+    check_gamma(gamma.cpu().numpy(), rg)
+    z = logZ.cpu().numpy()
+    live = L > 0
+    assert np.all(np.abs(z[live] - rz[live]) <= 1e-5 * np.maximum(1.0, np.abs(rz[live])))
+    assert np.all(np.isnan(z[~live]))
+
+
+def test_hmm_generic_left_to_right():
+    """K = 40 with left-to-right transitions (log 0 = -inf below the diagonal) and T = 300."""
+    import vqhmm
+    K, B, T = 40, 2, 300
+    log_pi, log_A, em = random_hmm(3, B, T, K)
+    tri = np.triu(np.ones((K, K), bool))
+    la = np.where(tri, log_A.astype(np.float64), -np.inf)
+    log_A = (la - np.logaddexp.reduce(la, axis=-1, keepdims=True)).astype(np.float32)
+    path, score = vqhmm.viterbi(*gpu(log_pi, log_A, em))
+    rp, rs = c_oracle.viterbi(log_pi, log_A, em, np.full(B, T))
+    assert np.array_equal(path.cpu().numpy(), rp)
+    gamma, logZ = vqhmm.forward_backward(*gpu(log_pi, log_A, em))
+    with np.errstate(divide="ignore", invalid="ignore"):
+        rg, rz = hmm_ref.forward_backward_f64(log_pi, log_A, em, np.full(B, T))
+    check_gamma(gamma.cpu().numpy(), rg)
+    assert np.all(np.abs(logZ.cpu().numpy() - rz) <= 1e-5 * np.abs(rz))
+
+
+def test_hmm_k_over_256_rejected():
+    import vqhmm
+    K, B, T = 257, 1, 4
     log_pi, log_A, em = random_hmm(1, B, T, K)
     with pytest.raises(RuntimeError, match="unsupported"):
         vqhmm.viterbi(*gpu(log_pi, log_A, em))

@@ -363,6 +363,13 @@ int launch_gather_chunks(const float* src, const int64_t* meta, int64_t B, int64
 int launch_log_softmax_vec(const float* x, int K, float* out, hipStream_t s);
 int launch_argmax_cf(const float* q, int64_t B, int64_t K, int64_t T, int32_t* idx, hipStream_t s);
 size_t viterbi_ws_bytes(int64_t B, int64_t T, int64_t K);
+// 32 < K <= 256: one workgroup per sequence, thread = state (hmm_generic.hip)
+size_t hmm_generic_viterbi_ws_bytes(int64_t B, int64_t T, int64_t K);
+size_t hmm_generic_fwdbwd_ws_bytes(int64_t B, int64_t T, int64_t K);
+int launch_viterbi_generic(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths,
+                           int64_t B, int64_t T, int64_t K, int32_t* path, float* score, void* ws, hipStream_t s);
+int launch_fwdbwd_generic(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths,
+                          int64_t B, int64_t T, int64_t K, float* gamma, float* logZ, void* ws, hipStream_t s);
 // K in (8, 32]: one sequence per wave (hmm_wide.hip)
 size_t viterbi_wide_ws_bytes(int64_t B, int64_t T);
 int launch_viterbi_wide(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths, int64_t B,
