@@ -425,8 +425,8 @@ int run_staged_head(const ElboPlan& p, const StepCtx& c, const float* const* w, 
 }
 
 // The softmax backward (logits_bwd) rides in the dec_conv1 dgrad epilogue when that
-// conv runs on conv2 and a row's K <= 4 channels sit in one lane.
-bool logits_bwd_fused(const ElboPlan& p) { return p.K <= 4 && conv2_supported(conv_of(p, nullptr, S_DEC1_DG)); }
+// conv runs on conv2 and a row's K <= 8 channels sit in one or two lanes (ACT 3 / 4).
+bool logits_bwd_fused(const ElboPlan& p) { return p.K <= 8 && conv2_supported(conv_of(p, nullptr, S_DEC1_DG)); }
 // ... and to_logits' dgrad too when the encoder conv2 width splits into float4s over the 4 lane groups.
 bool logits_dg_fused(const ElboPlan& p) { return logits_bwd_fused(p) && ld4(p.H2) % 16 == 0 && p.H2 <= 64; }
 
@@ -516,7 +516,7 @@ ConvArgs dec1_dg_args(const ElboPlan& p, const float* const* w, const float* gsc
   if (!w) w = kNull;
   ConvArgs a = conv_of(p, w, S_DEC1_DG);
   if (logits_bwd_fused(p)) {  // + logits_bwd in the epilogue
-    a.act = 3;
+    a.act = p.K <= 4 ? 3 : 4;
     a.lb_q = p.q; a.lb_dqx = p.dqx; a.lb_dlx = p.dlx; a.lb_scale = gscale; a.lb_dlog = p.dlog;
     if (logits_dg_fused(p)) {  // + to_logits_dgrad
       a.lb_W = w[LOGIT_W]; a.lb_h = p.h2e; a.lb_dh = p.dh2; a.lb_C = p.H2;

@@ -56,6 +56,12 @@ __device__ __forceinline__ float4 x_mask(const ConvArgs& a, int64_t m0, int s, i
 
 }  // namespace
 
+// The fused 1x1 tail: one 16-channel block with any outputs, or (C2 <= 32, e.g. to_params at D = 16)
+// two blocks without the softmax outputs (q / regimes need the row's channels in one block).
+static bool conv2_tail_ok(const ConvArgs& a) {
+  return a.tW == nullptr || a.C2 <= 16 || (a.C2 <= 32 && !a.q_out && !a.q_cf && !a.reg_out);
+}
+
 // The tile's MFMAs: acc[nb][pb] (16 n x 16 rows) += W_tap (n x c) @ X(rows + tap - 1, c)^T over the
 // KS * KCP 16-wide k-steps.  Operands of step s + 1 are read from LDS while the 16*PB MFMAs of step
 // s run (two register sets; sched_barrier keeps the reads ahead of the MFMAs), and the MFMAs are
@@ -156,12 +162,15 @@ __device__ __forceinline__ void c2_mfma_pk(const float* Ws, const float* Xw, int
 // backward of the row, see ConvArgs::lb_*).
 // Rows of a 16-row block outside [rlo, rhi) get their values (acc) but no stores: the fused
 // front conv's halo rows and the rows past a 14-row fused tile belong to the neighbouring tiles.
-template <int NB, int PB, int ACT>
+// TB = 2: a second 16-channel tail block (channels 16 .. C2-1, C2 <= 32: to_params at D <= 16) with
+// weights tw2 / bias tb1; no softmax outputs then.
+template <int NB, int PB, int ACT, int TB = 1>
 __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a, int64_t m0, int wave, int lg4, int l16,
                                                f32x4 (&acc)[NB][PB], const float4 (&auxv)[NB][PB],
                                                const float (&bias_r)[NB][4], const float (&tw)[NB][4],
                                                f32x4 tb0, float sc, bool tail, int rlo = 0, int rhi = 16,
-                                               float* xs_dh = nullptr, int xs_ld = 0) {
+                                               float* xs_dh = nullptr, int xs_ld = 0,
+                                               const float (*tw2)[4] = nullptr, f32x4 tb1 = f32x4{0.f, 0.f, 0.f, 0.f}) {
   // lane (lg4, l16) holds channels nb*16 + 4*lg4 + v of row m0 + (wave*PB+pb)*16 + l16
   const bool own = l16 >= rlo && l16 < rhi;
 #pragma unroll
@@ -187,31 +196,48 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a, int64_t m0, in
         }
         acc[nb][pb] = y;
         const int n0 = nb * 16 + 4 * lg4;
-        if constexpr (ACT == 3) {  // softmax backward of the row, then (optionally) to_logits' dgrad
+        if constexpr (ACT == 3 || ACT == 4) {  // softmax backward of the row, then (optionally) to_logits' dgrad
+          // ACT 3: K <= 4 channels (one lane group), ACT 4: K <= 8 (lane groups 0 and 1)
+          constexpr int KM = ACT == 4 ? 8 : 4;
           if (nb == 0) {
-            // channels 0..3 of row l16 sit in lane l16 (lg4 = 0): broadcast them to the row's 4 lanes
-            float yk[4];
+            // channels 0..3 of row l16 sit in lane l16 (lg4 = 0), 4..7 in lane 16 + l16 (lg4 = 1):
+            // broadcast them to the row's lanes
+            float yk[KM];
 #pragma unroll
             for (int k = 0; k < 4; ++k) yk[k] = __shfl(y[k], l16);
+            if constexpr (KM == 8) {
+#pragma unroll
+              for (int k = 0; k < 4; ++k) yk[4 + k] = __shfl(y[k], 16 + l16);
+            }
             // rows inside [0, R) are computed (a fused next conv's halo rows need them, xs_dh),
             // only owned rows are stored
             if (r >= 0 && r < a.R) {
               const float lsc = a.lb_scale ? *a.lb_scale : 1.f;
-              const float4 q4 = *reinterpret_cast<const float4*>(a.lb_q + r * 4);
-              const float4 x4 = *reinterpret_cast<const float4*>(a.lb_dqx + r * 4);
-              const float4 l4 = *reinterpret_cast<const float4*>(a.lb_dlx + r * 4);
-              const float qk[4] = {q4.x, q4.y, q4.z, q4.w}, xk[4] = {x4.x, x4.y, x4.z, x4.w};
-              const float lk[4] = {l4.x, l4.y, l4.z, l4.w};
-              float dq[4], sdot = 0.f;
+              float qk[KM], xk[KM], lk[KM];
 #pragma unroll
-              for (int k = 0; k < 4; ++k) {
+              for (int h = 0; h < KM / 4; ++h) {
+                const float4 q4 = *reinterpret_cast<const float4*>(a.lb_q + r * KM + 4 * h);
+                const float4 x4 = *reinterpret_cast<const float4*>(a.lb_dqx + r * KM + 4 * h);
+                const float4 l4 = *reinterpret_cast<const float4*>(a.lb_dlx + r * KM + 4 * h);
+                qk[4 * h] = q4.x; qk[4 * h + 1] = q4.y; qk[4 * h + 2] = q4.z; qk[4 * h + 3] = q4.w;
+                xk[4 * h] = x4.x; xk[4 * h + 1] = x4.y; xk[4 * h + 2] = x4.z; xk[4 * h + 3] = x4.w;
+                lk[4 * h] = l4.x; lk[4 * h + 1] = l4.y; lk[4 * h + 2] = l4.z; lk[4 * h + 3] = l4.w;
+              }
+              float dq[KM], sdot = 0.f;
+#pragma unroll
+              for (int k = 0; k < KM; ++k) {
                 dq[k] = yk[k] + lsc * xk[k];
                 sdot = fmaf(qk[k], dq[k], sdot);
               }
-              f32x4 dl;
+              float dl[KM];
 #pragma unroll
-              for (int k = 0; k < 4; ++k) dl[k] = qk[k] * (dq[k] - sdot) + lsc * lk[k];
-              if (lg4 == 0 && st_r) *reinterpret_cast<f32x4*>(a.lb_dlog + r * 4) = dl;
+              for (int k = 0; k < KM; ++k) dl[k] = qk[k] * (dq[k] - sdot) + lsc * lk[k];
+              if (lg4 < KM / 4 && st_r) {
+                f32x4 o4;
+#pragma unroll
+                for (int v = 0; v < 4; ++v) o4[v] = lg4 == 0 ? dl[v] : dl[(4 + v) % KM];
+                *reinterpret_cast<f32x4*>(a.lb_dlog + r * KM + 4 * lg4) = o4;
+              }
               if (a.lb_dh) {
                 // dh[r][c] = (h[r][c] > 0) * sum_k W[k][c] dl[k]: to_logits (1x1, K -> C) dgrad with the
                 // ReLU mask of its input h, the same k-ordered fma chain as the MFMA path; lane group
@@ -226,7 +252,7 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a, int64_t m0, in
                     const int c = c0 + v;
                     float sacc = 0.f;
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) sacc = fmaf(c < C && k < a.N ? a.lb_W[k * C + c] : 0.f, dl[k], sacc);
+                    for (int k = 0; k < KM; ++k) sacc = fmaf(c < C && k < a.N ? a.lb_W[k * C + c] : 0.f, dl[k], sacc);
                     o[v] = hv[v] > 0.f ? sacc : 0.f;
                   }
                   if (st_r) *reinterpret_cast<f32x4*>(a.lb_dh + r * L + c0) = o;
@@ -248,14 +274,16 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a, int64_t m0, in
         }
       }
       if (tail) {  // compile-time in every caller
+#pragma unroll
+        for (int tbk = 0; tbk < TB; ++tbk) {
         // z^T (16 c2 x 16 rows) = tW (16 x N) @ Y^T: B operand = the fragments above
-        f32x4 z = tb0;
+        f32x4 z = tbk == 0 ? tb0 : tb1;
 #pragma unroll
         for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
-          for (int v = 0; v < 4; ++v) z = mfma16x16x4(tw[nb][v], acc[nb][pb][v], z);
-        // lane holds c2 = 4*lg4 + v of row r
-        const int c0 = 4 * lg4;
+          for (int v = 0; v < 4; ++v) z = mfma16x16x4(tbk == 0 ? tw[nb][v] : tw2[nb][v], acc[nb][pb][v], z);
+        // lane holds c2 = 16 tbk + 4*lg4 + v of row r
+        const int c0 = 16 * tbk + 4 * lg4;
 #pragma unroll
         for (int v = 0; v < 4; ++v) z[v] = valid ? z[v] : 0.f;
         if (a.t_out && st_r && c0 < ld4(a.C2)) *reinterpret_cast<f32x4*>(a.t_out + r * ld4(a.C2) + c0) = z;
@@ -267,7 +295,7 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a, int64_t m0, in
             else if (c2 < a.C2) a.t_cf1[(b * (a.C2 - a.t_split) + c2 - a.t_split) * a.T + t] = z[v];
           }
         }
-        if (a.q_out || a.q_cf || a.reg_out) {
+        if (TB == 1 && (a.q_out || a.q_cf || a.reg_out)) {
           float m = -__builtin_inff();
 #pragma unroll
           for (int v = 0; v < 4; ++v)
@@ -305,6 +333,7 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a, int64_t m0, in
             }
             if (st_v && lg4 == 0) a.reg_out[b * a.T + t] = bi;
           }
+        }
         }
       }
     }
@@ -427,7 +456,7 @@ __global__ __launch_bounds__(256, (C2Occ<NB, KCP, TAIL>::W)) void conv2_kernel(C
 // over the grid, with its own 18-row X slot in LDS (written and read by that wave only, so no
 // further workgroup barrier) and its own register prefetch of the next tile.  Up to 4 waves per
 // SIMD keep the MFMA pipe fed while the others run their epilogues, stores and loads.
-template <int NB, int KCP, int KS>
+template <int NB, int KCP, int KS, int TB = 1>
 struct C2wCfg {
   static constexpr int KCW = KCP * 16;
   static constexpr int LDX = KCW + 8;          // = c2_ldx: conflict-free b128 operand reads
@@ -437,9 +466,39 @@ struct C2wCfg {
   static constexpr int PF = (XF4 + 63) / 64;   // float4 slots per lane
   static constexpr size_t W_FLOATS = (size_t)KS * NW * LDX;
   static constexpr size_t X_FLOATS = (size_t)XROWS * LDX;
-  static constexpr size_t E_FLOATS = (size_t)NW + 16 * NW + 16;  // bias, tail weight (16 x NW), tail bias
+  static constexpr int ET = 1 + 16 * TB;                          // rows of [bias | tail weight]
+  static constexpr size_t E_FLOATS = (size_t)NW * ET + 16 * TB;  // bias, tail weight (16 TB x NW), tail bias
   static constexpr size_t lds(int wpg) { return (W_FLOATS + E_FLOATS + (size_t)wpg * X_FLOATS) * 4; }
 };
+
+// Per-tile epilogue constants from the workgroup's LDS block Es = [bias (NW) | tail weight (16 TB x NW)
+// | tail bias (16 TB)]: bias of this lane's channels, tail weight columns (c2 = l16, and 16 + l16 for
+// the second block), tail bias of c2 = 4 lg4 .. (+16).
+template <int NB, int TB, int NW, int ET>
+__device__ __forceinline__ void c2_tail_consts(const float* Es, int lg4, int l16, bool tail, float (&bias_r)[NB][4],
+                                               float (&tw)[NB][4], float (&tw2)[NB][4], f32x4& tb0, f32x4& tb1) {
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    const float4 b4 = *reinterpret_cast<const float4*>(Es + nb * 16 + 4 * lg4);
+    bias_r[nb][0] = b4.x; bias_r[nb][1] = b4.y; bias_r[nb][2] = b4.z; bias_r[nb][3] = b4.w;
+    if (tail) {
+      const float4 t4 = *reinterpret_cast<const float4*>(Es + NW + l16 * NW + nb * 16 + 4 * lg4);
+      tw[nb][0] = t4.x; tw[nb][1] = t4.y; tw[nb][2] = t4.z; tw[nb][3] = t4.w;
+      if constexpr (TB > 1) {
+        const float4 u4 = *reinterpret_cast<const float4*>(Es + NW + (16 + l16) * NW + nb * 16 + 4 * lg4);
+        tw2[nb][0] = u4.x; tw2[nb][1] = u4.y; tw2[nb][2] = u4.z; tw2[nb][3] = u4.w;
+      }
+    }
+  }
+  if (tail) {
+    const float4 t4 = *reinterpret_cast<const float4*>(Es + ET * NW + 4 * lg4);
+    tb0 = f32x4{t4.x, t4.y, t4.z, t4.w};
+    if constexpr (TB > 1) {
+      const float4 u4 = *reinterpret_cast<const float4*>(Es + ET * NW + 16 + 4 * lg4);
+      tb1 = f32x4{u4.x, u4.y, u4.z, u4.w};
+    }
+  }
+}
 
 // waves per workgroup the register budget is sized for: 4 per SIMD (128 VGPRs) where that fits
 // without spills, 3 (170) for the wide layers
@@ -448,9 +507,10 @@ struct C2wOcc {
   static constexpr int MAXW = NB * KCP >= 8 ? 12 : 16;
 };
 
-template <int NB, int KCP, int KS, int ACT, bool TAIL, bool PK = false>
+template <int NB, int KCP, int KS, int ACT, int TAIL, bool PK = false>
 __global__ __launch_bounds__((64 * C2wOcc<NB, KCP>::MAXW)) void conv2w_kernel(ConvArgs a, int64_t ntiles) {
-  using C = C2wCfg<NB, KCP, KS>;
+  constexpr int TBC = TAIL > 1 ? TAIL : 1;  // tail blocks
+  using C = C2wCfg<NB, KCP, KS, TBC>;
   extern __shared__ float4 smem4[];
   float* Ws = reinterpret_cast<float*>(smem4);  // [KS][NW][LDX]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -479,11 +539,11 @@ __global__ __launch_bounds__((64 * C2wOcc<NB, KCP>::MAXW)) void conv2w_kernel(Co
     float v = 0.f;
     if (i < C::NW) {
       v = (a.bias && i < a.N) ? a.bias[i] : 0.f;
-    } else if (i < 17 * C::NW) {
+    } else if (i < C::ET * C::NW) {
       const int j = i - C::NW, c2 = j / C::NW, n = j - c2 * C::NW;
       v = (TAIL && c2 < a.C2 && n < a.N) ? a.tW[(int64_t)c2 * a.N + n] : 0.f;
     } else {
-      const int c2 = i - 17 * C::NW;
+      const int c2 = i - C::ET * C::NW;
       v = (TAIL && a.tb && c2 < a.C2) ? a.tb[c2] : 0.f;
     }
     Es[i] = v;
@@ -537,22 +597,11 @@ __global__ __launch_bounds__((64 * C2wOcc<NB, KCP>::MAXW)) void conv2w_kernel(Co
     if constexpr (PK) c2_mfma_pk<NB, C::LDX, C::NW>(Ws, Xs, lg4, l16, a.Kc, acc);
     else c2_mfma_tile<NB, 1, KCP, KS, C::LDX, C::NW>(Ws, Xs, lg4, l16, acc, a.pipe);
     __builtin_amdgcn_wave_barrier();  // the slot's reads are done before the next tile overwrites it
-    float bias_r[NB][4], tw[NB][4];
-    f32x4 tb0 = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb) {
-      const float4 b4 = *reinterpret_cast<const float4*>(Es + nb * 16 + 4 * lg4);
-      bias_r[nb][0] = b4.x; bias_r[nb][1] = b4.y; bias_r[nb][2] = b4.z; bias_r[nb][3] = b4.w;
-      if constexpr (TAIL) {
-        const float4 t4 = *reinterpret_cast<const float4*>(Es + C::NW + l16 * C::NW + nb * 16 + 4 * lg4);
-        tw[nb][0] = t4.x; tw[nb][1] = t4.y; tw[nb][2] = t4.z; tw[nb][3] = t4.w;
-      }
-    }
-    if constexpr (TAIL) {
-      const float4 t4 = *reinterpret_cast<const float4*>(Es + 17 * C::NW + 4 * lg4);
-      tb0 = f32x4{t4.x, t4.y, t4.z, t4.w};
-    }
-    conv2_epilogue<NB, 1, ACT>(a, m0, 0, lg4, l16, acc, auxv, bias_r, tw, tb0, sc, TAIL);
+    float bias_r[NB][4], tw[NB][4], tw2[NB][4];
+    f32x4 tb0 = f32x4{0.f, 0.f, 0.f, 0.f}, tb1 = tb0;
+    c2_tail_consts<NB, TBC, C::NW, C::ET>(Es, lg4, l16, TAIL != 0, bias_r, tw, tw2, tb0, tb1);
+    conv2_epilogue<NB, 1, ACT, TBC>(a, m0, 0, lg4, l16, acc, auxv, bias_r, tw, tb0, sc, TAIL, 0, 16, nullptr, 0, tw2,
+                                    tb1);
     tile = next;
   }
 }
@@ -575,19 +624,20 @@ static int conv_wmax(int dflt) {
 // re-read from HBM and the front launch disappears.  Every front row goes through the unfused
 // launch's MFMA sequence and epilogue, so stored and consumed values are the same bits as the
 // two-launch path (a halo row is computed by both tiles that touch it, identically).
-template <int NB, bool TAIL, int FKS>
+template <int NB, int TAIL, int FKS, int FKCP = 1>
 struct C2fCfg {
-  using C = C2wCfg<NB, 4, 3>;   // this conv: 33 .. 64 input channels
-  using F = C2wCfg<4, 1, FKS>;  // front: <= 16 -> <= 64 channels
+  using C = C2wCfg<NB, 4, 3, (TAIL > 1 ? TAIL : 1)>;  // this conv: 33 .. 64 input channels
+  using F = C2wCfg<4, FKCP, FKS>;  // front: <= 16 FKCP -> <= 64 channels
   static constexpr int TR = 14;  // output rows per tile
   static constexpr size_t lds(int wpg) {
     return (C::W_FLOATS + C::E_FLOATS + F::W_FLOATS + 64 + (size_t)wpg * (F::X_FLOATS + C::X_FLOATS)) * 4;
   }
 };
 
-template <int NB, bool TAIL, int FKS, int ACT, bool FPK>
+template <int NB, int TAIL, int FKS, int ACT, bool FPK, int FKCP = 1>
 __global__ __launch_bounds__(64 * 12) void conv2f_kernel(ConvArgs a, int64_t ntiles) {
-  using Q = C2fCfg<NB, TAIL, FKS>;
+  constexpr int TBC = TAIL > 1 ? TAIL : 1;
+  using Q = C2fCfg<NB, TAIL, FKS, FKCP>;
   using C = typename Q::C;
   using F = typename Q::F;
   constexpr int TR = Q::TR;
@@ -616,11 +666,11 @@ __global__ __launch_bounds__(64 * 12) void conv2f_kernel(ConvArgs a, int64_t nti
     float v = 0.f;
     if (i < C::NW) {
       v = (a.bias && i < a.N) ? a.bias[i] : 0.f;
-    } else if (i < 17 * C::NW) {
+    } else if (i < C::ET * C::NW) {
       const int j = i - C::NW, c2 = j / C::NW, n = j - c2 * C::NW;
       v = (TAIL && c2 < a.C2 && n < a.N) ? a.tW[(int64_t)c2 * a.N + n] : 0.f;
     } else {
-      const int c2 = i - 17 * C::NW;
+      const int c2 = i - C::ET * C::NW;
       v = (TAIL && a.tb && c2 < a.C2) ? a.tb[c2] : 0.f;
     }
     Es[i] = v;
@@ -679,7 +729,7 @@ __global__ __launch_bounds__(64 * 12) void conv2f_kernel(ConvArgs a, int64_t nti
 #pragma unroll
     for (int nb = 0; nb < 4; ++nb) acc1[nb][0] = f32x4{0.f, 0.f, 0.f, 0.f};
     if constexpr (FPK) c2_mfma_pk<4, F::LDX, F::NW>(Fs, X1, lg4, l16, a.f_Kc, acc1);  // = the unfused front's
-    else c2_mfma_tile<4, 1, 1, FKS, F::LDX, F::NW>(Fs, X1, lg4, l16, acc1, a.pipe);
+    else c2_mfma_tile<4, 1, FKCP, FKS, F::LDX, F::NW>(Fs, X1, lg4, l16, acc1, a.pipe);
     {
       float b1[4][4], tw0[4][4] = {};
 #pragma unroll
@@ -700,29 +750,18 @@ __global__ __launch_bounds__(64 * 12) void conv2f_kernel(ConvArgs a, int64_t nti
     for (int nb = 0; nb < NB; ++nb) acc[nb][0] = f32x4{0.f, 0.f, 0.f, 0.f};
     c2_mfma_tile<NB, 1, 4, 3, C::LDX, C::NW>(Ws, Xs, lg4, l16, acc, a.pipe);
     __builtin_amdgcn_wave_barrier();  // the slots' reads are done before the next tile overwrites them
-    float bias_r[NB][4], tw[NB][4];
-    f32x4 tb0 = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb) {
-      const float4 b4 = *reinterpret_cast<const float4*>(Es + nb * 16 + 4 * lg4);
-      bias_r[nb][0] = b4.x; bias_r[nb][1] = b4.y; bias_r[nb][2] = b4.z; bias_r[nb][3] = b4.w;
-      if constexpr (TAIL) {
-        const float4 t4 = *reinterpret_cast<const float4*>(Es + C::NW + l16 * C::NW + nb * 16 + 4 * lg4);
-        tw[nb][0] = t4.x; tw[nb][1] = t4.y; tw[nb][2] = t4.z; tw[nb][3] = t4.w;
-      }
-    }
-    if constexpr (TAIL) {
-      const float4 t4 = *reinterpret_cast<const float4*>(Es + 17 * C::NW + 4 * lg4);
-      tb0 = f32x4{t4.x, t4.y, t4.z, t4.w};
-    }
-    conv2_epilogue<NB, 1, ACT>(a, m0, 0, lg4, l16, acc, auxv, bias_r, tw, tb0, sc, TAIL, 0, TR);
+    float bias_r[NB][4], tw[NB][4], tw2[NB][4];
+    f32x4 tb0 = f32x4{0.f, 0.f, 0.f, 0.f}, tb1 = tb0;
+    c2_tail_consts<NB, TBC, C::NW, C::ET>(Es, lg4, l16, TAIL != 0, bias_r, tw, tw2, tb0, tb1);
+    conv2_epilogue<NB, 1, ACT, TBC>(a, m0, 0, lg4, l16, acc, auxv, bias_r, tw, tb0, sc, TAIL, 0, TR, nullptr, 0, tw2,
+                                    tb1);
     tile = next;
   }
 }
 
-template <int NB, bool TAIL, int FKS, int ACT>
+template <int NB, int TAIL, int FKS, int ACT, int FKCP = 1>
 static int launch_c2f(const ConvArgs& a, hipStream_t s) {
-  using Q = C2fCfg<NB, TAIL, FKS>;
+  using Q = C2fCfg<NB, TAIL, FKS, FKCP>;
   ConvArgs ap = a;
   ap.pipe = 1;
   const int64_t ntiles = cdiv(a.R, Q::TR);
@@ -741,7 +780,7 @@ static int launch_c2f(const ConvArgs& a, hipStream_t s) {
       return VQHMM_OK;
     }
   }
-  conv2f_kernel<NB, TAIL, FKS, ACT, false><<<(unsigned)grid, 64 * wpg, Q::lds(wpg), s>>>(ap, ntiles);
+  conv2f_kernel<NB, TAIL, FKS, ACT, false, FKCP><<<(unsigned)grid, 64 * wpg, Q::lds(wpg), s>>>(ap, ntiles);
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
 }
@@ -749,19 +788,28 @@ static int launch_c2f(const ConvArgs& a, hipStream_t s) {
 bool conv2_fused_supported(const ConvArgs& a) {
   const bool relu_pair = a.act == 1 && a.f_act == 1 && a.f_ks == 3;                        // forward
   const bool mask_pair = a.act == 2 && a.f_act == 2 && a.f_ks == 1 && a.aux && a.f_aux && !a.tW;  // data grad
+  // front input channels: <= 16 (one k-block), or <= 32 for the 1x1 data-gradient front (to_params at D = 16)
   return a.f_Wimg && a.Wimg && a.f_out && !a.src_cf && a.ks == 3 && (relu_pair || mask_pair) && a.f_Kc >= 1 &&
-         a.f_Kc <= 16 && a.Kc > 32 && a.Kc <= 64 && a.N <= 64 && (a.tW == nullptr || a.C2 <= 16) && !a.out_cf;
+         (a.f_Kc <= 16 || (mask_pair && a.f_Kc <= 32)) && a.Kc > 32 && a.Kc <= 64 && a.N <= 64 && conv2_tail_ok(a) &&
+         !a.out_cf;
 }
 
 int launch_conv2_fused(const ConvArgs& a, hipStream_t s) {
   if (!conv2_fused_supported(a)) return VQHMM_EUNSUPPORTED;
   if (a.R == 0) return VQHMM_OK;
-  if (a.act == 2) return a.N <= 64 && a.N > 32 ? launch_c2f<4, false, 1, 2>(a, s)
-                         : a.N > 16 ? launch_c2f<2, false, 1, 2>(a, s) : launch_c2f<1, false, 1, 2>(a, s);
-  const bool tail = a.tW != nullptr;
-  if (a.N <= 16) return tail ? launch_c2f<1, true, 3, 1>(a, s) : launch_c2f<1, false, 3, 1>(a, s);
-  if (a.N <= 32) return tail ? launch_c2f<2, true, 3, 1>(a, s) : launch_c2f<2, false, 3, 1>(a, s);
-  return tail ? launch_c2f<4, true, 3, 1>(a, s) : launch_c2f<4, false, 3, 1>(a, s);
+  if (a.act == 2) {
+    if (a.f_Kc > 16)
+      return a.N <= 64 && a.N > 32 ? launch_c2f<4, 0, 1, 2, 2>(a, s)
+             : a.N > 16 ? launch_c2f<2, 0, 1, 2, 2>(a, s) : launch_c2f<1, 0, 1, 2, 2>(a, s);
+    return a.N <= 64 && a.N > 32 ? launch_c2f<4, 0, 1, 2>(a, s)
+           : a.N > 16 ? launch_c2f<2, 0, 1, 2>(a, s) : launch_c2f<1, 0, 1, 2>(a, s);
+  }
+  const int tail = a.tW == nullptr ? 0 : a.C2 > 16 ? 2 : 1;
+  if (a.N <= 16)
+    return tail == 2 ? launch_c2f<1, 2, 3, 1>(a, s) : tail ? launch_c2f<1, 1, 3, 1>(a, s) : launch_c2f<1, 0, 3, 1>(a, s);
+  if (a.N <= 32)
+    return tail == 2 ? launch_c2f<2, 2, 3, 1>(a, s) : tail ? launch_c2f<2, 1, 3, 1>(a, s) : launch_c2f<2, 0, 3, 1>(a, s);
+  return tail == 2 ? launch_c2f<4, 2, 3, 1>(a, s) : tail ? launch_c2f<4, 1, 3, 1>(a, s) : launch_c2f<4, 0, 3, 1>(a, s);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -911,9 +959,9 @@ static bool conv2_pipe() {
   return v;
 }
 
-template <int NB, int KCP, int KS, int ACT, bool TAIL>
+template <int NB, int KCP, int KS, int ACT, int TAIL>
 static int launch_c2w(const ConvArgs& a, hipStream_t s) {
-  using C = C2wCfg<NB, KCP, KS>;
+  using C = C2wCfg<NB, KCP, KS, (TAIL > 1 ? TAIL : 1)>;
   const int64_t ntiles = cdiv(a.R, 16);
   int wmax = conv_wmax(C2wOcc<NB, KCP>::MAXW);
   while (wmax > 1 && C::lds(wmax) > 160 * 1024) --wmax;
@@ -934,22 +982,21 @@ static int launch_c2w(const ConvArgs& a, hipStream_t s) {
   return VQHMM_OK;
 }
 
-bool conv2_supported(const ConvArgs& a) {
-  return !a.src_cf && a.N <= 64 && a.Kc <= 64 && (a.tW == nullptr || a.C2 <= 16);
-}
+bool conv2_supported(const ConvArgs& a) { return !a.src_cf && a.N <= 64 && a.Kc <= 64 && conv2_tail_ok(a); }
 
-template <int NB, int KCP, int KS, int PB, int ACT, bool TAIL>
+template <int NB, int KCP, int KS, int PB, int ACT, int TAIL>
 static int launch_c2v(const ConvArgs& a, hipStream_t s) {
   ConvArgs ap = a;
   ap.pipe = conv2_pipe();
   if (conv2_wave_mode(a.R)) return launch_c2w<NB, KCP, KS, ACT, TAIL>(ap, s);
+  if constexpr (TAIL > 1) return VQHMM_EUNSUPPORTED;  // the workgroup-tile A/B kernel: one tail block
   using C = C2Cfg<NB, KCP, KS, PB>;
   const int64_t ntiles = cdiv(a.R, C::BM);
   int per_cu = (int)((160 * 1024) / C::LDS);
   if (per_cu < 1) return VQHMM_EUNSUPPORTED;
   if (per_cu > 4) per_cu = 4;
   const int64_t grid = ntiles < 256LL * per_cu ? ntiles : 256LL * per_cu;
-  conv2_kernel<NB, KCP, KS, PB, ACT, TAIL><<<(unsigned)grid, 256, C::LDS, s>>>(ap, ntiles);
+  conv2_kernel<NB, KCP, KS, PB, ACT, (TAIL != 0)><<<(unsigned)grid, 256, C::LDS, s>>>(ap, ntiles);
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
 }
@@ -961,17 +1008,22 @@ static int launch_c2p(const ConvArgs& a, hipStream_t s) {
   const bool tail = a.tW != nullptr;
   if (tail) {
     if constexpr (KS == 3) {
-      if (a.act == 1) return launch_c2v<NB, KCP, KS, PB, 1, true>(a, s);
+      if (a.act == 1)
+        return a.C2 > 16 ? launch_c2v<NB, KCP, KS, PB, 1, 2>(a, s) : launch_c2v<NB, KCP, KS, PB, 1, 1>(a, s);
     }
     return VQHMM_EUNSUPPORTED;
   }
-  if (a.act == 3) {
-    if constexpr (NB == 1 && KS == 3) return launch_c2v<NB, KCP, KS, PB, 3, false>(a, s);
+  if (a.act == 4) {  // K <= 8 softmax backward
+    if constexpr (NB == 1 && KS == 3) return launch_c2v<NB, KCP, KS, PB, 4, 0>(a, s);
     return VQHMM_EUNSUPPORTED;
   }
-  if (a.act == 2) return launch_c2v<NB, KCP, KS, PB, 2, false>(a, s);
-  if (a.act == 1) return launch_c2v<NB, KCP, KS, PB, 1, false>(a, s);
-  return launch_c2v<NB, KCP, KS, PB, 0, false>(a, s);
+  if (a.act == 3) {
+    if constexpr (NB == 1 && KS == 3) return launch_c2v<NB, KCP, KS, PB, 3, 0>(a, s);
+    return VQHMM_EUNSUPPORTED;
+  }
+  if (a.act == 2) return launch_c2v<NB, KCP, KS, PB, 2, 0>(a, s);
+  if (a.act == 1) return launch_c2v<NB, KCP, KS, PB, 1, 0>(a, s);
+  return launch_c2v<NB, KCP, KS, PB, 0, 0>(a, s);
 }
 
 // rows per tile = 64*PB; PB = 1 (measured best: it halves the X tile so more

@@ -89,6 +89,28 @@ __global__ __launch_bounds__(256, 2) void elbo_head_wave_kernel(HeadArgs a) {
   const float cent = a.beta / Bn;   // d loss / d (sum q*log q)
   auto& W = sh.wv[wave];
 
+  // windows dealt across the grid first: w = k * (4 * grid) + wave * grid + block
+  const int64_t nwin = cdiv(a.R, WOWN);
+  const int64_t stride = 4 * (int64_t)gridDim.x;
+  // the slot rotates with the block so the waves that get one window more sit on different SIMDs
+  int64_t w = (int64_t)((wave + blockIdx.x) & 3) * gridDim.x + blockIdx.x;
+  // row inputs of window wl (lane p = row wl * WOWN + p, clamped; validity from r where used).  With
+  // 1- or 2-block windows (small batches: a wave's chain, not the work, sets the time) the first
+  // window's are issued here, in flight across the weight staging, and every later window's right after
+  // the phase that last reads the current ones (B), in flight across phase C; 4-block windows have no
+  // registers to spare for rows held across C (38-59 VGPRs of spill) and load at the window's start.
+  constexpr bool PF_C = NBW <= 2;
+  const unsigned Tp = (unsigned)a.T + 2u;
+  HwRow<DM> cur;
+  float qprev_cur = 0.f;
+  auto load_win = [&](int64_t wl) {
+    const int64_t rr = wl * WOWN + lane;
+    const unsigned rc = (unsigned)(rr < a.R ? rr : a.R - 1);
+    hw_load<DM>(a, rc, (int)(rc / Tp), cur);
+    qprev_cur = a.q[(wl * WOWN - 1 < 0 ? 0 : wl * WOWN - 1) * 4 + (lane & 3)];  // lane k < K: q[r0 - 1][k]
+  };
+  if (PF_C && w < nwin) load_win(w);
+
   // ---- one-time: weights to LDS, log_pi, valid count
 #pragma unroll 8  // independent load -> store iterations: keep 8 loads in flight
   for (int i = tid; i < 16 * S::LDW2 && !(a.dbg & 16); i += 256) {
@@ -265,26 +287,16 @@ __global__ __launch_bounds__(256, 2) void elbo_head_wave_kernel(HeadArgs a) {
     }
   };
 
-  // windows dealt across the grid first: w = k * (4 * grid) + wave * grid + block
-  const int64_t nwin = cdiv(a.R, WOWN);
-  const int64_t stride = 4 * (int64_t)gridDim.x;
-  // the slot rotates with the block so the waves that get one window more sit on different SIMDs
-  int64_t w = (int64_t)((wave + blockIdx.x) & 3) * gridDim.x + blockIdx.x;
-  // (a wave sees 1-2 windows at the cfg2 sizes, so rows are loaded at the window's start —
-  // phase A waits only for u — rather than prefetched a window ahead in registers)
   for (; w < nwin && !(a.dbg & 8); w += stride) {
+    if (!PF_C) load_win(w);
     const int64_t r0 = w * WOWN;
     const int nown = (int)min<int64_t>(WOWN, a.R - r0);  // rows 0 .. nown-1 owned; row nown halo
     const int p = lane;
     const int64_t r = r0 + p;
     // (b, t) of the row in 32-bit arithmetic (R < 2^31, checked at launch)
-    const unsigned Tp = (unsigned)a.T + 2u;
     const unsigned rcl = (unsigned)(r < a.R ? r : a.R - 1);
     const int b = (int)(rcl / Tp);
     const int t = (int)(rcl - (unsigned)b * Tp) - 1;
-    HwRow<DM> cur;
-    hw_load<DM>(a, rcl, b, cur);
-    const float qprev_cur = a.q[(r0 - 1 < 0 ? 0 : r0 - 1) * 4 + (lane & 3)];  // lane k < K: q[r0 - 1][k]
     const bool valid = p <= nown && r < a.R && t >= 0 && t < a.T;
     const bool own = p < nown;
     const bool m = valid && t < cur.L;  // inside the sequence's length
@@ -450,6 +462,8 @@ __global__ __launch_bounds__(256, 2) void elbo_head_wave_kernel(HeadArgs a) {
       }
     }
     }
+    // the next window's rows: B was the last reader of cur / qprev_cur
+    if (PF_C && w + stride < nwin) load_win(w + stride);
     // ---------------- C: MLP backward (MFMA)
     if (a.need_grad && !(a.dbg & 4)) {
       phase_c();

@@ -34,7 +34,7 @@ struct ConvArgs {
   float* q_out;      // PCL softmax of the tail
   float* q_cf;       // CF softmax of the tail
   int32_t* reg_out;  // (B, T) first-index argmax over channels of that softmax (torch.argmax rule)
-  // act == 3 (conv2 only, N <= 4): the output y = dL/dq of the decoder path is also
+  // act == 3 (conv2 only, N <= 4; act == 4: N <= 8): the output y = dL/dq of the decoder path is also
   // pushed through the softmax backward (logits_bwd_kernel's formula):
   // lb_dlog = q * (dq - <q, dq>) + scale * lb_dlx,  dq = y + scale * lb_dqx
   const float* lb_q;
