@@ -34,11 +34,15 @@ struct Carver {
   }
 };
 
-// A/B switch to the previous tile-barrier MFMA head (VQHMM_HEAD=tile), read once.
-bool head_legacy() {
-  static const bool v = [] {
+// Head choice (VQHMM_HEAD, read once): default the workgroup-cooperative head (head_coop.hip) wherever it
+// applies; "wave" = the wave-window head for K <= 4 (head_wave.hip), "tile" = the tile-barrier MFMA head
+// (head_mfma.hip) — A/B switches.
+int head_choice() {
+  static const int v = [] {
     const char* e = getenv("VQHMM_HEAD");
-    return e && strcmp(e, "tile") == 0;
+    if (e && strcmp(e, "tile") == 0) return 2;
+    if (e && strcmp(e, "wave") == 0) return 1;
+    return 0;
   }();
   return v;
 }
@@ -93,8 +97,8 @@ struct ElboPlan {
                              // prologue and re-armed by the tail itself), [2] the status word, [3] spare
   // staged head (shapes the fused heads do not cover): Prior MLP as 1x1 convs
   bool staged;
-  bool wave_head;  // head_wave.hip (K <= 4)
-  bool k8_head;    // head_k8.hip (5 <= K <= 8); else head_mfma / head.hip
+  bool wave_head;  // head_wave.hip (K <= 4, VQHMM_HEAD=wave)
+  bool coop_head;  // head_coop.hip (K <= 8, the default); else head_mfma / head.hip
   float *hid, *lgA, *dhid, *nx, *dqc, *trw, *logpi;
   // backward
   float *dg2, *dg1, *dqd, *dlog, *dh2, *dh1, *dWc;
@@ -129,10 +133,10 @@ ElboPlan plan_elbo(const vqhmm_dims_t* d, int64_t B, int64_t T, void* ws) {
     HeadArgs hc{};
     hc.K = K; hc.U = p.U; hc.TH = p.TH; hc.D = D;
     hc.R = R;
-    p.wave_head = head_mfma_supported(hc) && p.U <= 4 && !head_legacy();
-    p.k8_head = !p.wave_head && head_k8_supported(hc) && !head_legacy();
+    p.coop_head = head_coop_supported(hc) && head_choice() == 0;
+    p.wave_head = !p.coop_head && head_mfma_supported(hc) && p.U <= 4 && head_choice() == 1;
   }
-  p.hgrid = p.wave_head ? head_wave_grid(R) : p.k8_head ? head_k8_grid(R) : head_grid(R);
+  p.hgrid = p.coop_head ? head_coop_grid(R, K) : p.wave_head ? head_wave_grid(R) : head_grid(R);
   p.dpar = c.take<float>(R * ld4(2 * D));
   p.dqx = c.take<float>(R * ld4(K));
   p.dlx = c.take<float>(R * ld4(K));
@@ -185,7 +189,7 @@ ElboPlan plan_elbo(const vqhmm_dims_t* d, int64_t B, int64_t T, void* ws) {
     w.N = shapes[i][0]; w.C = shapes[i][1]; w.ks = shapes[i][2];
     const int64_t tiles = cdiv(w.N, 64) * cdiv(w.C, 64);
     w.rows = (w.N <= 64 && w.C <= 64) ? wgrad2_rows(R, w.N, w.C, w.ks) : wgrad_chunks(R, tiles);
-    if (i < 6 && p.wgroup) w.rows = std::max<int64_t>(w.rows, wgroup_min_rows());
+    if (i < 6 && p.wgroup) w.rows = wgrad2_group_rows(std::max<int64_t>(w.rows, wgroup_min_rows()), w.N, w.C, w.ks);
     w.nchunks = cdiv(R, w.rows);
     w.slab = c.take<float>((size_t)w.nchunks * w.N * w.C * w.ks);
     w.bslab = c.take<float>((size_t)w.nchunks * w.N);
@@ -614,8 +618,8 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       if (c.need_grad == 2 && !c.norm) h.cnt_in = p.cnt;  // the prologue counted the batch (S_TOPCL)
       h.dpar = p.dpar; h.dqx = p.dqx; h.dlx = p.dlx; h.part = p.part;
       h.slab_W1 = p.sW1; h.slab_b1 = p.sb1; h.slab_W2 = p.sW2; h.slab_b2 = p.sb2; h.slab_q0 = p.sq0;
+      if (p.coop_head) return launch_head_coop(h, p.hgrid, s);
       if (p.wave_head) return launch_head_wave(h, p.hgrid, s);
-      if (p.k8_head) return launch_head_k8(h, p.hgrid, s);
       return launch_head(h, p.hgrid, s);
     }
     case S_FINAL:
@@ -694,7 +698,7 @@ void stage_work(const ElboPlan& p, int st, double* flops, double* bytes, int* mf
     *bytes = 4.0 * R * (2 * p.D + p.D + p.U + 2 * p.K + 2 * p.D + 2 * p.K);
     HeadArgs h{};
     h.K = p.K; h.U = p.U; h.TH = p.TH; h.D = p.D; h.R = p.R;
-    *mfma = (head_mfma_supported(h) || head_k8_supported(h)) ? 1 : 0;
+    *mfma = (head_mfma_supported(h) || head_coop_supported(h)) ? 1 : 0;
   } else if (st == S_TOPCL) {
     *bytes = 4.0 * (N * (p.D + p.U) + R * (ld4(p.D) + ld4(p.U)));
   } else if (st == S_LOGIT_BWD) {

@@ -1,76 +1,83 @@
-// Fused ELBO head for 5 <= K <= 8 (cfg4: K = 8, D = 16), U <= 4, TH in {64, 128, 256}, D <= 16:
+// Fused ELBO head, workgroup-cooperative windows (K <= 8, U <= 4, TH in {64, 128, 256}, D <= 16):
 // all of A4 + A8..A10 and their gradients (VQ_VAE_HMM_fixed.py:59-71 Prior MLP, :106-137 loss)
 // per PCL row, the Prior MLP forward and backward on v_mfma_f32_16x16x4_f32.
 //
-// At K = 8 the Prior MLP is U -> TH -> K^2 = 64 (51 kFLOP per position forward + backward, 5.6x
-// the K = 3 head), so the MLP, not the per-row VALU work, sets the time.  head_wave.hip keeps every
-// weight-gradient accumulator of a window in each wave; at K^2 = 64 that is 160 accumulator
-// registers per lane, so this kernel shares a window between the workgroup's 4 waves instead:
-//   window = 32 consecutive PCL rows (31 owned + 1 halo row whose log_A the last owned row's
-//            t -> t+1 term needs), processed by the whole workgroup, 3 LDS barriers per window;
-//   A      wave w computes transition-logit block ij in [16w, 16w+16) for the window's rows
-//          (lg^T = W2 relu(W1' u'^T) + b2; every wave recomputes the 2 x HB hidden MFMAs);
-//   B      thread = (row p, source state i) (8 threads per row, i >= K idle): the row of
-//          log_softmax -> log_A[i][:], the mean-field transition term, d log_A -> d logits,
-//          dq (the sum over i is a reduce-scatter over the row's 8 lanes on DPP), recon NLL
-//          (channels i, i+8), entropy (DPP over the 8 lanes), init term;
-//   C      wave w owns hidden blocks [w HBW, (w+1) HBW): hid (rows x h), dh = dlg W2, the
-//          ReLU mask, gW2[:, its h] += dlg^T relu(hid), gW1'[its h] += dhid^T u'.
-// Accumulators per lane: 4 KB x HBW + 4 HBW floats (40 at TH = 128), no cross-wave sums; the
-// workgroup's partial slabs have the layout head_wave.hip writes (same tail reduction).
+// The four waves of a workgroup share one window of WR consecutive PCL rows (WR - 1 owned + 1 halo
+// row whose log_A the last owned row's t -> t+1 term needs), 3 LDS barriers per window:
+//   A  transition logits lg^T = W2 relu(W1' u'^T) + b2 as (ij block, 16-row block) tasks dealt over
+//      the waves (a wave recomputes the hidden MFMAs of its row block);
+//   B  thread = (row p, source state i), KP threads per row (KP = 4 for K <= 4, 8 for K <= 8; i >= K
+//      idle): the row of log_softmax -> log_A[i][:], the mean-field transition term, d log_A ->
+//      d logits, dq (the sum over i is a reduce-scatter over the row's KP lanes on DPP), recon NLL
+//      (channels i, i + KP, ..), entropy (DPP over the row's lanes), init term;
+//   C  wave w owns hidden blocks [w HBW, (w+1) HBW): hid (rows x h), dh = dlg W2, the ReLU mask,
+//      gW2[:, its h] += dlg^T relu(hid), gW1'[its h] += dhid^T u'.
+// A wave keeps only its own hidden blocks' weight-gradient accumulators (4 KB HBW + 4 HBW floats: 16 at
+// K <= 4, 40 at K = 8, TH = 128), so there are no cross-wave sums; the slabs have head_wave.hip's
+// layout (same tail reduction).  WR = 256 / KP: 64 rows (4 row blocks) at K <= 4, 32 (2) at K <= 8.
 // Summation order differs from the reference's autograd; the tests hold it to 1e-5 relative.
 #include "kernels.h"
 
 namespace vqhmm {
 
 namespace {
-constexpr int K8_WR = 32;  // rows per window (incl. the halo row)
-constexpr int K8_WOWN = K8_WR - 1;
-
-template <int K, int HBW>
-struct K8Lds {
+template <int K, int HBW, int KP>
+struct CoopLds {
   static constexpr int KK = K * K;
   static constexpr int KB = (KK + 15) / 16;      // 16-wide ij blocks
   static constexpr int TH = 64 * HBW;
+  static constexpr int WR = 256 / KP;            // rows per window (incl. the halo row)
+  static constexpr int NRB = WR / 16;            // 16-row blocks per window
   static constexpr int LDW2 = TH + 4;            // W2S row stride (b128 phase-A reads conflict-free)
   static constexpr int LDL = 16 * KB + 4;        // lgS / dlgS row stride
   float W2S[16 * KB * LDW2];                     // rows ij >= KK zero
   float W1S[TH * 8];                             // W1' = [W1 | b1 | 0]  (TH x 8)
-  float uS[K8_WR * 8];                           // u' = [u, 1 at column U, 0]
-  float lgS[K8_WR * LDL];                        // transition logits of the window's rows
-  float dlgS[K8_WR * LDL];                       // their gradients (zero for ij >= KK, non-owned rows)
-  float aS[K8_WR * 8];                           // A_i = sum_j q[j] log_A[i][j] per row (next row's dq)
-  float wS[K8_WR];                               // pair weight (t-1, t) per row
+  float uS[WR * 8];                              // u' = [u, 1 at column U, 0]
+  float lgS[WR * LDL];                           // transition logits of the window's rows
+  float dlgS[WR * LDL];                          // their gradients (zero for ij >= KK, non-owned rows)
+  float aS[WR * KP];                             // A_i = sum_j q[j] log_A[i][j] per row (next row's dq)
+  float wS[WR];                                  // pair weight (t-1, t) per row
   double red[4][4];
-  float q0w[4][8];
+  float q0w[4][KP];
   unsigned long long cnt;
 };
 
-// all-reduce over the 8 lanes of a row (lane & 7): quad xor 1, quad xor 2, mirror within 8
 template <int CTRL>
 __device__ __forceinline__ float dppf(float v) {
   return __builtin_bit_cast(float, dpp_u32<CTRL>(__builtin_bit_cast(uint32_t, v)));
 }
-__device__ __forceinline__ float row8_sum(float v) {
+// all-reduce over the KP lanes of a row (lane % KP): quad xor 1, quad xor 2 (+ mirror within 8)
+template <int KP>
+__device__ __forceinline__ float row_sum(float v) {
   v += dppf<0xB1>(v);
   v += dppf<0x4E>(v);
-  return v + dppf<0x141>(v);
+  if constexpr (KP == 8) v += dppf<0x141>(v);
+  return v;
 }
-__device__ __forceinline__ float row8_max(float v) {
+template <int KP>
+__device__ __forceinline__ float row_max(float v) {
   v = fmaxf(v, dppf<0xB1>(v));
   v = fmaxf(v, dppf<0x4E>(v));
-  return fmaxf(v, dppf<0x141>(v));
+  if constexpr (KP == 8) v = fmaxf(v, dppf<0x141>(v));
+  return v;
 }
-// c[j] summed over the row's 8 lanes, lane i of the row ending with the sum for j = i
-// (reduce-scatter: mirror (partner 7 - i) halves the vector, then quad xor 2, then xor 1)
-__device__ __forceinline__ float row8_reduce_scatter(const float (&c)[8], int i) {
-  const bool hi4 = i & 4, hi2 = i & 2, hi1 = i & 1;
+// c[j] summed over the row's KP lanes, lane i of the row ending with the sum for j = i
+// (reduce-scatter: [mirror within 8 (partner 7 - i) halves the vector,] then quad xor 2, then xor 1)
+template <int KP>
+__device__ __forceinline__ float row_reduce_scatter(const float (&c)[KP], int i) {
   float h4[4];
+  if constexpr (KP == 8) {
+    const bool hi4 = i & 4;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const float send = hi4 ? c[k] : c[4 + k];  // what the partner keeps
-    h4[k] = (hi4 ? c[4 + k] : c[k]) + dppf<0x141>(send);
+    for (int k = 0; k < 4; ++k) {
+      const float send = hi4 ? c[k] : c[4 + k];  // what the partner keeps
+      h4[k] = (hi4 ? c[4 + k] : c[k]) + dppf<0x141>(send);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) h4[k] = c[k];
   }
+  const bool hi2 = i & 2, hi1 = i & 1;
   float h2[2];
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
@@ -82,34 +89,64 @@ __device__ __forceinline__ float row8_reduce_scatter(const float (&c)[8], int i)
 }
 
 // the global inputs of thread (row, i)
-template <int DM>
-struct K8Row {
-  float4 q0, q1;  // q of the row, states 0..7 (pad channels are zero)
+template <int DM, int KP>
+struct CoopRow {
+  float q[KP];    // q of the row, states 0 .. KP-1 (pad channels are zero)
   float qprev;    // q of the previous row, state i
   float lg;       // logits of the row, state i
-  float mu[DM / 8], lv[DM / 8], x[DM / 8];
+  float mu[DM / KP], lv[DM / KP], x[DM / KP];
   float u;        // u of the row, channel i (i < 4)
   int64_t L;
 };
 }  // namespace
 
-template <int K, int HBW, int DM>
-__global__ __launch_bounds__(256, 2) void elbo_head_k8_kernel(HeadArgs a) {
-  using S = K8Lds<K, HBW>;
+template <int K, int HBW, int DM, int KP>
+__global__ __launch_bounds__(256, 2) void elbo_head_coop_kernel(HeadArgs a) {
+  using S = CoopLds<K, HBW, KP>;
   constexpr int KK = S::KK, KB = S::KB, HB = 4 * HBW, TH = S::TH, LDL = S::LDL;
+  constexpr int WR = S::WR, WOWN = WR - 1, NRB = S::NRB;
   constexpr int SD = (KK + 3) / 4;  // 4-deep contraction steps over ij holding nonzero dlg
-  constexpr int NC = DM / 8;        // recon channels per lane
+  constexpr int NC = DM / KP;       // recon channels per lane
+  constexpr int NT = KB * NRB;      // phase A tasks (ij block, row block)
   extern __shared__ float4 smem4[];
   S& sh = *reinterpret_cast<S*>(smem4);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lg4 = lane >> 4, l16 = lane & 15;
-  const int prow = tid >> 3, si = tid & 7;  // phase B: (row, source state)
+  const int prow = tid / KP, si = tid % KP;  // phase B: (row, source state)
   const int U = a.U, D = a.D;
   const int ldp = ld4(2 * D), ldx = ld4(D), ldu = ld4(U);
   const float Bn = loss_norm_batch(a.norm, a.B);
   const float cpri = -a.beta / Bn;  // d loss / d (init + trans)[b]
   const float cent = a.beta / Bn;   // d loss / d (sum q*log q)
   const bool grad = a.need_grad != 0;
+
+  const unsigned Tp = (unsigned)a.T + 2u;
+  auto load_row = [&](int64_t r0, CoopRow<DM, KP>& v) {
+    const int64_t r = r0 + prow;
+    const unsigned rcl = (unsigned)(r < a.R ? r : a.R - 1);
+    const int b = (int)(rcl / Tp);
+    v.L = a.lengths[b];
+#pragma unroll
+    for (int h = 0; h < KP / 4; ++h) {
+      const float4 q4 = *reinterpret_cast<const float4*>(a.q + (int64_t)rcl * KP + 4 * h);
+      v.q[4 * h] = q4.x; v.q[4 * h + 1] = q4.y; v.q[4 * h + 2] = q4.z; v.q[4 * h + 3] = q4.w;
+    }
+    v.qprev = a.q[(int64_t)(rcl > 0 ? rcl - 1 : 0) * KP + si];
+    v.lg = a.logits[(int64_t)rcl * KP + si];
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      const int c = min(si + KP * k, D - 1);
+      v.mu[k] = a.par[(int64_t)rcl * ldp + c];
+      v.lv[k] = a.par[(int64_t)rcl * ldp + D + c];
+      v.x[k] = a.x[(int64_t)rcl * ldx + c];
+    }
+    v.u = a.u[(int64_t)rcl * ldu + min(si, ldu - 1)];
+  };
+  // the first window's rows in flight across the weight staging
+  const int64_t nwin = cdiv(a.R, WOWN);
+  CoopRow<DM, KP> cur;
+  int64_t w = blockIdx.x;
+  if (w < nwin) load_row(w * WOWN, cur);
 
   // ---- one-time: weights to LDS, zero the gradient pads, log_pi, valid count
 #pragma unroll 8
@@ -122,7 +159,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_k8_kernel(HeadArgs a) {
     const int h = i >> 3, c = i & 7;
     sh.W1S[i] = c < U ? a.W1[h * U + c] : (c == U ? a.b1[h] : 0.f);
   }
-  for (int i = tid; i < K8_WR * LDL; i += 256) sh.dlgS[i] = 0.f;
+  for (int i = tid; i < WR * LDL; i += 256) sh.dlgS[i] = 0.f;
   if (tid == 0) sh.cnt = a.norm ? (unsigned long long)a.norm[0] : a.cnt_in ? (unsigned long long)*a.cnt_in : 0ull;
   float lp_i = 0.f;  // log_pi[i]
   {
@@ -131,12 +168,6 @@ __global__ __launch_bounds__(256, 2) void elbo_head_k8_kernel(HeadArgs a) {
     float s = 0.f;
     for (int k = 0; k < K; ++k) s += __expf(a.log_prior[k] - m);
     if (si < K) lp_i = a.log_prior[si] - (m + __logf(s));
-  }
-  f32x4 b2f;
-#pragma unroll
-  for (int v = 0; v < 4; ++v) {
-    const int ij = 16 * wave + 4 * lg4 + v;
-    b2f[v] = ij < KK ? a.b2[ij] : 0.f;
   }
   __syncthreads();
   if (!a.norm && !a.cnt_in) {  // valid positions of the batch (mask.sum(), :120)
@@ -161,33 +192,9 @@ __global__ __launch_bounds__(256, 2) void elbo_head_k8_kernel(HeadArgs a) {
     for (int b = 0; b < KB; ++b) gW2[b][hb] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
 
-  const unsigned Tp = (unsigned)a.T + 2u;
-  auto load_row = [&](int64_t r0, K8Row<DM>& v) {
-    const int64_t r = r0 + prow;
-    const unsigned rcl = (unsigned)(r < a.R ? r : a.R - 1);
-    const int b = (int)(rcl / Tp);
-    v.L = a.lengths[b];
-    v.q0 = *reinterpret_cast<const float4*>(a.q + (int64_t)rcl * 8);
-    v.q1 = *reinterpret_cast<const float4*>(a.q + (int64_t)rcl * 8 + 4);
-    v.qprev = a.q[(int64_t)(rcl > 0 ? rcl - 1 : 0) * 8 + si];
-    v.lg = a.logits[(int64_t)rcl * 8 + si];
-#pragma unroll
-    for (int k = 0; k < NC; ++k) {
-      const int c = min(si + 8 * k, D - 1);
-      v.mu[k] = a.par[(int64_t)rcl * ldp + c];
-      v.lv[k] = a.par[(int64_t)rcl * ldp + D + c];
-      v.x[k] = a.x[(int64_t)rcl * ldx + c];
-    }
-    v.u = a.u[(int64_t)rcl * ldu + min(si, ldu - 1)];
-  };
-
-  const int64_t nwin = cdiv(a.R, K8_WOWN);
-  K8Row<DM> cur;
-  int64_t w = blockIdx.x;
-  if (w < nwin) load_row(w * K8_WOWN, cur);
   for (; w < nwin; w += gridDim.x) {
-    const int64_t r0 = w * K8_WOWN;
-    const int nown = (int)min<int64_t>(K8_WOWN, a.R - r0);
+    const int64_t r0 = w * WOWN;
+    const int nown = (int)min<int64_t>(WOWN, a.R - r0);
     const int64_t r = r0 + prow;
     const unsigned rcl = (unsigned)(r < a.R ? r : a.R - 1);
     const int b = (int)(rcl / Tp);
@@ -196,26 +203,61 @@ __global__ __launch_bounds__(256, 2) void elbo_head_k8_kernel(HeadArgs a) {
     const bool own = prow < nown;
     const bool m = valid && t < cur.L;
     const float wgt = (valid && t >= 1 && t < cur.L) ? 1.f : 0.f;  // pair (t-1, t) inside the length
-    float qv[8];
-    qv[0] = cur.q0.x; qv[1] = cur.q0.y; qv[2] = cur.q0.z; qv[3] = cur.q0.w;
-    qv[4] = cur.q1.x; qv[5] = cur.q1.y; qv[6] = cur.q1.z; qv[7] = cur.q1.w;
+    float qv[KP];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) qv[k] = (valid && k < K) ? qv[k] : 0.f;
+    for (int k = 0; k < KP; ++k) qv[k] = (valid && k < K) ? cur.q[k] : 0.f;
     const float qp = (valid && t >= 1 && si < K) ? cur.qprev : 0.f;  // q[t-1][i]
     float qi = 0.f;  // q[t][si] (a select chain: no dynamic register indexing)
 #pragma unroll
-    for (int k = 0; k < 8; ++k) qi = si == k ? qv[k] : qi;
+    for (int k = 0; k < KP; ++k) qi = si == k ? qv[k] : qi;
 
     lds_barrier();  // the previous window's phases B2 / C are done with uS, lgS, dlgS, aS, wS
-    // ---------------- L: u' rows to LDS
-    sh.uS[prow * 8 + si] = si < U ? (valid ? cur.u : 0.f) : (si == U ? 1.f : 0.f);
-    lds_barrier();
-    // ---------------- A: wave w -> logits block ij in [16w, 16w + 16), both 16-row blocks
-    if (wave < KB) {
-      f32x4 lg[2] = {b2f, b2f};
-      float ub[2];
+    // ---------------- L: u' rows to LDS (thread (row, i) writes columns i and i + KP of u')
 #pragma unroll
-      for (int rb = 0; rb < 2; ++rb) ub[rb] = sh.uS[(rb * 16 + l16) * 8 + lg4];
+    for (int c = si; c < 8; c += KP) sh.uS[prow * 8 + c] = c < U ? (valid ? cur.u : 0.f) : (c == U ? 1.f : 0.f);
+    lds_barrier();
+    // ---------------- A: tasks (ij block, 16-row block) over the waves; with 4 ij blocks (K > 6) wave w
+    // takes block w for every row block in one pass (the W2 operands read once for all of them)
+    if constexpr (KB == 4) {
+      f32x4 lg[NRB];
+      float ub[NRB];
+#pragma unroll
+      for (int rb = 0; rb < NRB; ++rb) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int ij = 16 * wave + 4 * lg4 + v;
+          lg[rb][v] = ij < KK ? a.b2[ij] : 0.f;
+        }
+        ub[rb] = sh.uS[(rb * 16 + l16) * 8 + lg4];
+      }
+#pragma unroll 2
+      for (int hb = 0; hb < HB; ++hb) {
+        const float w1a = lg4 < U ? sh.W1S[(hb * 16 + l16) * 8 + lg4] : 0.f;
+        f32x4 bb;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) bb[v] = sh.W1S[(hb * 16 + 4 * lg4 + v) * 8 + U];
+        const f32x4 w2v = *reinterpret_cast<const f32x4*>(&sh.W2S[(wave * 16 + l16) * S::LDW2 + hb * 16 + 4 * lg4]);
+        f32x4 hc[NRB];
+#pragma unroll
+        for (int rb = 0; rb < NRB; ++rb) hc[rb] = mfma16x16x4(w1a, ub[rb], bb);  // hid^T (h x rows), bias start
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+#pragma unroll
+          for (int rb = 0; rb < NRB; ++rb) lg[rb] = mfma16x16x4(w2v[v], relu_f(hc[rb][v]), lg[rb]);
+      }
+#pragma unroll
+      for (int rb = 0; rb < NRB; ++rb)
+        *reinterpret_cast<f32x4*>(&sh.lgS[(rb * 16 + l16) * LDL + wave * 16 + 4 * lg4]) = lg[rb];
+    } else
+    for (int tk = wave; tk < NT; tk += 4) {
+      const int ijb = tk % KB, rb = tk / KB;
+      f32x4 lg;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int ij = 16 * ijb + 4 * lg4 + v;
+        lg[v] = ij < KK ? a.b2[ij] : 0.f;
+      }
+      const float ub = sh.uS[(rb * 16 + l16) * 8 + lg4];
 #pragma unroll 2
       for (int hb = 0; hb < HB; ++hb) {
         // u' columns c >= U are [1 (bias), 0, ..]: only c < U in the MFMA, the bias is the accumulator's start
@@ -223,29 +265,23 @@ __global__ __launch_bounds__(256, 2) void elbo_head_k8_kernel(HeadArgs a) {
         f32x4 bb;
 #pragma unroll
         for (int v = 0; v < 4; ++v) bb[v] = sh.W1S[(hb * 16 + 4 * lg4 + v) * 8 + U];
-        const f32x4 w2v = *reinterpret_cast<const f32x4*>(&sh.W2S[(wave * 16 + l16) * S::LDW2 + hb * 16 + 4 * lg4]);
-        f32x4 hc[2];
+        const f32x4 w2v = *reinterpret_cast<const f32x4*>(&sh.W2S[(ijb * 16 + l16) * S::LDW2 + hb * 16 + 4 * lg4]);
+        const f32x4 hc = mfma16x16x4(w1a, ub, bb);  // hid^T (h x rows), bias start
 #pragma unroll
-        for (int rb = 0; rb < 2; ++rb) hc[rb] = mfma16x16x4(w1a, ub[rb], bb);  // hid^T (h x rows), bias start
-#pragma unroll
-        for (int v = 0; v < 4; ++v)
-#pragma unroll
-          for (int rb = 0; rb < 2; ++rb) lg[rb] = mfma16x16x4(w2v[v], relu_f(hc[rb][v]), lg[rb]);
+        for (int v = 0; v < 4; ++v) lg = mfma16x16x4(w2v[v], relu_f(hc[v]), lg);
       }
-#pragma unroll
-      for (int rb = 0; rb < 2; ++rb)
-        *reinterpret_cast<f32x4*>(&sh.lgS[(rb * 16 + l16) * LDL + wave * 16 + 4 * lg4]) = lg[rb];
+      *reinterpret_cast<f32x4*>(&sh.lgS[(rb * 16 + l16) * LDL + ijb * 16 + 4 * lg4]) = lg;
     }
     lds_barrier();
     // ---------------- B: thread = (row prow, state si)
-    float la[8];
+    float la[KP];
     float A_i = 0.f;
     float rsj = 0.f;  // after the reduce-scatter: sum_i q[t-1][i] log_A[i][si]
     {
       const float* lr = &sh.lgS[prow * LDL + (si < K ? si : 0) * K];
       float mx = -__builtin_inff();
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
+      for (int j = 0; j < KP; ++j) {
         la[j] = j < K ? lr[j] : 0.f;
         if (j < K) mx = fmaxf(mx, la[j]);
       }
@@ -258,13 +294,13 @@ __global__ __launch_bounds__(256, 2) void elbo_head_k8_kernel(HeadArgs a) {
 #pragma unroll
       for (int j = 0; j < K; ++j) A_i = fmaf(qv[j], la[j], A_i);
       if (si >= K) A_i = 0.f;
-      float c[8];
+      float c[KP];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) c[j] = (j < K && si < K) ? qp * la[j] : 0.f;
-      rsj = row8_reduce_scatter(c, si);
+      for (int j = 0; j < KP; ++j) c[j] = (j < K && si < K) ? qp * la[j] : 0.f;
+      rsj = row_reduce_scatter<KP>(c, si);
     }
     if (own && si < K) s_tr = fmaf(wgt * qp, A_i, s_tr);
-    sh.aS[prow * 8 + si] = A_i;
+    sh.aS[prow * KP + si] = A_i;
     if (si == 0) sh.wS[prow] = wgt;
     if (grad && si < K) {  // d log_A[i][:] -> d transition logits (log_softmax backward)
       float qs = 0.f;
@@ -276,14 +312,14 @@ __global__ __launch_bounds__(256, 2) void elbo_head_k8_kernel(HeadArgs a) {
 #pragma unroll
       for (int j = 0; j < K; ++j) dl[j] = g * qv[j] - __expf(la[j]) * rs;
     }
-    // recon NLL (channels si, si + 8) and its gradient
+    // recon NLL (channels si, si + KP, ..) and its gradient
 #pragma unroll
     for (int k = 0; k < NC; ++k) {
-      const int ch = si + 8 * k;
+      const int ch = si + KP * k;
       float dmu = 0.f, dlv = 0.f;
       if (own && m && ch < D) {
         const float ev = __expf(cur.lv[k]);
-        const float var = (ev < 1e-8f ? 1e-8f : ev)  /* clamp(min=1e-8), NaN stays NaN */;
+        const float var = ev < 1e-8f ? 1e-8f : ev;  // clamp(min=1e-8), NaN stays NaN
         const float df = cur.mu[k] - cur.x[k];
         const float r2 = df * df / var;
         s_rec += 0.5f * (__logf(6.2831855f * var) + r2);
@@ -296,14 +332,14 @@ __global__ __launch_bounds__(256, 2) void elbo_head_k8_kernel(HeadArgs a) {
       }
     }
     if (grad && own && 2 * D + si < ldp) a.dpar[r * ldp + 2 * D + si] = 0.f;
-    // entropy and its direct logits gradient (reductions over the row's 8 lanes)
+    // entropy and its direct logits gradient (reductions over the row's lanes)
     {
       const float lgv = (valid && si < K) ? cur.lg : 0.f;
-      const float mx = row8_max(si < K ? lgv : -__builtin_inff());
-      const float lse = mx + __logf(row8_sum(si < K ? __expf(lgv - mx) : 0.f));
-      const float f = row8_sum(si < K ? qi * (lgv - lse) : 0.f);
+      const float mx = row_max<KP>(si < K ? lgv : -__builtin_inff());
+      const float lse = mx + __logf(row_sum<KP>(si < K ? __expf(lgv - mx) : 0.f));
+      const float f = row_sum<KP>(si < K ? qi * (lgv - lse) : 0.f);
       if (own && m && si == 0) s_ent -= f;
-      if (grad && own) a.dlx[r * 8 + si] = (m && si < K) ? cent * qi * ((lgv - lse) - f) : 0.f;
+      if (grad && own) a.dlx[r * KP + si] = (m && si < K) ? cent * qi * ((lgv - lse) - f) : 0.f;
     }
     if (own && valid && t == 0 && si < K) {
       s_init = fmaf(qi, lp_i, s_init);
@@ -312,19 +348,19 @@ __global__ __launch_bounds__(256, 2) void elbo_head_k8_kernel(HeadArgs a) {
     lds_barrier();  // dlgS, aS, wS of every row
     // ---------------- B2: dq (lane si = state j), then prefetch the next window's rows
     if (grad && own) {
-      float v = cpri * (wgt * rsj + sh.wS[prow + 1] * sh.aS[(prow + 1) * 8 + si]);
+      float v = cpri * (wgt * rsj + sh.wS[prow + 1] * sh.aS[(prow + 1) * KP + si]);
       if (valid && t == 0) v = fmaf(cpri, lp_i, v);
-      a.dqx[r * 8 + si] = (valid && si < K) ? v : 0.f;
+      a.dqx[r * KP + si] = (valid && si < K) ? v : 0.f;
     }
-    if (w + gridDim.x < nwin) load_row((w + gridDim.x) * K8_WOWN, cur);
+    if (w + gridDim.x < nwin) load_row((w + gridDim.x) * WOWN, cur);
     if (!grad) continue;
     // ---------------- C: MLP backward on this wave's hidden blocks
-    if (wave < KB) {  // db2: column sums of dlg, ij = 16 wave + l16, rows lg4 * 8 ..
+    if (wave < KB) {  // db2: column sums of dlg, ij = 16 wave + l16, rows lg4 * WR / 4 ..
 #pragma unroll
-      for (int k = 0; k < 8; ++k) db2acc += sh.dlgS[(lg4 * 8 + k) * LDL + wave * 16 + l16];
+      for (int k = 0; k < WR / 4; ++k) db2acc += sh.dlgS[(lg4 * (WR / 4) + k) * LDL + wave * 16 + l16];
     }
 #pragma unroll
-    for (int rb = 0; rb < 2; ++rb) {
+    for (int rb = 0; rb < NRB; ++rb) {
       const float ua = lg4 < U ? sh.uS[(rb * 16 + l16) * 8 + lg4] : 0.f;  // u'[row l16][c lg4], c < U
       float dla[SD], dlt[4][KB], ubv[4];
 #pragma unroll
@@ -367,7 +403,8 @@ __global__ __launch_bounds__(256, 2) void elbo_head_k8_kernel(HeadArgs a) {
   double ds[4] = {(double)s_rec, (double)s_init, (double)s_tr, (double)s_ent};
 #pragma unroll
   for (int k = 0; k < 4; ++k) ds[k] = wave_sum_dpp(ds[k]);
-  // q0: lanes of one state si are lane & 7 == si: sum over lane >> 3 (xor 8, 16, 32)
+  // q0: the lanes of one state si are lane % KP == si: sum over lane / KP (xor KP .. 32)
+  if constexpr (KP == 4) q0acc += __shfl_xor(q0acc, 4);
   q0acc += __shfl_xor(q0acc, 8);
   q0acc += xor16(q0acc);
   q0acc += xor32(q0acc);
@@ -377,7 +414,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_k8_kernel(HeadArgs a) {
   if (lane == 0)
 #pragma unroll
     for (int k = 0; k < 4; ++k) sh.red[wave][k] = ds[k];
-  if (lane < 8) sh.q0w[wave][lane] = q0acc;
+  if (lane < KP) sh.q0w[wave][lane] = q0acc;
   __syncthreads();
   if (tid < 4) a.part[blockIdx.x * 4 + tid] = ((sh.red[0][tid] + sh.red[1][tid]) + sh.red[2][tid]) + sh.red[3][tid];
   if (!grad) return;
@@ -404,39 +441,50 @@ __global__ __launch_bounds__(256, 2) void elbo_head_k8_kernel(HeadArgs a) {
   }
 }
 
-bool head_k8_supported(const HeadArgs& a) {
-  return a.K >= 5 && a.K <= 8 && a.U >= 1 && a.U <= 4 && (a.TH == 64 || a.TH == 128 || a.TH == 256) && a.D >= 1 &&
+bool head_coop_supported(const HeadArgs& a) {
+  return a.K >= 1 && a.K <= 8 && a.U >= 1 && a.U <= 4 && (a.TH == 64 || a.TH == 128 || a.TH == 256) && a.D >= 1 &&
          a.D <= 16 && a.R < (1ll << 31);
 }
 
-int head_k8_grid(int64_t R) {
-  const int64_t nwin = cdiv(R, K8_WOWN);
-  return (int)(nwin < 512 ? (nwin > 0 ? nwin : 1) : 512);
+// workgroups (= weight-gradient slabs): one per window up to 512 (2 per CU); VQHMM_HEAD_GRID sets
+// another cap (tuning A/B, read once)
+int head_coop_grid(int64_t R, int K) {
+  static const int cap = [] {
+    const char* e = getenv("VQHMM_HEAD_GRID");
+    const int v = e ? atoi(e) : 0;
+    return v >= 64 && v <= 1024 ? v : 512;
+  }();
+  const int64_t nwin = cdiv(R, K <= 4 ? 63 : 31);
+  return (int)(nwin < cap ? (nwin > 0 ? nwin : 1) : cap);
 }
 
-int launch_head_k8(const HeadArgs& a, int grid, hipStream_t s) {
-  if (!head_k8_supported(a)) return VQHMM_EUNSUPPORTED;
+int launch_head_coop(const HeadArgs& a, int grid, hipStream_t s) {
+  if (!head_coop_supported(a)) return VQHMM_EUNSUPPORTED;
   if (a.R == 0) return VQHMM_OK;
-#define VQHMM_K8(KV, HBWV)                                                                         \
-  {                                                                                                \
-    const size_t lds = sizeof(K8Lds<KV, HBWV>);                                                    \
-    if (a.D <= 8) elbo_head_k8_kernel<KV, HBWV, 8><<<grid, 256, lds, s>>>(a);                      \
-    else elbo_head_k8_kernel<KV, HBWV, 16><<<grid, 256, lds, s>>>(a);                              \
+#define VQHMM_HC(KV, HBWV, KPV)                                                                      \
+  {                                                                                                  \
+    const size_t lds = sizeof(CoopLds<KV, HBWV, KPV>);                                               \
+    if (a.D <= 8) elbo_head_coop_kernel<KV, HBWV, 8, KPV><<<grid, 256, lds, s>>>(a);                 \
+    else elbo_head_coop_kernel<KV, HBWV, 16, KPV><<<grid, 256, lds, s>>>(a);                         \
   }
-#define VQHMM_K8_TH(KV)                      \
-  switch (a.TH) {                            \
-    case 64: VQHMM_K8(KV, 1) break;          \
-    case 128: VQHMM_K8(KV, 2) break;         \
-    default: VQHMM_K8(KV, 4) break;          \
+#define VQHMM_HC_TH(KV, KPV)                  \
+  switch (a.TH) {                             \
+    case 64: VQHMM_HC(KV, 1, KPV) break;      \
+    case 128: VQHMM_HC(KV, 2, KPV) break;     \
+    default: VQHMM_HC(KV, 4, KPV) break;      \
   }
   switch (a.K) {
-    case 5: VQHMM_K8_TH(5) break;
-    case 6: VQHMM_K8_TH(6) break;
-    case 7: VQHMM_K8_TH(7) break;
-    default: VQHMM_K8_TH(8) break;
+    case 1: VQHMM_HC_TH(1, 4) break;
+    case 2: VQHMM_HC_TH(2, 4) break;
+    case 3: VQHMM_HC_TH(3, 4) break;
+    case 4: VQHMM_HC_TH(4, 4) break;
+    case 5: VQHMM_HC_TH(5, 8) break;
+    case 6: VQHMM_HC_TH(6, 8) break;
+    case 7: VQHMM_HC_TH(7, 8) break;
+    default: VQHMM_HC_TH(8, 8) break;
   }
-#undef VQHMM_K8_TH
-#undef VQHMM_K8
+#undef VQHMM_HC_TH
+#undef VQHMM_HC
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
 }

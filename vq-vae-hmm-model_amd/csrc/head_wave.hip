@@ -558,9 +558,16 @@ static int head_wave_nbw(int64_t R) {
   return R >= 98304 ? 4 : R >= 32768 ? 2 : 1;
 }
 
+// workgroups (= weight-gradient slabs the tail reduces): up to 512 (2 per CU); VQHMM_HEAD_GRID caps it
+// lower (tuning A/B, read once)
 int head_wave_grid(int64_t R) {
+  static const int cap = [] {
+    const char* e = getenv("VQHMM_HEAD_GRID");
+    const int v = e ? atoi(e) : 0;
+    return v >= 64 && v <= 512 ? v : 512;
+  }();
   const int64_t nwin = cdiv(R, 16 * head_wave_nbw(R) - 1);
-  return (int)(nwin < 512 ? (nwin > 0 ? nwin : 1) : 512);
+  return (int)(nwin < cap ? (nwin > 0 ? nwin : 1) : cap);
 }
 
 template <int NBW>

@@ -234,6 +234,8 @@ struct WgradGroup {
   int njobs;
 };
 bool wgrad2_group_supported(const WgradArgs& a);
+// a grouped job's rows per chunk (a multiple of its stage rows: 64, or 192 for the small outputs)
+int64_t wgrad2_group_rows(int64_t rows, int N, int C, int ks);
 int launch_wgrad2_group(const WgradArgs* jobs, int n, hipStream_t s);
 // Staged ELBO head (head_staged.hip): shapes the fused heads do not cover.
 struct StagedHeadArgs {
@@ -264,10 +266,11 @@ int head_wave_grid(int64_t R);
 int launch_head_wave(const HeadArgs& a, int grid, hipStream_t s);
 bool head_mfma_supported(const HeadArgs& a);
 int launch_head_mfma(const HeadArgs& a, int grid, hipStream_t s);
-// 5 <= K <= 8 MFMA head (head_k8.hip): U <= 4, TH in {64, 128, 256}, D <= 16; its grid / slab count
-bool head_k8_supported(const HeadArgs& a);
-int head_k8_grid(int64_t R);
-int launch_head_k8(const HeadArgs& a, int grid, hipStream_t s);
+// workgroup-cooperative MFMA head (head_coop.hip): K <= 8, U <= 4, TH in {64, 128, 256}, D <= 16; its
+// grid / slab count
+bool head_coop_supported(const HeadArgs& a);
+int head_coop_grid(int64_t R, int K);
+int launch_head_coop(const HeadArgs& a, int grid, hipStream_t s);
 int launch_head(const HeadArgs& a, int grid, hipStream_t s);
 int launch_prior_fwd(const PriorArgs& p, hipStream_t s);
 // Prior.forward on MFMA (prior.hip): K*K <= 64, U <= 4, TH in {64, 128, 256}

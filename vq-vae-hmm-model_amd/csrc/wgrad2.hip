@@ -21,19 +21,27 @@
 namespace vqhmm {
 
 namespace {
-constexpr int RT = 64;  // rows per stage
+constexpr int RT = 64;     // rows per stage (the output-heavy jobs)
+constexpr int RT_S = 96;   // rows per stage of the small jobs (< 4096 outputs: MFMA work per 64-row stage is
+                           // a few dozen MFMAs per wave, so the stage's loads, stores and two barriers set
+                           // the time; 1.5x the rows, 2/3 of the stages: 128 or more push the group kernel
+                           // past 256 registers, i.e. to one wave per SIMD)
+constexpr int RT_S4 = 128;  // ... for the 4-row-wave body (its 16-row slices must split evenly over 4 waves)
 }
 
 // LDS floats of one wgrad2 body: dY stage, X stage, bias partials, row-wave exchange
-template <int NPAD, int CPAD>
-constexpr int w2_lds_floats() { return RT * (NPAD + 4) + (RT + 2) * (CPAD + 4) + 256 + 1536; }
-constexpr int W2_LDS_MAX = RT * 68 + (RT + 2) * 68 + 256 + 1536;
+template <int NPAD, int CPAD, int RTV = RT>
+constexpr int w2_lds_floats() { return RTV * (NPAD + 4) + (RTV + 2) * (CPAD + 4) + 256 + 1536; }
+constexpr int w2_max(int a, int b) { return a > b ? a : b; }
+// the group launch's dynamic LDS: the largest body (64x64 at RT, 16x64 / 64x16 small jobs at RT_S)
+constexpr int W2_LDS_MAX = w2_max(w2_max(w2_lds_floats<64, 64>(), w2_lds_floats<16, 16, RT_S4>()),
+                                  w2_max(w2_lds_floats<16, 64, RT_S>(), w2_lds_floats<64, 16, RT_S>()));
 
 // One chunk (workgroup) of the split-K weight gradient; smem = w2_lds_floats<NPAD, CPAD>() floats.
 // PK (k = 3, 3*C <= 16): the three taps share ONE 16-wide MFMA column block, column j = tap*C + c
 // (a per-lane gather from the X stage), so a narrow-input layer (enc_conv1 C = 5, the composed
 // decoder conv1 C = K = 3) issues a third of the MFMAs of the tap-major form.
-template <int NBW, int CBW, int KS, int NPAD, int CPAD, int WR, bool PK = false>
+template <int NBW, int CBW, int KS, int NPAD, int CPAD, int WR, bool PK = false, int RT = vqhmm::RT>
 __device__ __forceinline__ void wgrad2_body(const WgradArgs& a, int WN, int WC, int64_t chunk, float* smem) {
   static_assert(!PK || (KS == 3 && CBW == 1), "packed taps: k = 3, one column block");
   constexpr int KA = PK ? 1 : KS;  // accumulator tap blocks
@@ -140,7 +148,8 @@ __device__ __forceinline__ void wgrad2_body(const WgradArgs& a, int WN, int WC, 
     // this wave's 16-row slices of the stage, as 4 * (4 / WR) MFMA steps (one row per lane group
     // each): the operands of step s + 1 are read from LDS while the MFMAs of step s run (two
     // register sets, sched_barrier keeps the reads ahead); each accumulator's chain is unchanged
-    constexpr int NST = 4 * (4 / WR);
+    static_assert((RT / 16) % WR == 0 && RT % 16 == 0, "a stage's 16-row slices split evenly over the row-waves");
+    constexpr int NST = 4 * ((RT / 16) / WR);
     float av[2][NBW], bv[2][KA][CBW];
     auto load = [&](int st, float (&a_)[NBW], float (&b_)[KA][CBW]) {
       const int sl = wr + (st >> 2) * WR, e = st & 3;
@@ -258,19 +267,20 @@ __global__ __launch_bounds__(256) void wgrad2_kernel(WgradArgs a, int WN, int WC
 // b - blk0[j] of job j.  Each job is one of the launch shapes below (variant id = its row in
 // w2_variant, +10 for k = 3), so every body keeps its own register/LDS layout; big jobs come
 // first so their workgroups start first and the small ones fill the tail.
-#define VQHMM_W2_VARIANTS(KSV, O)                                     \
-  case O + 0: wgrad2_body<4, 1, KSV, 64, 64, 1>(a, WN, WC, ch, sm); break; \
-  case O + 1: wgrad2_body<2, 1, KSV, 32, 64, 1>(a, WN, WC, ch, sm); break; \
-  case O + 2: wgrad2_body<1, 2, KSV, 64, 32, 1>(a, WN, WC, ch, sm); break; \
-  case O + 3: wgrad2_body<1, 1, KSV, 16, 64, 1>(a, WN, WC, ch, sm); break; \
-  case O + 4: wgrad2_body<1, 1, KSV, 64, 16, 1>(a, WN, WC, ch, sm); break; \
-  case O + 5: wgrad2_body<1, 1, KSV, 16, 32, 2>(a, WN, WC, ch, sm); break; \
-  case O + 6: wgrad2_body<1, 1, KSV, 32, 16, 2>(a, WN, WC, ch, sm); break; \
-  case O + 7: wgrad2_body<1, 1, KSV, 32, 32, 1>(a, WN, WC, ch, sm); break; \
-  case O + 8: wgrad2_body<1, 1, KSV, 16, 16, 4>(a, WN, WC, ch, sm); break;
+#define VQHMM_W2_VARIANTS(KSV, O)                                                   \
+  case O + 0: wgrad2_body<4, 1, KSV, 64, 64, 1>(a, WN, WC, ch, sm); break;               \
+  case O + 1: wgrad2_body<2, 1, KSV, 32, 64, 1>(a, WN, WC, ch, sm); break;               \
+  case O + 2: wgrad2_body<1, 2, KSV, 64, 32, 1>(a, WN, WC, ch, sm); break;               \
+  case O + 3: wgrad2_body<1, 1, KSV, 16, 64, 1, false, RT_S>(a, WN, WC, ch, sm); break;  \
+  case O + 4: wgrad2_body<1, 1, KSV, 64, 16, 1, false, RT_S>(a, WN, WC, ch, sm); break;  \
+  case O + 5: wgrad2_body<1, 1, KSV, 16, 32, 2, false, RT_S>(a, WN, WC, ch, sm); break;  \
+  case O + 6: wgrad2_body<1, 1, KSV, 32, 16, 2, false, RT_S>(a, WN, WC, ch, sm); break;  \
+  case O + 7: wgrad2_body<1, 1, KSV, 32, 32, 1, false, RT_S>(a, WN, WC, ch, sm); break;  \
+  case O + 8: wgrad2_body<1, 1, KSV, 16, 16, 4, false, RT_S4>(a, WN, WC, ch, sm); break;
 
 __global__ __launch_bounds__(256) void wgrad2_group_kernel(WgradGroup g) {
-  __shared__ float sm[W2_LDS_MAX];
+  extern __shared__ float4 smem4[];
+  float* sm = reinterpret_cast<float*>(smem4);  // W2_LDS_MAX floats
   int j = 0;
   while (j + 1 < g.njobs && (int64_t)blockIdx.x >= g.blk0[j + 1]) ++j;
   const WgradArgs& a = g.job[j];
@@ -279,7 +289,7 @@ __global__ __launch_bounds__(256) void wgrad2_group_kernel(WgradGroup g) {
   switch (g.variant[j]) {
     VQHMM_W2_VARIANTS(1, 0)
     VQHMM_W2_VARIANTS(3, 10)
-    case 20: wgrad2_body<1, 1, 3, 64, 16, 1, true>(a, WN, WC, ch, sm); break;
+    case 20: wgrad2_body<1, 1, 3, 64, 16, 1, true, RT_S>(a, WN, WC, ch, sm); break;
     default: break;
   }
 }
@@ -313,6 +323,20 @@ static int w2_variant(int N, int C, int ks, int* WN, int* WC) {
   return v + (ks == 3 ? 10 : 0);
 }
 
+// rows per stage of a job in the grouped launch (variants 0..2 and 10..12 are the output-heavy bodies)
+static int w2_group_rt(int variant) {
+  const int v = variant % 10;
+  return (variant < 20 && v <= 2) ? RT : (variant < 20 && v == 8) ? RT_S4 : RT_S;
+}
+
+// a grouped job's rows per chunk: `rows` rounded up to its stage size
+int64_t wgrad2_group_rows(int64_t rows, int N, int C, int ks) {
+  int wn, wc;
+  const int v = w2_variant(N, C, ks, &wn, &wc);
+  const int rt = v < 0 ? RT : w2_group_rt(v);
+  return cdiv(rows, rt) * rt;
+}
+
 bool wgrad2_group_supported(const WgradArgs& a) {
   int wn, wc;
   return !a.x_cf && a.N <= 64 && a.C <= 64 && (a.ks == 1 || a.ks == 3) && w2_variant(a.N, a.C, a.ks, &wn, &wc) >= 0;
@@ -337,14 +361,15 @@ int launch_wgrad2_group(const WgradArgs* jobs, int n, hipStream_t s) {
   g.blk0[0] = 0;
   for (int i = 0; i < n; ++i) {
     const WgradArgs& a = jobs[ord[i]];
-    if (!wgrad2_group_supported(a) || a.rows_per_chunk % RT) return VQHMM_EINVAL;
+    if (!wgrad2_group_supported(a)) return VQHMM_EINVAL;
     g.job[i] = a;
     g.job[i].pipe = pipe;
     g.variant[i] = w2_variant(a.N, a.C, a.ks, &g.wn[i], &g.wc[i]);
+    if (a.rows_per_chunk % w2_group_rt(g.variant[i])) return VQHMM_EINVAL;
     g.blk0[i + 1] = g.blk0[i] + cdiv(a.R, a.rows_per_chunk);
   }
   if (g.blk0[n] == 0) return VQHMM_OK;
-  wgrad2_group_kernel<<<(unsigned)g.blk0[n], 256, 0, s>>>(g);
+  wgrad2_group_kernel<<<(unsigned)g.blk0[n], 256, W2_LDS_MAX * sizeof(float), s>>>(g);
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
 }
