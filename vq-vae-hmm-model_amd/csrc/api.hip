@@ -113,6 +113,9 @@ struct ElboPlan {
 void plan_images(ElboPlan& p, Carver& c);
 
 ElboPlan plan_elbo(const vqhmm_dims_t* d, int64_t B, int64_t T, void* ws) {
+  // size / shape queries: carve from a non-null base (kernel choices test pointers for presence;
+  // nothing is dereferenced), so the plan is exactly the one a real workspace gets
+  if (!ws) return plan_elbo(d, B, T, reinterpret_cast<void*>(4096));
   ElboPlan p{};
   p.B = B; p.T = (int)T; p.R = B * (T + 2);
   p.D = d->input_dim; p.H = d->hidden_dim; p.H2 = d->hidden_dim2; p.K = d->K; p.U = d->u_dim; p.TH = d->trans_hidden;
@@ -634,6 +637,18 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       wgrad_jobs(p, wa);
       if (p.wgroup) {  // all six in S_W_ENC1's launch (every dY is ready by then, in any stage order)
         if (st != S_W_ENC1) return VQHMM_OK;
+        // timing experiment only (gradients are then incomplete): VQHMM_WGRAD_JOBMASK bit i keeps job i
+        static const int jmask = [] {
+          const char* e = getenv("VQHMM_WGRAD_JOBMASK");
+          return e ? atoi(e) : 63;
+        }();
+        if (jmask != 63) {
+          WgradArgs sel[6];
+          int n = 0;
+          for (int i = 0; i < 6; ++i)
+            if (jmask >> i & 1) sel[n++] = wa[i];
+          return n ? launch_wgrad2_group(sel, n, s) : VQHMM_OK;
+        }
         return launch_wgrad2_group(wa, 6, s);
       }
       return launch_wgrad(wa[st - S_W_PAR], s);
