@@ -150,7 +150,7 @@ import sys, torch
 sys.path.insert(0, sys.argv[1])
 import vqhmm
 D, H, K, H2 = (int(v) for v in sys.argv[3].split(","))
-B, T = 96, 150
+B, T = (int(v) for v in sys.argv[4].split(",")) if len(sys.argv) > 4 else (96, 150)
 gen = torch.Generator().manual_seed(5)
 x = torch.randn(B, D, T, generator=gen).cuda()
 u = torch.randn(B, 4, T, generator=gen).cuda()
@@ -170,7 +170,7 @@ torch.save({"grad": st.grad.cpu(), "flat": st.flat.cpu(), "m": st.exp_avg.cpu(),
 """
 
 
-def _run_both(tmp_path, env, dims):
+def _run_both(tmp_path, env, dims, bt=(96, 150)):
     """The same 4 steps in two fresh processes, env=1 and env=0 (the switches are read once per
     process); loss, gradient, moments and parameters must agree bit for bit."""
     import os
@@ -181,7 +181,8 @@ def _run_both(tmp_path, env, dims):
     out = {}
     for flag in ("1", "0"):
         f = str(tmp_path / f"{env}{flag}.pt")
-        subprocess.run([sys.executable, "-c", _SPLIT_RUN, pkg, f, ",".join(map(str, dims))], check=True,
+        subprocess.run([sys.executable, "-c", _SPLIT_RUN, pkg, f, ",".join(map(str, dims)), ",".join(map(str, bt))],
+                       check=True,
                        timeout=300, env=dict(os.environ, **{env: flag}))
         out[flag] = torch.load(f, weights_only=True)
     for k in ("grad", "flat", "m", "v", "loss"):
@@ -199,6 +200,14 @@ def test_fused_conv_pairs_match_separate_launches(tmp_path, dims):
     """enc_conv1 -> enc_conv2 and dec_conv1 -> dec_conv2 fused into one launch each (conv2f_kernel:
     14-row tiles, the front rows computed in-tile) against the two-launch path (VQHMM_CONV_FUSE=0)."""
     _run_both(tmp_path, "VQHMM_CONV_FUSE", dims)
+
+
+@pytest.mark.parametrize("dims,bt", [((5, 64, 3, 32), (96, 150)), ((4, 64, 4, 16), (40, 77)), ((3, 64, 2, 32), (8, 50)),
+                                     ((5, 64, 3, 32), (256, 150))])  # 319 strips: workgroups run 2
+def test_strip_forward_matches_pair_launches(tmp_path, dims, bt):
+    """The four forward convolutions as ONE strip launch (strip.hip: 128-row windows, 3 recomputed
+    halo rows a side, activations in LDS) against the pair launches (VQHMM_STRIP=0): same bits."""
+    _run_both(tmp_path, "VQHMM_STRIP", dims, bt)
 
 
 def test_tail_rerun_after_one_forward_is_identical():

@@ -1,0 +1,45 @@
+"""Phase timings of the strip kernel (strip.hip, VQHMM_STRIP_PROF=1 builds its profiling variant):
+per-workgroup s_memrealtime stamps (100 MHz) of the first strip's phases, medians over workgroups.
+usage: VQHMM_STRIP_PROF=1 python tools/strip_prof.py [B ...]"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "vq-vae-hmm-model_amd"))
+import vqhmm  # noqa: E402
+from vqhmm import _ext  # noqa: E402
+
+NAMES = ["staging", "x->LDS", "enc_conv1", "enc_conv2+logits", "dec_conv1", "dec_conv2+params", "other strips"]
+
+
+def run(B, T=200, D=5, H=64, K=3, H2=32):
+    gen = torch.Generator().manual_seed(0)
+    x = torch.randn(B, D, T, generator=gen).cuda()
+    u = torch.randn(B, 4, T, generator=gen).cuda()
+    L = torch.full((B,), T, dtype=torch.int64)
+    torch.manual_seed(0)
+    m = vqhmm.VAE_HMM(D, H, K, H2, u_dim=4, trans_hidden=128).cuda()
+    st = vqhmm.TrainState(m, lr=1e-3)
+    xs, us, Ls = st.prepare(x, u, L)
+    for _ in range(5):
+        st.forward_backward(xs, us, Ls, 1.0)
+    torch.cuda.synchronize()
+    buf = np.zeros(256 * 16, dtype=np.uint64)
+    _ext.check(_ext.load().vqhmm_debug_prof(buf.ctypes.data_as(ctypes.c_void_p), buf.size), "debug_prof")
+    t = buf.reshape(256, 16).astype(np.int64)
+    used = t[:, 8] > 0
+    t = t[used]
+    d = np.diff(t[:, :8], axis=1) * 10 / 1000.0  # us
+    t0 = t[:, 0].min()
+    print(f"B={B}: {used.sum()} workgroups, strips/wg {t[:, 8].min()}..{t[:, 8].max()}, "
+          f"kernel span {(t[:, 7].max() - t0) * 0.01:.2f} us, start skew {(t[:, 0].max() - t0) * 0.01:.2f} us")
+    for i, n in enumerate(NAMES):
+        print(f"  {n:18s} median {np.median(d[:, i]):7.2f}  max {d[:, i].max():7.2f} us")
+
+
+if __name__ == "__main__":
+    for b in (sys.argv[1:] or ["128", "1024"]):
+        run(int(b))

@@ -517,6 +517,17 @@ bool front_fused(const ElboPlan& p, const float* const* w, int st) {
   return on && (st == S_ENC2 || st == S_DEC2 || st == S_DEC2_DG) && conv2_fused_supported(fused_pair(p, w, st));
 }
 
+// The four forward convolutions as one strip launch (strip.hip) where its shapes apply; VQHMM_STRIP=0
+// keeps the two pair launches (A/B), read once
+bool strip_fwd_on(const ElboPlan& p) {
+  static const bool on = [] {
+    const char* e = getenv("VQHMM_STRIP");
+    return !e || atoi(e) != 0;
+  }();
+  return on && strip_fwd_supported(conv_of(p, nullptr, S_ENC1), conv_of(p, nullptr, S_ENC2),
+                                   conv_of(p, nullptr, S_DEC1), conv_of(p, nullptr, S_DEC2));
+}
+
 // dec_conv1's data gradient with, for K <= 4, the softmax backward (+ to_logits' dgrad) in its epilogue
 ConvArgs dec1_dg_args(const ElboPlan& p, const float* const* w, const float* gscale) {
   static const float* const kNull[VQHMM_NPARAMS] = {};
@@ -581,9 +592,14 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
     case S_COMPOSE:  // runs inside S_TOPCL's launch
       return VQHMM_OK;
     case S_ENC1: case S_DEC1:
+      if (strip_fwd_on(p)) return VQHMM_OK;            // in S_ENC2's strip launch
       if (front_fused(p, w, st + 1)) return VQHMM_OK;  // runs inside the next conv's launch
       return launch_conv(conv_of(p, w, st), s);
     case S_ENC2: case S_DEC2:
+      if (strip_fwd_on(p))
+        return st == S_DEC2 ? VQHMM_OK
+                            : launch_strip_fwd(conv_of(p, w, S_ENC1), conv_of(p, w, S_ENC2), conv_of(p, w, S_DEC1),
+                                               conv_of(p, w, S_DEC2), s);
       if (front_fused(p, w, st)) return launch_conv2_fused(fused_pair(p, w, st), s);
       return launch_conv(conv_of(p, w, st), s);
     case S_DEC2_DG:
@@ -790,11 +806,17 @@ int vqhmm_elbo_stage_info(const vqhmm_dims_t* d, int64_t B, int64_t T, int stage
   const bool fused_front = (pair_of == S_ENC2 || pair_of == S_DEC2 || pair_of == S_DEC2_DG) &&
                            front_fused(plan_elbo(d, B, T, reinterpret_cast<void*>(4096)), nullptr, pair_of);
   const bool bwd_pair = bwd_pair_fused(plan_elbo(d, B, T, reinterpret_cast<void*>(4096)), nullptr, nullptr);
+  const bool strip = strip_fwd_on(plan_elbo(d, B, T, reinterpret_cast<void*>(4096)));
+  const bool in_strip = strip && (stage == S_ENC1 || stage == S_ENC2 || stage == S_DEC1 || stage == S_DEC2);
   if (name && name_len) {
     const char* nm = kStageNames[stage];
+    if (in_strip)
+      nm = stage == S_ENC2 ? "strip_fwd(enc_conv1+enc_conv2+to_logits+dec_conv1+dec_conv2+to_params)"
+                           : "(in strip_fwd)";
     if (p.wgroup && stage == S_W_ENC1) nm = "wgrad_group(all 6 weight gradients)";
     else if (p.wgroup && stage >= S_W_PAR && stage < S_W_ENC1) nm = "(wgrad: in wgrad_group)";
-    else if (fused_front && (stage == S_ENC1 || stage == S_DEC1 || stage == S_PAR_DG))
+    else if (in_strip) {
+    } else if (fused_front && (stage == S_ENC1 || stage == S_DEC1 || stage == S_PAR_DG))
       nm = stage == S_ENC1 ? "(enc_conv1: in enc_conv2's launch)"
            : stage == S_DEC1 ? "(dec_conv1: in dec_conv2's launch)" : "(to_params_dgrad: in dec_conv2_dgrad's launch)";
     else if (fused_front && stage == S_ENC2) nm = "enc_conv1+enc_conv2+to_logits";
@@ -812,7 +834,19 @@ int vqhmm_elbo_stage_info(const vqhmm_dims_t* d, int64_t B, int64_t T, int stage
   double f, b;
   int m;
   stage_work(p, stage, &f, &b, &m);
-  if (fused_front && pair_of != stage) {
+  if (in_strip) {  // S_ENC2's launch does all four; HBM sees x in and every activation out once
+    f = 0; b = 0;
+    if (stage == S_ENC2) {
+      for (int st2 : {S_ENC1, S_ENC2, S_DEC1, S_DEC2}) {
+        double f1, b1;
+        int m1;
+        stage_work(p, st2, &f1, &b1, &m1);
+        f += f1;
+      }
+      const double R = (double)p.R;
+      b = 4.0 * R * (ld4(p.D) + ld4(p.H) + ld4(p.H2) + 2 * ld4(p.K) + 2 * ld4(p.H) + ld4(2 * p.D));
+    }
+  } else if (fused_front && pair_of != stage) {
     f = 0; b = 0;  // counted with the launch it runs in
   } else if (fused_front) {
     double f1, b1;

@@ -219,6 +219,11 @@ __host__ __device__ inline int64_t c2_image_floats(int N, int Kc, int ks) {
   return (int64_t)ks * 16 * c2_nb(N) * c2_ldx(Kc);
 }
 int launch_conv2(const ConvArgs& a, hipStream_t s);
+// Forward strip kernel (strip.hip): enc_conv1 -> enc_conv2 + to_logits + softmax -> composed dec_conv1
+// -> dec_conv2 + to_params in ONE launch over 128-row strips, the activations between layers in LDS
+// (the four ConvArgs of the separate launches; packed-tap fronts, H = 64, H2 <= 32, K <= 4, 2D <= 16)
+bool strip_fwd_supported(const ConvArgs& e1, const ConvArgs& e2, const ConvArgs& d1, const ConvArgs& d2);
+int launch_strip_fwd(const ConvArgs& e1, const ConvArgs& e2, const ConvArgs& d1, const ConvArgs& d2, hipStream_t s);
 int launch_wgrad(const WgradArgs& a, hipStream_t s);
 int64_t wgrad_chunks(int64_t R, int64_t tiles);
 bool wgrad2_supported(const WgradArgs& a);
