@@ -12,7 +12,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import vqhmm  # noqa: E402
 from vqhmm import _ext  # noqa: E402
 
-NAMES = ["staging", "x->LDS", "enc_conv1", "enc_conv2+logits", "dec_conv1", "dec_conv2+params", "other strips"]
+NAMES = ["staging", "enc_conv1+enc_conv2+logits", "dec_conv1+dec_conv2+params", "-", "-", "-", "other strips"]
 
 
 def run(B, T=200, D=5, H=64, K=3, H2=32):
@@ -32,12 +32,20 @@ def run(B, T=200, D=5, H=64, K=3, H2=32):
     t = buf.reshape(256, 16).astype(np.int64)
     used = t[:, 8] > 0
     t = t[used]
+    w0 = t[:, [2, 4, 5, 6, 3]].astype(np.int64)  # wave 0 in the second phase: start, front, loop, tail, barrier
+    t[:, 4:7] = t[:, 3:4]  # stamps 0, 1, 2, 3, 7
     d = np.diff(t[:, :8], axis=1) * 10 / 1000.0  # us
     t0 = t[:, 0].min()
     print(f"B={B}: {used.sum()} workgroups, strips/wg {t[:, 8].min()}..{t[:, 8].max()}, "
           f"kernel span {(t[:, 7].max() - t0) * 0.01:.2f} us, start skew {(t[:, 0].max() - t0) * 0.01:.2f} us")
     for i, n in enumerate(NAMES):
-        print(f"  {n:18s} median {np.median(d[:, i]):7.2f}  max {d[:, i].max():7.2f} us")
+        if n != "-":
+            print(f"  {n:28s} median {np.median(d[:, i]):7.2f}  max {d[:, i].max():7.2f} us")
+    dw = np.median(np.diff(w0, axis=1), axis=0) * 0.01
+    print("  wave 0, second phase: front %.2f, dec_conv2 loop %.2f, tail %.2f, to barrier %.2f us" % tuple(dw))
+    if t[:, 9].max() > 0:  # VQHMM_STRIP_PROF=2: serialised latency probes from the kernel's start
+        for k, n in ((9, "x load"), (10, "+ constants"), (11, "+ front weights"), (12, "+ image DMA")):
+            print(f"  {n:18s} at {np.median(t[:, k] - t[:, 0]) * 0.01:7.2f} us")
 
 
 if __name__ == "__main__":

@@ -1,17 +1,19 @@
 // Strip kernels: several convolution layers of the training step in ONE launch, the activations
 // between the layers kept in LDS (VQ_VAE_HMM_fixed.py:38-41 Encoder.forward, :80-90 Decoder.forward).
 //
-// A strip is a window of ST_WIN = 128 consecutive PCL rows whose middle ST_OWN = 122 rows it owns.
-// Each layer is computed on the whole window (one 16-row MFMA block per wave, 8 waves), so a k = 3
-// layer's output is exact one row further inside the window than its input; the forward chain
-//   x -> enc_conv1 -> enc_conv2 (+ to_logits, softmax) -> composed dec_conv1 -> dec_conv2 (+ to_params)
-// has four k = 3 layers and an LDS input of ST_WIN + 2 rows, so rows >= ST_HALO = 3 from the window
-// edges are exact at the end: the strip stores exactly those (owned rows tile [0, R) without overlap).
-// No workgroup ever waits for another; the 2.5% of recomputed rows replace four launches' fixed
-// costs (weight staging, the first tile's latency, the tail) with one, which is what bounds the
-// step at the strong-scaling shard sizes (B = 128 per GPU).
+// A strip is a window of ST_WIN = 128 consecutive PCL rows whose middle ST_OWN = 124 rows it owns
+// (owned rows tile [0, R) without overlap).  Wave w of the 8-wave workgroup owns the window's
+// 16-row block w through the whole chain
+//   x -> enc_conv1 -> enc_conv2 (+ to_logits, softmax) -> composed dec_conv1 -> dec_conv2 (+ to_params).
+// The narrow front convs (enc_conv1 on x, dec_conv1 on q: packed taps, 16 MFMAs a block) are computed
+// by the wave itself for the 18 rows its 64-wide conv reads (two overlapping MFMA blocks) into its own
+// LDS slot, so only q (and the next strip's x) cross waves: two workgroup barriers per strip.  The
+// window's outer rows are inexact after the k = 3 layers (x is loaded with a 2-row halo), so a strip
+// stores rows >= ST_HALO = 2 from its edges only: 3% recomputed rows replace four launches' fixed
+// costs (weight staging, the first tile's latency, the tail) with one — what bounds the step at the
+// strong-scaling shard sizes (B = 128 per GPU).
 //
-// Every row goes through the fused-pair launches' MFMA sequences and epilogue (conv2_dev.h), so
+// Every row goes through the pair launches' MFMA sequences and epilogue arithmetic (conv2_dev.h), so
 // the stored activations are the same bits as the conv2f path (tests: strip = pair launches).
 #include "vqhmm.h"
 
@@ -22,21 +24,35 @@
 
 namespace vqhmm {
 
+struct StripFwdArgs {
+  int64_t R;
+  int T, D, H2, K, P;  // P = 2D (to_params outputs)
+  const float* xp;     // PCL x (R, ld4(D))
+  const float *img_e1, *img_d1;  // packed-front images [3][64][24] (the prologue's)
+  const float *img_e2, *img_d2;  // enc_conv2 [3][16 NB2][72] / dec_conv2 [3][64][72] images
+  const float *b_e1, *b_e2, *b_d1, *b_d2;
+  const float *tWl, *tbl;        // to_logits (K, H2), (K)
+  const float *tWp, *tbp;        // to_params (P, 64), (P)
+  float *h1e, *h2e, *logits, *q, *g1, *g2, *par;
+  int64_t nstrip;
+  int dbg;  // profiling experiments (VQHMM_STRIP_DBG, read once; results then invalid): 1 = no global stores
+};
+
 namespace {
 constexpr int ST_WIN = 128;                    // window rows: 8 MFMA row blocks, one per wave
-constexpr int ST_HALO = 3;                     // recomputed rows on each side
+constexpr int ST_HALO = 2;                     // inexact rows on each side
 constexpr int ST_OWN = ST_WIN - 2 * ST_HALO;   // rows a strip stores
-constexpr int ST_SR = ST_WIN + 2;              // LDS rows of a layer input (the k = 3 halo)
-constexpr int ST_XLD = 8;                      // row stride of the narrow buffers (x, q)
-constexpr int ST_LDW = 72;                     // c2_ldx(64): 64-channel buffers and weight images
-constexpr int ST_LDF = 24;                     // c2_ldx(<= 16): the narrow layers' weight images
+constexpr int ST_XR = ST_WIN + 4;              // rows of the shared x / q buffers (s0 - 2 .. s0 + 129)
+constexpr int ST_XLD = 8;                      // their row stride
+constexpr int ST_LDW = 72;                     // c2_ldx(64): 64-channel slots and weight images
+constexpr int ST_LDF = 24;                     // the prologue's packed-front image row stride
 
 // profiling builds (VQHMM_STRIP_PROF=1, read once): s_memrealtime stamps of workgroup w's phases in
 // g_prof[w * 16 + k] (vqhmm_debug_prof); results unchanged
 __device__ unsigned long long g_prof[256 * 16];
-template <bool PROF>
+template <int PROF>
 __device__ __forceinline__ void stamp(int k) {
-  if constexpr (PROF) {
+  if constexpr (PROF > 0) {
     if (threadIdx.x == 0 && blockIdx.x < 256) g_prof[blockIdx.x * 16 + k] = __builtin_amdgcn_s_memrealtime();
   }
 }
@@ -44,32 +60,44 @@ __device__ __forceinline__ void stamp(int k) {
 template <int NB2>
 struct StripFwdLds {
   static constexpr int NW2 = 16 * NB2;
-  float We2[3 * NW2 * ST_LDW];  // enc_conv2 image (the prologue's, [tap][n][c])
+  float We2[3 * NW2 * ST_LDW];  // enc_conv2 image
   float Wd2[3 * 64 * ST_LDW];   // dec_conv2 image
-  float Ee2[NW2 * 17 + 16];     // enc_conv2 bias | to_logits weight | bias (c2_tail_consts layout)
-  float Ed2[64 * 17 + 16];      // dec_conv2 bias | to_params weight | bias
-  float bf[2][64];              // enc_conv1 / composed dec_conv1 bias
-  float XA[ST_SR * ST_XLD];     // x rows, then q rows
-  float XB[ST_SR * ST_LDW];     // h1 rows, then g1 rows
+  float Wf[2][3 * 64 * 8];      // enc_conv1 / dec_conv1 images, channels 0..7 ([tap][n][8])
+  float Ee2[NW2 * 17 + 16];     // enc_conv2 bias | to_logits weight (16 x NW2) | bias
+  float Ed2[64 * 17 + 16];      // dec_conv2 bias | to_params weight (16 x 64) | bias
+  float bf[2][64];              // enc_conv1 / dec_conv1 bias
+  float Xx[ST_XR * ST_XLD];     // x rows s0 - 2 .. s0 + 129
+  float Xq[ST_XR * ST_XLD];     // q rows s0 - 2 .. s0 + 129 (the 2 + 2 outer rows stay zero)
+  float slot[8][18 * ST_LDW];   // per wave: the 64-wide conv's 18 input rows rb - 1 .. rb + 16
 };
 
-// A packed-tap front conv's weights as c2_mfma_pk gathers them from its image, held in registers
-// for the whole launch: w[nb][e] = image value of k-column 4 lg4 + e, output channel nb*16 + l16.
-__device__ __forceinline__ void pk_weights(const float* img, int C, int lg4, int l16, float (&w)[4][4]) {
+// row_bt's validity test with 32-bit arithmetic (R < 2^31): PCL row r is a sequence position
+__device__ __forceinline__ bool row_valid(int64_t r, int64_t R, int T) {
+  if (r < 0 || r >= R) return false;
+  const unsigned Tp = (unsigned)T + 2u, m = (unsigned)r % Tp;
+  return m >= 1u && m <= (unsigned)T;
+}
+
+// A packed-tap front's weights as c2_mfma_pk gathers them (k-column 4 lg4 + e, channel nb*16 + l16),
+// from the compact [tap][n][8] LDS image into registers for the whole launch; columns past 3C are 0
+__device__ __forceinline__ void pk_weights(const float* Wf, int C, int lg4, int l16, float (&w)[4][4]) {
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int k = 4 * lg4 + e;
     const bool in = k < 3 * C;
-    const int tap = in ? k / C : 0, c = in ? k - tap * C : 15;
+    const int tap = in ? k / C : 0, c = in ? k - tap * C : 0;
 #pragma unroll
-    for (int nb = 0; nb < 4; ++nb) w[nb][e] = img[(tap * 64 + nb * 16 + l16) * ST_LDF + c];
+    for (int nb = 0; nb < 4; ++nb) {
+      const float v = Wf[(tap * 64 + nb * 16 + l16) * 8 + c];
+      w[nb][e] = in ? v : 0.f;
+    }
   }
 }
 
-// c2_mfma_pk with register weights and ST_XLD-stride input rows: the same MFMA sequence (columns
-// past 3C multiply the image's zero pad column by 0, as c2_mfma_pk's zero X column does)
-__device__ __forceinline__ void pk_mfma(const float (&w)[4][4], const float* Xw, int C, int lg4, int l16,
-                                        f32x4 (&acc)[4][1]) {
+// One packed-tap front MFMA block (c2_mfma_pk's sequence): 16 output rows whose k = 3 inputs are rows
+// Xw[l16 + tap] (stride ST_XLD); k-columns past 3C are 0 x 0.
+__device__ __forceinline__ void pk_block(const float (&w)[4][4], const float* Xw, int C, int lg4, int l16,
+                                         f32x4 (&acc)[4]) {
   float b[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -80,77 +108,167 @@ __device__ __forceinline__ void pk_mfma(const float (&w)[4][4], const float* Xw,
     b[e] = in ? v : 0.f;
   }
 #pragma unroll
-  for (int nb = 0; nb < 4; ++nb)
+  for (int nb = 0; nb < 4; ++nb) {
+    acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int e = 0; e < 4; ++e) acc[nb][0] = mfma16x16x4(w[nb][e], b[e], acc[nb][0]);
-}
-
-// element i of a conv2w-style [bias (NW) | tail weight (16 x NW) | tail bias (16)] block (conv2w_kernel's Es)
-template <int NW>
-__device__ __forceinline__ float es_val(const ConvArgs& a, int i) {
-  if (i < NW) return (a.bias && i < a.N) ? a.bias[i] : 0.f;
-  if (i < 17 * NW) {
-    const int j = i - NW, c2 = j / NW, n = j - c2 * NW;
-    return (c2 < a.C2 && n < a.N) ? a.tW[(int64_t)c2 * a.N + n] : 0.f;
+    for (int e = 0; e < 4; ++e) acc[nb] = mfma16x16x4(w[nb][e], b[e], acc[nb]);
   }
-  const int c2 = i - 17 * NW;
-  return (a.tb && c2 < a.C2) ? a.tb[c2] : 0.f;
 }
 
-// a front conv's epilogue (bias, ReLU, pad rows 0; owned rows stored) and its rows into the XB slot
-__device__ __forceinline__ void front_out(const ConvArgs& a, int64_t rb, int lg4, int l16, f32x4 (&acc)[4][1],
-                                          const float* bias, int rlo, int rhi, float* xb) {
-  float b1[4][4], tw0[4][4] = {};
-  float4 aux[4][1] = {};
+// conv2_epilogue's ACT = 1 arithmetic on a 64-wide block (bias, ReLU, pad rows 0): rows r0 + l16;
+// rows l16 in [slo, shi) are stored to out (PCL, 64 channels); every row goes to the LDS slot rows xs.
+__device__ __forceinline__ void front_epi(f32x4 (&acc)[4], const f32x4 (&bias)[4], int64_t r0, int64_t R, int T,
+                                          int lg4, int l16, int slo, int shi, float* out, float* xs,
+                                          bool nostore) {
+  const int64_t r = r0 + l16;
+  const bool valid = row_valid(r, R, T);
+  const bool st = l16 >= slo && l16 < shi && r < R && !nostore;
 #pragma unroll
   for (int nb = 0; nb < 4; ++nb) {
-    const float4 b4 = *reinterpret_cast<const float4*>(bias + nb * 16 + 4 * lg4);
-    b1[nb][0] = b4.x; b1[nb][1] = b4.y; b1[nb][2] = b4.z; b1[nb][3] = b4.w;
-  }
-  conv2_epilogue<4, 1, 1>(a, rb, 0, lg4, l16, acc, aux, b1, tw0, f32x4{0.f, 0.f, 0.f, 0.f}, 1.0f, false, rlo, rhi);
+    f32x4 y;
 #pragma unroll
-  for (int nb = 0; nb < 4; ++nb) *reinterpret_cast<f32x4*>(xb + l16 * ST_LDW + nb * 16 + 4 * lg4) = acc[nb][0];
+    for (int v = 0; v < 4; ++v) {
+      const float yy = relu_f(acc[nb][v] * 1.0f + bias[nb][v]);
+      y[v] = valid ? yy : 0.f;
+    }
+    acc[nb] = y;
+    if (st) *reinterpret_cast<f32x4*>(out + r * 64 + nb * 16 + 4 * lg4) = y;
+    *reinterpret_cast<f32x4*>(xs + l16 * ST_LDW + nb * 16 + 4 * lg4) = y;
+  }
+}
+
+// The lane's epilogue constants of a [bias | tail weight | tail bias] block, held in registers
+template <int NB>
+struct TailConsts {
+  f32x4 bias[NB], tw[NB], tb;
+  __device__ __forceinline__ void load(const float* Es, int lg4, int l16) {
+    constexpr int NW = 16 * NB;
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      const float4 b4 = *reinterpret_cast<const float4*>(Es + nb * 16 + 4 * lg4);
+      const float4 t4 = *reinterpret_cast<const float4*>(Es + NW + l16 * NW + nb * 16 + 4 * lg4);
+      bias[nb] = f32x4{b4.x, b4.y, b4.z, b4.w};
+      tw[nb] = f32x4{t4.x, t4.y, t4.z, t4.w};
+    }
+    const float4 t4 = *reinterpret_cast<const float4*>(Es + 17 * NW + 4 * lg4);
+    tb = f32x4{t4.x, t4.y, t4.z, t4.w};
+  }
+};
+
+// conv2_epilogue's ACT = 1 + one-block 1x1 tail (+ softmax) arithmetic: y (NW channels, stored to out
+// with row stride ldn), z = tail(y) (stored to t_out, stride ldt), q = softmax(z) (SM: to q_out and the
+// LDS rows xq); rows l16 in [slo, shi) are stored.
+template <int NB, bool SM>
+__device__ __forceinline__ void tail_epi(f32x4 (&acc)[NB], const TailConsts<NB>& k, int64_t r0, int64_t R, int T,
+                                         int lg4, int l16, int slo, int shi, int N, float* out, int C2, float* t_out,
+                                         float* q_out, float* xq, bool nostore) {
+  const int64_t r = r0 + l16;
+  const bool valid = row_valid(r, R, T);
+  const bool st = l16 >= slo && l16 < shi && r < R && !nostore;
+  const int ldn = ld4(N), ldt = ld4(C2);
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    f32x4 y;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const float yy = relu_f(acc[nb][v] * 1.0f + k.bias[nb][v]);
+      y[v] = valid ? yy : 0.f;
+    }
+    acc[nb] = y;
+    const int n0 = nb * 16 + 4 * lg4;
+    if (st && n0 < ldn) *reinterpret_cast<f32x4*>(out + r * ldn + n0) = y;
+  }
+  f32x4 z = k.tb;
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) z = mfma16x16x4(k.tw[nb][v], acc[nb][v], z);
+  const int c0 = 4 * lg4;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) z[v] = valid ? z[v] : 0.f;
+  if (st && c0 < ldt) *reinterpret_cast<f32x4*>(t_out + r * ldt + c0) = z;
+  if constexpr (SM) {
+    float m = -__builtin_inff();
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+      if (c0 + v < C2) m = fmaxf(m, z[v]);
+    m = fmaxf(m, xor16(m));
+    m = fmaxf(m, xor32(m));
+    float e[4], s = 0.f;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      e[v] = (c0 + v < C2) ? __expf(z[v] - m) : 0.f;
+      s += e[v];
+    }
+    s += xor16(s);
+    s += xor32(s);
+    f32x4 qv;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) qv[v] = valid ? e[v] / s : 0.f;
+    if (st && c0 < ldt) *reinterpret_cast<f32x4*>(q_out + r * ldt + c0) = qv;
+    if (c0 < ST_XLD) *reinterpret_cast<f32x4*>(xq + l16 * ST_XLD + c0) = qv;
+  }
+}
+
+// element i of a [bias (NW) | tail weight (16 x NW) | tail bias (16)] block
+template <int NW>
+__device__ __forceinline__ float es_val(const float* bias, int N, const float* tW, const float* tb, int C2, int i) {
+  if (i < NW) return i < N ? bias[i] : 0.f;
+  if (i < 17 * NW) {
+    const int j = i - NW, c2 = j / NW, n = j - c2 * NW;
+    return (c2 < C2 && n < N) ? tW[(int64_t)c2 * N + n] : 0.f;
+  }
+  const int c2 = i - 17 * NW;
+  return c2 < C2 ? tb[c2] : 0.f;
+}
+
+__device__ __forceinline__ void dma16(const float* src, float* dst) {
+  __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint32_t*>(src), (__attribute__((address_space(3))) void*)dst,
+                                   16, 0, 0);
 }
 }  // namespace
 
-// e1 enc_conv1 (packed taps), e2 enc_conv2 + to_logits + softmax, d1 composed dec_conv1 (packed
-// taps), d2 dec_conv2 + to_params: the four ConvArgs of the pair launches (outputs, images, biases).
-template <int NB2, bool PROF>
-__global__ __launch_bounds__(512) void strip_fwd_kernel(ConvArgs e1, ConvArgs e2, ConvArgs d1, ConvArgs d2,
-                                                        int64_t nstrip) {
+template <int NB2, int PROF>
+__global__ __launch_bounds__(512) void strip_fwd_kernel(StripFwdArgs a) {
   using S = StripFwdLds<NB2>;
   constexpr int NW2 = S::NW2;
   extern __shared__ float4 smem4[];
   S& sh = *reinterpret_cast<S*>(smem4);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lg4 = lane >> 4, l16 = lane & 15;
-  const int64_t R = e1.R;
-  const int ldx = ld4(e1.Kc);  // x row stride (<= 8)
+  const int64_t R = a.R;
+  const int T = a.T, ldx = ld4(a.D);
+  float* slot = sh.slot[wave];
 
-  // x rows of the window at s0: thread i < 2 ST_SR holds float4 i % 2 of LDS row i / 2 (PCL row
-  // s0 - 1 + i / 2); the load is unconditional (clamped), the mask applied when it is stored
+  // x rows s0 - 2 .. s0 + 129 of a window: thread i < 2 ST_XR holds float4 i % 2 of row i / 2;
+  // the load is unconditional (clamped), the mask applied when it is stored
   auto load_x = [&](int64_t s0) {
     const int row = tid >> 1, h = 4 * (tid & 1);
-    int64_t r = s0 - 1 + row;
+    int64_t r = s0 - 2 + row;
     r = r < 0 ? 0 : (r >= R ? R - 1 : r);
-    return *reinterpret_cast<const float4*>(e1.src + r * ldx + (h < ldx ? h : 0));
+    return *reinterpret_cast<const float4*>(a.xp + r * ldx + (h < ldx ? h : 0));
   };
   auto store_x = [&](int64_t s0, float4 v) {
-    if (tid < 2 * ST_SR) {
+    if (tid < 2 * ST_XR) {
       const int row = tid >> 1, h = 4 * (tid & 1);
-      const int64_t r = s0 - 1 + row;
+      const int64_t r = s0 - 2 + row;
       const bool ok = r >= 0 && r < R && h < ldx;
-      *reinterpret_cast<float4*>(sh.XA + row * ST_XLD + h) = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(sh.Xx + row * ST_XLD + h) = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
 
   stamp<PROF>(0);
+  // ---- once.  vmcnt retires in order, so: the front images (LDS DMA) first, then x and the epilogue
+  // constants (registers), then the two 64-wide images (LDS DMA): waiting for x / the constants never
+  // waits for the big images, which stay in flight through the first enc_conv1.
+  // Wf[img][row][8] <- image row (tap, n) channels 0..7, by waves 0..3 only: those store x before the
+  // first barrier, so their wait for x (younger) covers these
+  for (int j = wave; wave < 4 && j < 12; j += 4) {
+    const int g = j * 64 + lane, img = g / 384, i = g - img * 384, row = i >> 1, h = 4 * (i & 1);
+    dma16((img ? a.img_d1 : a.img_e1) + row * ST_LDF + h, &sh.Wf[0][0] + j * 256);
+  }
   int64_t s = blockIdx.x;
   float4 px = load_x(s * ST_OWN - ST_HALO);
-
-  // ---- once: epilogue constants, front biases and front weights into registers; then the two
-  // 64-wide images by LDS DMA, issued last so that waiting for the register loads never waits for
-  // them: they stay in flight through x -> LDS and enc_conv1 (waited for before enc_conv2)
   constexpr int NE = NW2 * 17 + 16, ND = 64 * 17 + 16, NC = NE + ND + 128;  // sh.Ee2 | sh.Ed2 | sh.bf
   constexpr int NCJ = (NC + 511) / 512;
   float cv[NCJ];
@@ -158,32 +276,19 @@ __global__ __launch_bounds__(512) void strip_fwd_kernel(ConvArgs e1, ConvArgs e2
   for (int j = 0; j < NCJ; ++j) {
     const int i = tid + 512 * j;
     float v = 0.f;
-    if (i < NE) {
-      v = es_val<NW2>(e2, i);
-    } else if (i < NE + ND) {
-      v = es_val<64>(d2, i - NE);
-    } else if (i < NC) {
-      const int k = i - NE - ND, n = k & 63;
-      const ConvArgs& f = k < 64 ? e1 : d1;
-      v = (f.bias && n < f.N) ? f.bias[n] : 0.f;
-    }
+    if (i < NE) v = es_val<NW2>(a.b_e2, a.H2, a.tWl, a.tbl, a.K, i);
+    else if (i < NE + ND) v = es_val<64>(a.b_d2, 64, a.tWp, a.tbp, a.P, i - NE);
+    else if (i < NC) v = (i - NE - ND < 64 ? a.b_e1 : a.b_d1)[(i - NE - ND) & 63];
     cv[j] = v;
   }
-  float wE[4][4], wD[4][4];
-  pk_weights(e1.Wimg, e1.Kc, lg4, l16, wE);
-  pk_weights(d1.Wimg, d1.Kc, lg4, l16, wD);
   {
     constexpr int N1 = 3 * NW2 * ST_LDW / 4, N2 = 3 * 64 * ST_LDW / 4;  // float4s of each image
-    constexpr int C1 = (N1 + 63) / 64, C2 = (N2 + 63) / 64;              // 1 KB chunks (one per wave instruction)
+    constexpr int C1 = (N1 + 63) / 64, C2 = (N2 + 63) / 64;              // one wave instruction = 1 KB
     for (int c = wave; c < C1 + C2; c += 8) {
       const bool first = c < C1;
       const int cc = first ? c : c - C1;
       const int i = cc * 64 + lane;
-      const float* src = first ? e2.Wimg : d2.Wimg;
-      float* dst = (first ? sh.We2 : sh.Wd2) + cc * 256;
-      if (i < (first ? N1 : N2))
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint32_t*>(src) + 4 * i,
-                                         (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+      if (i < (first ? N1 : N2)) dma16((first ? a.img_e2 : a.img_d2) + 4 * i, (first ? sh.We2 : sh.Wd2) + cc * 256);
     }
   }
   static_assert(offsetof(S, Ed2) == offsetof(S, Ee2) + NE * 4 && offsetof(S, bf) == offsetof(S, Ed2) + ND * 4,
@@ -191,94 +296,129 @@ __global__ __launch_bounds__(512) void strip_fwd_kernel(ConvArgs e1, ConvArgs e2
 #pragma unroll
   for (int j = 0; j < NCJ; ++j)
     if (tid + 512 * j < NC) sh.Ee2[tid + 512 * j] = cv[j];
-  for (int i = tid; i < 2 * ST_LDW; i += 512) sh.XB[(i < ST_LDW ? 0 : (ST_SR - 1) * ST_LDW) + i % ST_LDW] = 0.f;
-  lds_barrier();  // LDS only: the image DMA stays in flight
+  if (tid < 4 * ST_XLD) sh.Xq[(tid < 2 * ST_XLD ? 0 : (ST_XR - 4) * ST_XLD) + tid] = 0.f;  // rows never written
+  store_x(s * ST_OWN - ST_HALO, px);
+  lds_barrier();  // LDS only: the big images stay in flight (the front images are older than x: landed)
   stamp<PROF>(1);
-  int it = 0;  // profiling: the first strip's phases
+  float wE[4][4], wD[4][4];
+  pk_weights(sh.Wf[0], a.D, lg4, l16, wE);
+  pk_weights(sh.Wf[1], a.K, lg4, l16, wD);
+  f32x4 bE[4], bD[4];
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb) {
+    const float4 e4 = *reinterpret_cast<const float4*>(sh.bf[0] + nb * 16 + 4 * lg4);
+    const float4 d4 = *reinterpret_cast<const float4*>(sh.bf[1] + nb * 16 + 4 * lg4);
+    bE[nb] = f32x4{e4.x, e4.y, e4.z, e4.w};
+    bD[nb] = f32x4{d4.x, d4.y, d4.z, d4.w};
+  }
+  TailConsts<NB2> kE;
+  TailConsts<4> kD;
+  kE.load(sh.Ee2, lg4, l16);
+  kD.load(sh.Ed2, lg4, l16);
 
-  // rows of this wave's block that the strip owns
-  const int rlo = max(0, ST_HALO - 16 * wave), rhi = min(16, ST_HALO + ST_OWN - 16 * wave);
-  for (; s < nstrip; s += gridDim.x) {
+  // this wave's block: window rows 16 w .. 16 w + 15.  Stored rows (window rows ST_HALO .. ST_HALO +
+  // ST_OWN - 1): the 64-wide convs' l16 range; the fronts' block A (rows 16w - 1 + l16) stores rows
+  // 16w .. 16w + 14, block B (rows 16w + 1 + l16) row 16w + 15
+  const int mlo = ST_HALO - 16 * wave, mhi = ST_HALO + ST_OWN - 16 * wave;  // in block-row units
+  const int slo = max(0, mlo), shi = min(16, mhi);
+  const int alo = max(1, mlo + 1), ahi = min(16, mhi + 1);
+  const bool bown = 15 >= mlo && 15 < mhi;
+  const bool nost = a.dbg & 1;
+  int it = 0;
+  for (; s < a.nstrip; s += gridDim.x) {
     const int64_t s0 = s * ST_OWN - ST_HALO;  // PCL row of window row 0
     const int64_t rb = s0 + 16 * wave;        // PCL row of this wave's block row 0
-    store_x(s0, px);
-    lds_barrier();
-    if (it == 0) stamp<PROF>(2);
     {
       const int64_t nx = s + gridDim.x;
-      px = load_x((nx < nstrip ? nx : s) * ST_OWN - ST_HALO);  // the next strip's x, in flight
+      px = load_x((nx < a.nstrip ? nx : s) * ST_OWN - ST_HALO);  // the next strip's x, in flight
     }
-    // ---- enc_conv1 + ReLU: x (XA) -> h1 (XB, h1e)
+    // ---- enc_conv1 + ReLU for rows rb - 1 .. rb + 16 (h1e: owned rows) -> slot
     {
-      f32x4 acc[4][1];
-#pragma unroll
-      for (int nb = 0; nb < 4; ++nb) acc[nb][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-      pk_mfma(wE, sh.XA + 16 * wave * ST_XLD, e1.Kc, lg4, l16, acc);
-      front_out(e1, rb, lg4, l16, acc, sh.bf[0], rlo, rhi, sh.XB + (16 * wave + 1) * ST_LDW);
+      f32x4 acc[4], acc2[4];
+      pk_block(wE, sh.Xx + (16 * wave) * ST_XLD, a.D, lg4, l16, acc);
+      pk_block(wE, sh.Xx + (16 * wave + 2) * ST_XLD, a.D, lg4, l16, acc2);
+      front_epi(acc, bE, rb - 1, R, T, lg4, l16, alo, ahi, a.h1e, slot, nost);
+      front_epi(acc2, bE, rb + 1, R, T, lg4, l16, bown ? 14 : 16, bown ? 15 : 16, a.h1e, slot + 2 * ST_LDW, nost);
     }
-    if (it == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the image DMA (first strip)
-    lds_barrier();
-    if (it == 0) stamp<PROF>(3);
-    // ---- enc_conv2 + ReLU (h2e) + to_logits (logits) + softmax (q, and q -> XA)
+    if (it == 0) {  // the first strip: every wave's share of the image DMA has landed
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      lds_barrier();
+    } else {
+      __builtin_amdgcn_wave_barrier();
+    }
+    // ---- enc_conv2 + ReLU (h2e) + to_logits (logits) + softmax (q; all 16 rows -> Xq)
     {
       f32x4 acc[NB2][1];
 #pragma unroll
       for (int nb = 0; nb < NB2; ++nb) acc[nb][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-      c2_mfma_tile<NB2, 1, 4, 3, ST_LDW, NW2>(sh.We2, sh.XB + 16 * wave * ST_LDW, lg4, l16, acc, true);
-      float bias_r[NB2][4], tw[NB2][4], tw2[NB2][4];
-      f32x4 tb0 = f32x4{0.f, 0.f, 0.f, 0.f}, tb1 = tb0;
-      c2_tail_consts<NB2, 1, NW2, 17>(sh.Ee2, lg4, l16, true, bias_r, tw, tw2, tb0, tb1);
-      float4 aux[NB2][1] = {};
-      conv2_epilogue<NB2, 1, 1, 1>(e2, rb, 0, lg4, l16, acc, aux, bias_r, tw, tb0, 1.0f, true, rlo, rhi, nullptr, 0,
-                                   tw2, tb1, sh.XA + (16 * wave + 1) * ST_XLD, ST_XLD);
+      c2_mfma_tile<NB2, 1, 4, 3, ST_LDW, NW2>(sh.We2, slot, lg4, l16, acc, true);
+      f32x4 y[NB2];
+#pragma unroll
+      for (int nb = 0; nb < NB2; ++nb) y[nb] = acc[nb][0];
+      tail_epi<NB2, true>(y, kE, rb, R, T, lg4, l16, slo, shi, a.H2, a.h2e, a.K, a.logits, a.q,
+                          sh.Xq + (16 * wave + 2) * ST_XLD, nost);
     }
-    lds_barrier();
+    lds_barrier();  // q of every block; everyone is done with Xx
+    if (it == 0) stamp<PROF>(2);
+    // ---- composed dec_conv1 + ReLU for rows rb - 1 .. rb + 16 (g1: owned rows) -> slot
+    {
+      f32x4 acc[4], acc2[4];
+      pk_block(wD, sh.Xq + (16 * wave) * ST_XLD, a.K, lg4, l16, acc);
+      pk_block(wD, sh.Xq + (16 * wave + 2) * ST_XLD, a.K, lg4, l16, acc2);
+      front_epi(acc, bD, rb - 1, R, T, lg4, l16, alo, ahi, a.g1, slot, nost);
+      front_epi(acc2, bD, rb + 1, R, T, lg4, l16, bown ? 14 : 16, bown ? 15 : 16, a.g1, slot + 2 * ST_LDW, nost);
+    }
+    __builtin_amdgcn_wave_barrier();
     if (it == 0) stamp<PROF>(4);
-    // ---- composed dec_conv1 + ReLU: q (XA) -> g1 (XB, g1)
+    // ---- dec_conv2 + ReLU (g2) + to_params (par)
     {
       f32x4 acc[4][1];
 #pragma unroll
       for (int nb = 0; nb < 4; ++nb) acc[nb][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-      pk_mfma(wD, sh.XA + 16 * wave * ST_XLD, d1.Kc, lg4, l16, acc);
-      front_out(d1, rb, lg4, l16, acc, sh.bf[1], rlo, rhi, sh.XB + (16 * wave + 1) * ST_LDW);
-    }
-    lds_barrier();
-    if (it == 0) stamp<PROF>(5);
-    // ---- dec_conv2 + ReLU (g2) + to_params (par).  No barrier after it: the next strip's x goes
-    // to XA (last read before the barrier above), and its barrier orders XB's next writes.
-    {
-      f32x4 acc[4][1];
+      c2_mfma_tile<4, 1, 4, 3, ST_LDW, 64>(sh.Wd2, slot, lg4, l16, acc, true);
+      f32x4 y[4];
 #pragma unroll
-      for (int nb = 0; nb < 4; ++nb) acc[nb][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-      c2_mfma_tile<4, 1, 4, 3, ST_LDW, 64>(sh.Wd2, sh.XB + 16 * wave * ST_LDW, lg4, l16, acc, true);
-      float bias_r[4][4], tw[4][4], tw2[4][4];
-      f32x4 tb0 = f32x4{0.f, 0.f, 0.f, 0.f}, tb1 = tb0;
-      c2_tail_consts<4, 1, 64, 17>(sh.Ed2, lg4, l16, true, bias_r, tw, tw2, tb0, tb1);
-      float4 aux[4][1] = {};
-      conv2_epilogue<4, 1, 1, 1>(d2, rb, 0, lg4, l16, acc, aux, bias_r, tw, tb0, 1.0f, true, rlo, rhi, nullptr, 0, tw2,
-                                 tb1);
-    }
-    if constexpr (PROF) {
-      if (it == 0) {
-        __syncthreads();
-        stamp<PROF>(6);
+      for (int nb = 0; nb < 4; ++nb) y[nb] = acc[nb][0];
+      if constexpr (PROF > 0) {
+        if (it == 0) {
+          asm volatile("s_nop 0" : : "v"(y[3][3]));  // the loop's results are in
+          stamp<PROF>(5);
+        }
       }
+      tail_epi<4, false>(y, kD, rb, R, T, lg4, l16, slo, shi, 64, a.g2, a.P, a.par, nullptr, nullptr, nost);
     }
+    if (it == 0) stamp<PROF>(6);
+    // the next strip's x (Xx is free: every wave passed the barrier after its last read)
+    {
+      const int64_t nx = s + gridDim.x;
+      store_x((nx < a.nstrip ? nx : s) * ST_OWN - ST_HALO, px);
+    }
+    lds_barrier();  // Xx written; Xq and the slots free again
+    if (it == 0) stamp<PROF>(3);
     ++it;
   }
-  if constexpr (PROF) {
+  if constexpr (PROF > 0) {
     __syncthreads();
     stamp<PROF>(7);
     if (threadIdx.x == 0 && blockIdx.x < 256) g_prof[blockIdx.x * 16 + 8] = (unsigned long long)it;
   }
 }
 
-static bool prof_on() {
-  static const bool v = [] {
-    const char* e = getenv("VQHMM_STRIP_PROF");
-    return e && atoi(e) != 0;
+static StripFwdArgs strip_fwd_args(const ConvArgs& e1, const ConvArgs& e2, const ConvArgs& d1, const ConvArgs& d2) {
+  StripFwdArgs a{};
+  a.R = e1.R; a.T = e1.T; a.D = e1.Kc; a.H2 = e2.N; a.K = e2.C2; a.P = d2.C2;
+  a.xp = e1.src;
+  a.img_e1 = e1.Wimg; a.img_d1 = d1.Wimg; a.img_e2 = e2.Wimg; a.img_d2 = d2.Wimg;
+  a.b_e1 = e1.bias; a.b_e2 = e2.bias; a.b_d1 = d1.bias; a.b_d2 = d2.bias;
+  a.tWl = e2.tW; a.tbl = e2.tb; a.tWp = d2.tW; a.tbp = d2.tb;
+  a.h1e = e1.out; a.h2e = e2.out; a.logits = e2.t_out; a.q = e2.q_out; a.g1 = d1.out; a.g2 = d2.out; a.par = d2.t_out;
+  a.nstrip = cdiv(e1.R, ST_OWN);
+  static const int dbg = [] {
+    const char* e = getenv("VQHMM_STRIP_DBG");
+    return e ? atoi(e) : 0;
   }();
-  return v;
+  a.dbg = dbg;
+  return a;
 }
 
 bool strip_fwd_supported(const ConvArgs& e1, const ConvArgs& e2, const ConvArgs& d1, const ConvArgs& d2) {
@@ -292,16 +432,24 @@ bool strip_fwd_supported(const ConvArgs& e1, const ConvArgs& e2, const ConvArgs&
          !d2.q_out && !d2.q_cf && !d2.reg_out;
 }
 
+static int prof_on() {
+  static const int v = [] {
+    const char* e = getenv("VQHMM_STRIP_PROF");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 int launch_strip_fwd(const ConvArgs& e1, const ConvArgs& e2, const ConvArgs& d1, const ConvArgs& d2, hipStream_t s) {
   if (!strip_fwd_supported(e1, e2, d1, d2)) return VQHMM_EUNSUPPORTED;
-  const int64_t nstrip = cdiv(e1.R, ST_OWN);
-  const unsigned grid = (unsigned)(nstrip < 256 ? nstrip : 256);
-#define VQHMM_SF(NB2, P) strip_fwd_kernel<NB2, P><<<grid, 512, sizeof(StripFwdLds<NB2>), s>>>(e1, e2, d1, d2, nstrip)
-  const bool prof = prof_on();
+  const StripFwdArgs a = strip_fwd_args(e1, e2, d1, d2);
+  const unsigned grid = (unsigned)(a.nstrip < 256 ? a.nstrip : 256);
+#define VQHMM_SF(NB2, P) strip_fwd_kernel<NB2, P><<<grid, 512, sizeof(StripFwdLds<NB2>), s>>>(a)
+  const bool prof = prof_on() != 0;
   if (c2_nb(e2.N) == 1) {
-    if (prof) VQHMM_SF(1, true); else VQHMM_SF(1, false);
+    if (prof) VQHMM_SF(1, 1); else VQHMM_SF(1, 0);
   } else {
-    if (prof) VQHMM_SF(2, true); else VQHMM_SF(2, false);
+    if (prof) VQHMM_SF(2, 1); else VQHMM_SF(2, 0);
   }
 #undef VQHMM_SF
   VQHMM_LAUNCH_CHECK();
