@@ -182,10 +182,11 @@ int vqhmm_elbo_status_offset(const vqhmm_dims_t* dims, int64_t B, int64_t T, siz
 int vqhmm_elbo_debug_buffers(const vqhmm_dims_t* dims, int64_t B, int64_t T, const void* workspace,
                              const float** buffers16);
 
-/* Phase timestamps (s_memrealtime ticks, 100 MHz) of the last launch of a kernel built for
- * profiling (VQHMM_STRIP_PROF=1 in the environment, read once; results unchanged): 16 slots per
- * workgroup for the first 256 workgroups.  Host-only, synchronous (tools/strip_prof.py). */
-int vqhmm_debug_prof(uint64_t* out, int64_t n);
+/* Phase timestamps (s_memrealtime ticks, 100 MHz) of the last launch of a kernel family built for
+ * profiling (which = 0: the strip kernels, VQHMM_STRIP_PROF=1; 1: the conv2 kernels, VQHMM_CONV_PROF=1;
+ * the switches are read once; results unchanged): 16 slots per workgroup for the first 256
+ * workgroups.  Host-only, synchronous (tools/strip_prof.py). */
+int vqhmm_debug_prof(int which, uint64_t* out, int64_t n);
 
 /* Stage table of the training step (forward stages then backward stages, in
  * launch order).  stage_info: name, algorithmic FLOPs and bytes of ONE launch

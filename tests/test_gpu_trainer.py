@@ -210,6 +210,14 @@ def test_strip_forward_matches_pair_launches(tmp_path, dims, bt):
     _run_both(tmp_path, "VQHMM_STRIP", dims, bt)
 
 
+@pytest.mark.parametrize("dims,bt", [((5, 64, 3, 32), (96, 150)), ((8, 64, 2, 30), (40, 77)), ((5, 64, 4, 31), (8, 50)),
+                                     ((5, 64, 3, 32), (256, 150))])
+def test_strip_backward_matches_pair_launches(tmp_path, dims, bt):
+    """The backward's data-gradient convolutions (to_params -> dec_conv2 -> dec_conv1 + softmax backward
+    + to_logits -> enc_conv2) as ONE strip launch against the pair launches (VQHMM_STRIP_BWD=0): same bits."""
+    _run_both(tmp_path, "VQHMM_STRIP_BWD", dims, bt)
+
+
 def test_tail_rerun_after_one_forward_is_identical():
     """The backward (its one-launch tail included) run twice after ONE forward gives the same bits:
     the tail re-arms its own dWc counters, so the second launch waits for its own reduction

@@ -13,6 +13,8 @@ import vqhmm  # noqa: E402
 from vqhmm import _ext  # noqa: E402
 
 NAMES = ["staging", "enc_conv1+enc_conv2+logits", "dec_conv1+dec_conv2+params", "-", "-", "-", "other strips"]
+# the backward strip (profiled when it is the step's last strip launch: the default)
+NAMES_BWD = ["DMA issue", "params+dec2 dgrad, dg1 swap", "dec1 dgrad+logits bwd", "-", "-", "-", "enc2 dgrad + rest"]
 
 
 def run(B, T=200, D=5, H=64, K=3, H2=32):
@@ -28,7 +30,7 @@ def run(B, T=200, D=5, H=64, K=3, H2=32):
         st.forward_backward(xs, us, Ls, 1.0)
     torch.cuda.synchronize()
     buf = np.zeros(256 * 16, dtype=np.uint64)
-    _ext.check(_ext.load().vqhmm_debug_prof(buf.ctypes.data_as(ctypes.c_void_p), buf.size), "debug_prof")
+    _ext.check(_ext.load().vqhmm_debug_prof(0, buf.ctypes.data_as(ctypes.c_void_p), buf.size), "debug_prof")
     t = buf.reshape(256, 16).astype(np.int64)
     used = t[:, 8] > 0
     t = t[used]
@@ -38,11 +40,13 @@ def run(B, T=200, D=5, H=64, K=3, H2=32):
     t0 = t[:, 0].min()
     print(f"B={B}: {used.sum()} workgroups, strips/wg {t[:, 8].min()}..{t[:, 8].max()}, "
           f"kernel span {(t[:, 7].max() - t0) * 0.01:.2f} us, start skew {(t[:, 0].max() - t0) * 0.01:.2f} us")
-    for i, n in enumerate(NAMES):
+    names = NAMES_BWD if os.environ.get("VQHMM_STRIP_BWD", "1") != "0" else NAMES
+    for i, n in enumerate(names):
         if n != "-":
             print(f"  {n:28s} median {np.median(d[:, i]):7.2f}  max {d[:, i].max():7.2f} us")
-    dw = np.median(np.diff(w0, axis=1), axis=0) * 0.01
-    print("  wave 0, second phase: front %.2f, dec_conv2 loop %.2f, tail %.2f, to barrier %.2f us" % tuple(dw))
+    if names is NAMES:
+        dw = np.median(np.diff(w0, axis=1), axis=0) * 0.01
+        print("  wave 0, second phase: front %.2f, dec_conv2 loop %.2f, tail %.2f, to barrier %.2f us" % tuple(dw))
     if t[:, 9].max() > 0:  # VQHMM_STRIP_PROF=2: serialised latency probes from the kernel's start
         for k, n in ((9, "x load"), (10, "+ constants"), (11, "+ front weights"), (12, "+ image DMA")):
             print(f"  {n:18s} at {np.median(t[:, k] - t[:, 0]) * 0.01:7.2f} us")

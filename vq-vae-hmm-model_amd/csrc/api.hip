@@ -562,6 +562,18 @@ bool bwd_pair_fused(const ElboPlan& p, const float* const* w, const float* gscal
   return conv2_bwd_pair_supported(conv_of(p, w, S_ENC2_DG), f);
 }
 
+// The backward's four data-gradient convolutions as one strip launch (strip.hip) where its shapes apply;
+// VQHMM_STRIP_BWD=0 keeps the pair launches (A/B), read once
+bool strip_bwd_on(const ElboPlan& p) {
+  static const bool on = [] {
+    const char* e = getenv("VQHMM_STRIP_BWD");
+    return !e || atoi(e) != 0;
+  }();
+  return on && logits_dg_fused(p) &&
+         strip_bwd_supported(conv_of(p, nullptr, S_PAR_DG), conv_of(p, nullptr, S_DEC2_DG), dec1_dg_args(p, nullptr, nullptr),
+                             conv_of(p, nullptr, S_ENC2_DG));
+}
+
 // VQHMM_TAIL_FUSED=0: grad_tail and compose_bwd / compose_adam as two launches (A/B); read once
 bool tail_fused_on() {
   static const bool v = [] {
@@ -603,6 +615,7 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       if (front_fused(p, w, st)) return launch_conv2_fused(fused_pair(p, w, st), s);
       return launch_conv(conv_of(p, w, st), s);
     case S_DEC2_DG:
+      if (strip_bwd_on(p)) return VQHMM_OK;  // in S_ENC2_DG's strip launch
       if (front_fused(p, w, st)) {
         ConvArgs a = fused_pair(p, w, st);
         a.f_scale = c.gscale;  // the front is S_PAR_DG
@@ -610,6 +623,11 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       }
       return launch_conv(conv_of(p, w, st), s);
     case S_ENC2_DG:
+      if (strip_bwd_on(p)) {
+        ConvArgs pd = conv_of(p, w, S_PAR_DG);
+        pd.scale = c.gscale;  // dpar is the head's gradient for dloss = 1
+        return launch_strip_bwd(pd, conv_of(p, w, S_DEC2_DG), dec1_dg_args(p, w, c.gscale), conv_of(p, w, st), s);
+      }
       if (bwd_pair_fused(p, w, c.gscale))
         return launch_conv2_bwd_pair(conv_of(p, w, st), dec1_dg_args(p, w, c.gscale), s);
       return launch_conv(conv_of(p, w, st), s);
@@ -617,11 +635,11 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       if (logits_dg_fused(p)) return VQHMM_OK;  // ran in S_DEC1_DG's epilogue
       return launch_conv(conv_of(p, w, st), s);
     case S_DEC1_DG: {
-      if (bwd_pair_fused(p, w, c.gscale)) return VQHMM_OK;  // runs inside S_ENC2_DG's launch
+      if (strip_bwd_on(p) || bwd_pair_fused(p, w, c.gscale)) return VQHMM_OK;  // runs inside S_ENC2_DG's launch
       return launch_conv(dec1_dg_args(p, w, c.gscale), s);
     }
     case S_PAR_DG: {
-      if (front_fused(p, w, S_DEC2_DG)) return VQHMM_OK;  // runs inside S_DEC2_DG's launch
+      if (strip_bwd_on(p) || front_fused(p, w, S_DEC2_DG)) return VQHMM_OK;  // in a later stage's launch
       ConvArgs a = conv_of(p, w, st);
       a.scale = c.gscale;  // dpar is the head's gradient for dloss = 1
       return launch_conv(a, s);
@@ -808,14 +826,20 @@ int vqhmm_elbo_stage_info(const vqhmm_dims_t* d, int64_t B, int64_t T, int stage
   const bool bwd_pair = bwd_pair_fused(plan_elbo(d, B, T, reinterpret_cast<void*>(4096)), nullptr, nullptr);
   const bool strip = strip_fwd_on(plan_elbo(d, B, T, reinterpret_cast<void*>(4096)));
   const bool in_strip = strip && (stage == S_ENC1 || stage == S_ENC2 || stage == S_DEC1 || stage == S_DEC2);
+  const bool bstrip = strip_bwd_on(plan_elbo(d, B, T, reinterpret_cast<void*>(4096)));
+  const bool in_bstrip = bstrip && (stage == S_PAR_DG || stage == S_DEC2_DG || stage == S_DEC1_DG ||
+                                    stage == S_LOGIT_BWD || stage == S_LOGIT_DG || stage == S_ENC2_DG);
   if (name && name_len) {
     const char* nm = kStageNames[stage];
     if (in_strip)
       nm = stage == S_ENC2 ? "strip_fwd(enc_conv1+enc_conv2+to_logits+dec_conv1+dec_conv2+to_params)"
                            : "(in strip_fwd)";
+    if (in_bstrip)
+      nm = stage == S_ENC2_DG ? "strip_bwd(to_params_dgrad+dec_conv2_dgrad+dec_conv1_dgrad+logits_bwd+to_logits_dgrad+enc_conv2_dgrad)"
+                              : "(in strip_bwd)";
     if (p.wgroup && stage == S_W_ENC1) nm = "wgrad_group(all 6 weight gradients)";
     else if (p.wgroup && stage >= S_W_PAR && stage < S_W_ENC1) nm = "(wgrad: in wgrad_group)";
-    else if (in_strip) {
+    else if (in_strip || in_bstrip) {
     } else if (fused_front && (stage == S_ENC1 || stage == S_DEC1 || stage == S_PAR_DG))
       nm = stage == S_ENC1 ? "(enc_conv1: in enc_conv2's launch)"
            : stage == S_DEC1 ? "(dec_conv1: in dec_conv2's launch)" : "(to_params_dgrad: in dec_conv2_dgrad's launch)";
@@ -846,6 +870,19 @@ int vqhmm_elbo_stage_info(const vqhmm_dims_t* d, int64_t B, int64_t T, int stage
       const double R = (double)p.R;
       b = 4.0 * R * (ld4(p.D) + ld4(p.H) + ld4(p.H2) + 2 * ld4(p.K) + 2 * ld4(p.H) + ld4(2 * p.D));
     }
+  } else if (in_bstrip) {  // S_ENC2_DG's launch does all six; HBM: dpar, the masks, q / dqx / dlx, h2 in, grads out
+    f = 0; b = 0;
+    if (stage == S_ENC2_DG) {
+      for (int st2 : {S_PAR_DG, S_DEC2_DG, S_DEC1_DG, S_LOGIT_BWD, S_LOGIT_DG, S_ENC2_DG}) {
+        double f1, b1;
+        int m1;
+        stage_work(p, st2, &f1, &b1, &m1);
+        f += f1;
+      }
+      const double R = (double)p.R;
+      b = 4.0 * R * (ld4(2 * p.D) + 3 * ld4(p.H) + 3 * ld4(p.K) + ld4(p.H2) +          // dpar, g2, g1, h1, q, dqx, dlx, h2
+                     2 * ld4(p.H) + 2 * ld4(p.K) + ld4(p.H2) + ld4(p.H));             // dg2, dg1, dqd, dlog, dh2, dh1
+    }
   } else if (fused_front && pair_of != stage) {
     f = 0; b = 0;  // counted with the launch it runs in
   } else if (fused_front) {
@@ -855,7 +892,8 @@ int vqhmm_elbo_stage_info(const vqhmm_dims_t* d, int64_t B, int64_t T, int stage
     f += f1;
     b += b1;
   }
-  if ((stage == S_LOGIT_BWD && logits_bwd_fused(p)) || (stage == S_LOGIT_DG && logits_dg_fused(p))) {
+  if (in_bstrip) {
+  } else if ((stage == S_LOGIT_BWD && logits_bwd_fused(p)) || (stage == S_LOGIT_DG && logits_dg_fused(p))) {
     f = 0; b = 0;
   } else if (stage == S_DEC1_DG && logits_bwd_fused(p)) {  // its epilogue does the logits backward (+ dgrad)
     double f1, b1;
@@ -870,7 +908,8 @@ int vqhmm_elbo_stage_info(const vqhmm_dims_t* d, int64_t B, int64_t T, int stage
     }
     m = 0;  // K output channels: bytes, not flops, bound it
   }
-  if (bwd_pair && stage == S_DEC1_DG) {
+  if (in_bstrip) {
+  } else if (bwd_pair && stage == S_DEC1_DG) {
     f = 0; b = 0;
   } else if (bwd_pair && stage == S_ENC2_DG) {  // + dec_conv1 dgrad with its fused epilogue work
     double f1, b1;
@@ -932,6 +971,15 @@ int vqhmm_elbo_debug_buffers(const vqhmm_dims_t* d, int64_t B, int64_t T, const 
                         p.dpar, p.dg2, p.dg1, p.dqd, p.dlog, p.dh2, p.dh1, p.dqx};
   for (int i = 0; i < 16; ++i) out[i] = v[i];
   return VQHMM_OK;
+}
+
+int vqhmm_debug_prof(int which, uint64_t* out, int64_t n) {
+  if (!out || n < 0 || n > 256 * 16) return VQHMM_EINVAL;
+  switch (which) {
+    case 0: return strip_prof_copy(out, n);
+    case 1: return conv2_prof_copy(out, n);
+  }
+  return VQHMM_EINVAL;
 }
 
 int vqhmm_adam_f32(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, double lr,

@@ -15,6 +15,7 @@
 #include <stdlib.h>
 
 #include "conv2_dev.h"
+#include "prof.h"
 
 namespace vqhmm {
 
@@ -288,6 +289,7 @@ __global__ __launch_bounds__(64 * 12) void conv2f_kernel(ConvArgs a, int64_t nti
   float* X1 = Fb + 64 + wave * (F::X_FLOATS + C::X_FLOATS);  // front input rows m0-2 .. m0+15
   float* Xs = X1 + F::X_FLOATS;                                // front output rows m0-1 .. m0+14
   const int lg4 = lane >> 4, l16 = lane & 15;
+  stamp_if(a.prof, 0);
 
   {
     const float4* src = reinterpret_cast<const float4*>(a.Wimg);
@@ -329,6 +331,8 @@ __global__ __launch_bounds__(64 * 12) void conv2f_kernel(ConvArgs a, int64_t nti
     pf[k] = x_raw(fa, tile * TR - 1, s < F::XF4 ? s : 0, F::KCW);
   }
   __syncthreads();  // weights; from here on the waves never wait for each other
+  stamp_if(a.prof, 1);
+  int ntl = 0;
   while (tile < ntiles) {
     const int64_t m0 = tile * TR;
     // ReLU masks of both epilogues (ACT = 2), older than the prefetch in the vmcnt order
@@ -393,6 +397,12 @@ __global__ __launch_bounds__(64 * 12) void conv2f_kernel(ConvArgs a, int64_t nti
     conv2_epilogue<NB, 1, ACT, TBC>(a, m0, 0, lg4, l16, acc, auxv, bias_r, tw, tb0, sc, TAIL, 0, TR, nullptr, 0, tw2,
                                     tb1);
     tile = next;
+    if (ntl++ == 0) stamp_if(a.prof, 2);
+  }
+  if (a.prof) {
+    __syncthreads();
+    stamp_if(true, 7);
+    if (threadIdx.x == 0 && blockIdx.x < 256) g_prof[blockIdx.x * 16 + 8] = (unsigned long long)ntl;
   }
 }
 
@@ -401,6 +411,8 @@ static int launch_c2f(const ConvArgs& a, hipStream_t s) {
   using Q = C2fCfg<NB, TAIL, FKS, FKCP>;
   ConvArgs ap = a;
   ap.pipe = 1;
+  static const int prof = prof_env("VQHMM_CONV_PROF");
+  ap.prof = prof;
   const int64_t ntiles = cdiv(a.R, Q::TR);
   int wmax = conv_wmax(12);
   while (wmax > 1 && Q::lds(wmax) > 160 * 1024) --wmax;
@@ -688,5 +700,7 @@ int launch_conv2(const ConvArgs& a, hipStream_t s) {
   if (a.R == 0) return VQHMM_OK;
   return a.ks == 3 ? launch_c2_n<3>(a, s) : launch_c2_n<1>(a, s);
 }
+
+int conv2_prof_copy(uint64_t* out, int64_t n) { return prof_copy(out, n); }
 
 }  // namespace vqhmm

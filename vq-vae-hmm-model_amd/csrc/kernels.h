@@ -60,6 +60,7 @@ struct ConvArgs {
   const float* f_aux;
   const float* f_scale;
   float* f_out;
+  int prof;          // conv2 kernels: phase stamps (prof.h, VQHMM_CONV_PROF; set by the launcher)
 };
 
 // Loss normalisers of compute_loss (VQ_VAE_HMM_fixed.py:120 mask.sum()*C, :131/:135 B).
@@ -224,6 +225,14 @@ int launch_conv2(const ConvArgs& a, hipStream_t s);
 // (the four ConvArgs of the separate launches; packed-tap fronts, H = 64, H2 <= 32, K <= 4, 2D <= 16)
 bool strip_fwd_supported(const ConvArgs& e1, const ConvArgs& e2, const ConvArgs& d1, const ConvArgs& d2);
 int launch_strip_fwd(const ConvArgs& e1, const ConvArgs& e2, const ConvArgs& d1, const ConvArgs& d2, hipStream_t s);
+// Backward strip kernel (strip.hip): to_params dgrad -> dec_conv2 dgrad -> composed dec_conv1 dgrad +
+// softmax backward + to_logits dgrad -> enc_conv2 dgrad in ONE launch (the four ConvArgs of those launches;
+// f = dec_conv1's ACT 3 args with lb_dh; H = 64, H2 in (16, 32], K <= 4, 2D <= 16)
+bool strip_bwd_supported(const ConvArgs& pd, const ConvArgs& d2, const ConvArgs& f, const ConvArgs& e2);
+int launch_strip_bwd(const ConvArgs& pd, const ConvArgs& d2, const ConvArgs& f, const ConvArgs& e2, hipStream_t s);
+// phase stamps of the last profiled launch (prof.h): strip.hip (VQHMM_STRIP_PROF), conv2.hip (VQHMM_CONV_PROF)
+int strip_prof_copy(uint64_t* out, int64_t n);
+int conv2_prof_copy(uint64_t* out, int64_t n);
 int launch_wgrad(const WgradArgs& a, hipStream_t s);
 int64_t wgrad_chunks(int64_t R, int64_t tiles);
 bool wgrad2_supported(const WgradArgs& a);

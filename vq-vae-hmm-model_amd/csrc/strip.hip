@@ -21,6 +21,7 @@
 #include <stdlib.h>
 
 #include "conv2_dev.h"
+#include "prof.h"
 
 namespace vqhmm {
 
@@ -47,15 +48,6 @@ constexpr int ST_XLD = 8;                      // their row stride
 constexpr int ST_LDW = 72;                     // c2_ldx(64): 64-channel slots and weight images
 constexpr int ST_LDF = 24;                     // the prologue's packed-front image row stride
 
-// profiling builds (VQHMM_STRIP_PROF=1, read once): s_memrealtime stamps of workgroup w's phases in
-// g_prof[w * 16 + k] (vqhmm_debug_prof); results unchanged
-__device__ unsigned long long g_prof[256 * 16];
-template <int PROF>
-__device__ __forceinline__ void stamp(int k) {
-  if constexpr (PROF > 0) {
-    if (threadIdx.x == 0 && blockIdx.x < 256) g_prof[blockIdx.x * 16 + k] = __builtin_amdgcn_s_memrealtime();
-  }
-}
 
 template <int NB2>
 struct StripFwdLds {
@@ -404,6 +396,236 @@ __global__ __launch_bounds__(512) void strip_fwd_kernel(StripFwdArgs a) {
   }
 }
 
+static int prof_on() {
+  static const int v = prof_env("VQHMM_STRIP_PROF");
+  return v;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Backward strip: to_params dgrad (1x1, mask g2) -> dec_conv2 dgrad (mask g1) -> composed dec_conv1
+// dgrad + softmax backward + to_logits dgrad (mask h2) -> enc_conv2 dgrad (mask h1) in ONE launch
+// (VQ_VAE_HMM_fixed.py:80-90 / :38-41 backward).  Wave w owns the window's block w: it computes the
+// 1x1 front for the 18 rows its dec_conv2 dgrad reads (dpar and the g2 mask come from HBM, so they are
+// exact at the window edges too), then dg1 goes through LDS (aliasing the per-wave slots) to the
+// dec_conv1 dgrad, and dh2 through LDS to the enc_conv2 dgrad: three workgroup barriers per strip;
+// rows >= 2 from the window edges are exact and stored.  Same MFMA sequences and epilogue
+// arithmetic as the pair launches (conv2f_kernel's front / main conv, conv2g_kernel's pair).
+struct StripBwdArgs {
+  int64_t R;
+  int T, ldp;                      // ldp = ld4(2D): dpar row stride (<= 16)
+  const float* dpar;               // PCL (R, ldp): the head's gradient of mu | logvar
+  const float *g2, *g1, *h1e;      // the ReLU masks (PCL, 64 channels)
+  const float *img_pd, *img_d2, *img_c1, *img_e2;  // dgrad images: [1][64][24], [3][64][72], [3][16][72], [3][64][40]
+  const float* gscale;             // device scale of dpar (null: 1)
+  float *dg2, *dg1, *dh1;
+  int64_t nstrip;
+};
+
+namespace {
+constexpr int SB_LDE = 40;  // c2_ldx(32): enc_conv2's dgrad input rows (dh2) and its image
+
+struct StripBwdLds {
+  float Wd2[3 * 64 * ST_LDW];    // dec_conv2 dgrad image
+  float We2[3 * 64 * SB_LDE];    // enc_conv2 dgrad image (32 input channels)
+  float Wc1[3 * 16 * ST_LDW];    // composed dec_conv1 dgrad image (K <= 4 outputs of 16)
+  float slot[8][18 * ST_LDW];    // per wave: dg2 rows rb - 1 .. rb + 16; then, all waves: dg1 rows s0 - 1 ..
+  float Dh2[(ST_WIN + 2) * SB_LDE];  // dh2 rows s0 - 1 .. s0 + 128
+};
+static_assert(8 * 18 * ST_LDW >= (ST_WIN + 2) * ST_LDW, "dg1 rows alias the slots");
+
+// conv2_epilogue's ACT = 2 arithmetic (scale, no bias, ReLU-backward mask, pad rows 0) on a 64-wide
+// block: rows r0 + l16, stored (PCL, 64 channels) for l16 in [slo, shi), optionally to LDS rows xs
+__device__ __forceinline__ void mask_epi(f32x4 (&acc)[4], const float4 (&aux)[4], float sc, int64_t r0, int64_t R,
+                                         int T, int lg4, int l16, int slo, int shi, float* out, float* xs, int xld) {
+  const int64_t r = r0 + l16;
+  const bool valid = row_valid(r, R, T);
+  const bool st = l16 >= slo && l16 < shi && r < R;
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb) {
+    const float av[4] = {aux[nb].x, aux[nb].y, aux[nb].z, aux[nb].w};
+    f32x4 y;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      float yy = acc[nb][v] * sc + 0.f;
+      yy = av[v] > 0.f ? yy : 0.f;
+      y[v] = valid ? yy : 0.f;
+    }
+    acc[nb] = y;
+    if (st) *reinterpret_cast<f32x4*>(out + r * 64 + nb * 16 + 4 * lg4) = y;
+    if (xs) *reinterpret_cast<f32x4*>(xs + l16 * xld + nb * 16 + 4 * lg4) = y;
+  }
+}
+
+// the 64-channel mask rows r0 + l16 of a block (clamped into [0, R): rows outside are not stored)
+__device__ __forceinline__ void load_mask(const float* m, int64_t r0, int64_t R, int lg4, int l16, float4 (&aux)[4]) {
+  int64_t r = r0 + l16;
+  r = r < 0 ? 0 : (r >= R ? R - 1 : r);
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb) aux[nb] = *reinterpret_cast<const float4*>(m + r * 64 + nb * 16 + 4 * lg4);
+}
+}  // namespace
+
+template <int PROF>
+__global__ __launch_bounds__(512) void strip_bwd_kernel(StripBwdArgs a, ConvArgs f) {
+  extern __shared__ float4 smem4[];
+  StripBwdLds& sh = *reinterpret_cast<StripBwdLds*>(smem4);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lg4 = lane >> 4, l16 = lane & 15;
+  const int64_t R = a.R;
+  const int T = a.T;
+  float* slot = sh.slot[wave];
+  float* D1 = &sh.slot[0][0];  // dg1 rows s0 - 1 .. s0 + 128 (after the slots' last read)
+
+  stamp<PROF>(0);
+  // ---- once: the 1x1 front's weights (registers), then the images by LDS DMA (waited for before the
+  // first dec_conv2 dgrad)
+  float wP[4][4];  // A operand of the 1x1 front: image[n = nb*16 + l16][k = 4 lg4 + e]
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb) {
+    const float4 w4 = *reinterpret_cast<const float4*>(a.img_pd + (nb * 16 + l16) * ST_LDF + 4 * lg4);
+    wP[nb][0] = w4.x; wP[nb][1] = w4.y; wP[nb][2] = w4.z; wP[nb][3] = w4.w;
+  }
+  const float psc = a.gscale ? *a.gscale : 1.0f;
+  {
+    constexpr int N1 = 3 * 64 * ST_LDW / 4, N2 = 3 * 64 * SB_LDE / 4, N3 = 3 * 16 * ST_LDW / 4;
+    constexpr int C1 = (N1 + 63) / 64, C2 = (N2 + 63) / 64, C3 = (N3 + 63) / 64;
+    for (int c = wave; c < C1 + C2 + C3; c += 8) {
+      const int k = c < C1 ? 0 : c < C1 + C2 ? 1 : 2;
+      const int cc = k == 0 ? c : k == 1 ? c - C1 : c - C1 - C2;
+      const int i = cc * 64 + lane, n = k == 0 ? N1 : k == 1 ? N2 : N3;
+      const float* src = k == 0 ? a.img_d2 : k == 1 ? a.img_e2 : a.img_c1;
+      float* dst = k == 0 ? sh.Wd2 : k == 1 ? sh.We2 : sh.Wc1;
+      if (i < n) dma16(src + 4 * i, dst + cc * 256);
+    }
+  }
+  stamp<PROF>(1);
+
+  const int mlo = ST_HALO - 16 * wave, mhi = ST_HALO + ST_OWN - 16 * wave;
+  const int slo = max(0, mlo), shi = min(16, mhi);
+  const int alo = max(1, mlo + 1), ahi = min(16, mhi + 1);
+  const bool bown = 15 >= mlo && 15 < mhi;
+  int it = 0;
+  for (int64_t s = blockIdx.x; s < a.nstrip; s += gridDim.x) {
+    const int64_t s0 = s * ST_OWN - ST_HALO;
+    const int64_t rb = s0 + 16 * wave;
+    // ---- to_params dgrad (1x1, x scale, mask g2) for rows rb - 1 .. rb + 16: two blocks -> dg2, slot
+    {
+      float4 mA[4], mB[4], xA, xB;
+      load_mask(a.g2, rb - 1, R, lg4, l16, mA);
+      load_mask(a.g2, rb + 1, R, lg4, l16, mB);
+      auto ld_dpar = [&](int64_t r) {  // row r, channels 4 lg4 .. (x_mask: rows outside / pad channels 0)
+        const int64_t rc = r < 0 ? 0 : (r >= R ? R - 1 : r);
+        const float4 v = *reinterpret_cast<const float4*>(a.dpar + rc * a.ldp + min(4 * lg4, a.ldp - 4));
+        return (r >= 0 && r < R && 4 * lg4 < a.ldp) ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+      };
+      xA = ld_dpar(rb - 1 + l16);
+      xB = ld_dpar(rb + 1 + l16);
+      f32x4 acc[4], acc2[4];
+      const float bA[4] = {xA.x, xA.y, xA.z, xA.w}, bB[4] = {xB.x, xB.y, xB.z, xB.w};
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+        acc2[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb) {
+          acc[nb] = mfma16x16x4(wP[nb][e], bA[e], acc[nb]);
+          acc2[nb] = mfma16x16x4(wP[nb][e], bB[e], acc2[nb]);
+        }
+      mask_epi(acc, mA, psc, rb - 1, R, T, lg4, l16, alo, ahi, a.dg2, slot, ST_LDW);
+      mask_epi(acc2, mB, psc, rb + 1, R, T, lg4, l16, bown ? 14 : 16, bown ? 15 : 16, a.dg2, slot + 2 * ST_LDW,
+               ST_LDW);
+    }
+    float4 m1[4];
+    load_mask(a.g1, rb, R, lg4, l16, m1);
+    if (it == 0) {  // the first strip: every wave's share of the image DMA has landed
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      lds_barrier();
+    } else {
+      __builtin_amdgcn_wave_barrier();
+    }
+    // ---- dec_conv2 dgrad (mask g1) -> dg1 (registers, HBM)
+    f32x4 d1[4];
+    {
+      f32x4 acc[4][1];
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) acc[nb][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+      c2_mfma_tile<4, 1, 4, 3, ST_LDW, 64>(sh.Wd2, slot, lg4, l16, acc, true);
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) d1[nb] = acc[nb][0];
+      mask_epi(d1, m1, 1.0f, rb, R, T, lg4, l16, slo, shi, a.dg1, nullptr, 0);
+    }
+    lds_barrier();  // every slot read
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) *reinterpret_cast<f32x4*>(D1 + (16 * wave + 1 + l16) * ST_LDW + nb * 16 + 4 * lg4) = d1[nb];
+    float4 m2[4];
+    load_mask(a.h1e, rb, R, lg4, l16, m2);
+    lds_barrier();  // dg1 of every block
+    if (it == 0) stamp<PROF>(2);
+    // ---- composed dec_conv1 dgrad + softmax backward + to_logits dgrad (mask h2): dqd, dlog, dh2 (HBM),
+    // dh2 of all 16 rows -> Dh2 (conv2g_kernel's front, conv2_epilogue ACT 3)
+    {
+      f32x4 acc1[1][1] = {{f32x4{0.f, 0.f, 0.f, 0.f}}};
+      c2_mfma_tile<1, 1, 4, 3, ST_LDW, 16>(sh.Wc1, D1 + 16 * wave * ST_LDW, lg4, l16, acc1, true);
+      const float zb1[1][4] = {}, tw1[1][4] = {};
+      const float4 aux1[1][1] = {};
+      const float fsc = f.scale ? *f.scale : 1.0f;
+      conv2_epilogue<1, 1, 3>(f, rb, 0, lg4, l16, acc1, aux1, zb1, tw1, f32x4{0.f, 0.f, 0.f, 0.f}, fsc, false, slo,
+                              shi, sh.Dh2 + (16 * wave + 1) * SB_LDE, SB_LDE);
+    }
+    lds_barrier();  // dh2 of every block
+    if (it == 0) stamp<PROF>(3);
+    // ---- enc_conv2 dgrad (mask h1) -> dh1
+    {
+      f32x4 acc[4][1];
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) acc[nb][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+      c2_mfma_tile<4, 1, 2, 3, SB_LDE, 64>(sh.We2, sh.Dh2 + 16 * wave * SB_LDE, lg4, l16, acc, true);
+      f32x4 y[4];
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) y[nb] = acc[nb][0];
+      mask_epi(y, m2, 1.0f, rb, R, T, lg4, l16, slo, shi, a.dh1, nullptr, 0);
+    }
+    // no barrier: the next strip writes the slots (dg1, last read before the barrier above) and Dh2
+    // only after its own first two barriers
+    ++it;
+  }
+  if constexpr (PROF > 0) {
+    __syncthreads();
+    stamp<PROF>(7);
+    if (threadIdx.x == 0 && blockIdx.x < 256) g_prof[blockIdx.x * 16 + 8] = (unsigned long long)it;
+  }
+}
+
+bool strip_bwd_supported(const ConvArgs& pd, const ConvArgs& d2, const ConvArgs& f, const ConvArgs& e2) {
+  return pd.R > 0 && pd.R < (1ll << 31) && pd.ks == 1 && pd.act == 2 && pd.Wimg && pd.aux && pd.out && pd.N == 64 &&
+         pd.Kc >= 1 && pd.Kc <= 16 && !pd.src_cf && !pd.bias &&
+         d2.src == pd.out && d2.ks == 3 && d2.act == 2 && d2.Wimg && d2.aux && d2.out && d2.Kc == 64 && d2.N == 64 &&
+         !d2.bias && !d2.scale &&
+         f.src == d2.out && f.act == 3 && f.ks == 3 && f.Wimg && f.Kc == 64 && f.N >= 1 && f.N <= 4 && f.lb_dh &&
+         f.lb_C > 16 && f.lb_C <= 32 && ld4(f.lb_C) == 32 && !f.bias && !f.out_cf &&
+         e2.src == f.lb_dh && e2.ks == 3 && e2.act == 2 && e2.Wimg && e2.aux && e2.out && e2.Kc == f.lb_C &&
+         e2.N == 64 && !e2.bias && !e2.scale && !e2.tW && !e2.out_cf;
+}
+
+int launch_strip_bwd(const ConvArgs& pd, const ConvArgs& d2, const ConvArgs& f, const ConvArgs& e2, hipStream_t s) {
+  if (!strip_bwd_supported(pd, d2, f, e2)) return VQHMM_EUNSUPPORTED;
+  StripBwdArgs a{};
+  a.R = pd.R; a.T = pd.T; a.ldp = ld4(pd.Kc);
+  a.dpar = pd.src; a.g2 = pd.aux; a.g1 = d2.aux; a.h1e = e2.aux;
+  a.img_pd = pd.Wimg; a.img_d2 = d2.Wimg; a.img_c1 = f.Wimg; a.img_e2 = e2.Wimg;
+  a.gscale = pd.scale;
+  a.dg2 = pd.out; a.dg1 = d2.out; a.dh1 = e2.out;
+  a.nstrip = cdiv(pd.R, ST_OWN);
+  const unsigned grid = (unsigned)(a.nstrip < 256 ? a.nstrip : 256);
+  if (prof_on()) strip_bwd_kernel<1><<<grid, 512, sizeof(StripBwdLds), s>>>(a, f);
+  else strip_bwd_kernel<0><<<grid, 512, sizeof(StripBwdLds), s>>>(a, f);
+  VQHMM_LAUNCH_CHECK();
+  return VQHMM_OK;
+}
+
 static StripFwdArgs strip_fwd_args(const ConvArgs& e1, const ConvArgs& e2, const ConvArgs& d1, const ConvArgs& d2) {
   StripFwdArgs a{};
   a.R = e1.R; a.T = e1.T; a.D = e1.Kc; a.H2 = e2.N; a.K = e2.C2; a.P = d2.C2;
@@ -432,13 +654,7 @@ bool strip_fwd_supported(const ConvArgs& e1, const ConvArgs& e2, const ConvArgs&
          !d2.q_out && !d2.q_cf && !d2.reg_out;
 }
 
-static int prof_on() {
-  static const int v = [] {
-    const char* e = getenv("VQHMM_STRIP_PROF");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
+int strip_prof_copy(uint64_t* out, int64_t n) { return prof_copy(out, n); }
 
 int launch_strip_fwd(const ConvArgs& e1, const ConvArgs& e2, const ConvArgs& d1, const ConvArgs& d2, hipStream_t s) {
   if (!strip_fwd_supported(e1, e2, d1, d2)) return VQHMM_EUNSUPPORTED;
@@ -458,9 +674,3 @@ int launch_strip_fwd(const ConvArgs& e1, const ConvArgs& e2, const ConvArgs& d1,
 
 }  // namespace vqhmm
 
-extern "C" int vqhmm_debug_prof(uint64_t* out, int64_t n) {
-  if (!out || n < 0 || n > 256 * 16) return VQHMM_EINVAL;
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vqhmm::g_prof), (size_t)n * 8, 0, hipMemcpyDeviceToHost) != hipSuccess)
-    return VQHMM_ELAUNCH;
-  return VQHMM_OK;
-}

@@ -85,7 +85,7 @@ _SIGS = {
     "vqhmm_argmax_f32": (ctypes.c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "vqhmm_elbo_debug_buffers": (ctypes.c_int, [ctypes.POINTER(Dims), c_i64, c_i64, c_vp, ctypes.POINTER(c_vp)]),
     "vqhmm_elbo_status_offset": (ctypes.c_int, [ctypes.POINTER(Dims), c_i64, c_i64, ctypes.POINTER(c_sz)]),
-    "vqhmm_debug_prof": (ctypes.c_int, [c_vp, c_i64]),
+    "vqhmm_debug_prof": (ctypes.c_int, [ctypes.c_int, c_vp, c_i64]),
 }
 
 # bits of the step's device status word (include/vqhmm.h VQHMM_STATUS_*)
