@@ -184,6 +184,7 @@ int vqhmm_elbo_debug_buffers(const vqhmm_dims_t* dims, int64_t B, int64_t T, con
 
 /* Phase timestamps (s_memrealtime ticks, 100 MHz) of the last launch of a kernel family built for
  * profiling (which = 0: the strip kernels, VQHMM_STRIP_PROF=1; 1: the conv2 kernels, VQHMM_CONV_PROF=1;
+ * 2: the cooperative ELBO head, VQHMM_HEAD_PROF=1;
  * the switches are read once; results unchanged): 16 slots per workgroup for the first 256
  * workgroups.  Host-only, synchronous (tools/strip_prof.py). */
 int vqhmm_debug_prof(int which, uint64_t* out, int64_t n);

@@ -47,6 +47,8 @@ def run(B, T=200, D=5, H=64, K=3, H2=32):
     if names is NAMES:
         dw = np.median(np.diff(w0, axis=1), axis=0) * 0.01
         print("  wave 0, second phase: front %.2f, dec_conv2 loop %.2f, tail %.2f, to barrier %.2f us" % tuple(dw))
+        fw = np.median(np.diff(t[:, [2, 10, 11, 4]].astype(np.int64), axis=1), axis=0) * 0.01
+        print("    front: LDS reads + 32 MFMAs %.2f, epilogue A %.2f, epilogue B + wave barrier %.2f us" % tuple(fw))
     if t[:, 9].max() > 0:  # VQHMM_STRIP_PROF=2: serialised latency probes from the kernel's start
         for k, n in ((9, "x load"), (10, "+ constants"), (11, "+ front weights"), (12, "+ image DMA")):
             print(f"  {n:18s} at {np.median(t[:, k] - t[:, 0]) * 0.01:7.2f} us")

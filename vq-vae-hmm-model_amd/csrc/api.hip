@@ -569,7 +569,9 @@ bool strip_bwd_on(const ElboPlan& p) {
     const char* e = getenv("VQHMM_STRIP_BWD");
     return !e || atoi(e) != 0;
   }();
-  return on && logits_dg_fused(p) &&
+  // measured (tools/gpu_stripab.sh): B = 128 0.124 -> 0.116 ms, 256 0.1765 -> 0.1715, 512 0.2784 -> 0.2761,
+  // cfg2 (207k rows) 0.462 -> 0.467: below 2^17 rows only, as the backward pair
+  return on && p.R < ((int64_t)1 << 17) && logits_dg_fused(p) &&
          strip_bwd_supported(conv_of(p, nullptr, S_PAR_DG), conv_of(p, nullptr, S_DEC2_DG), dec1_dg_args(p, nullptr, nullptr),
                              conv_of(p, nullptr, S_ENC2_DG));
 }
@@ -978,6 +980,7 @@ int vqhmm_debug_prof(int which, uint64_t* out, int64_t n) {
   switch (which) {
     case 0: return strip_prof_copy(out, n);
     case 1: return conv2_prof_copy(out, n);
+    case 2: return head_prof_copy(out, n);
   }
   return VQHMM_EINVAL;
 }

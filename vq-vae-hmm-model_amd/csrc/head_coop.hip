@@ -17,6 +17,7 @@
 // layout (same tail reduction).  WR = 256 / KP: 64 rows (4 row blocks) at K <= 4, 32 (2) at K <= 8.
 // Summation order differs from the reference's autograd; the tests hold it to 1e-5 relative.
 #include "kernels.h"
+#include "prof.h"
 
 namespace vqhmm {
 
@@ -113,6 +114,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_coop_kernel(HeadArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lg4 = lane >> 4, l16 = lane & 15;
   const int prow = tid / KP, si = tid % KP;  // phase B: (row, source state)
+  stamp_if(a.dbg & 16, 0);
   const int U = a.U, D = a.D;
   const int ldp = ld4(2 * D), ldx = ld4(D), ldu = ld4(U);
   const float Bn = loss_norm_batch(a.norm, a.B);
@@ -182,6 +184,8 @@ __global__ __launch_bounds__(256, 2) void elbo_head_coop_kernel(HeadArgs a) {
   }
   __syncthreads();
   const float inv_n = 1.0f / fmaxf((float)(sh.cnt * (unsigned long long)D), 1.0f);
+  stamp_if(a.dbg & 16, 1);
+  int nwn = 0;
 
   float s_rec = 0.f, s_ent = 0.f, s_tr = 0.f, s_init = 0.f, q0acc = 0.f, db2acc = 0.f;
   f32x4 gW2[KB][HBW], gW1[HBW];
@@ -397,7 +401,9 @@ __global__ __launch_bounds__(256, 2) void elbo_head_coop_kernel(HeadArgs a) {
         }
       }
     }
+    if (nwn++ == 0) stamp_if(a.dbg & 16, 2);
   }
+  stamp_if(a.dbg & 16, 3);
 
   // ---------------- epilogue: loss partials, q0 / db2 sums, weight-gradient partials (fixed order)
   double ds[4] = {(double)s_rec, (double)s_init, (double)s_tr, (double)s_ent};
@@ -439,6 +445,11 @@ __global__ __launch_bounds__(256, 2) void elbo_head_coop_kernel(HeadArgs a) {
       else if (l16 == U) sb1[h] = gW1[hl][v];
     }
   }
+  if (a.dbg & 16) {
+    __syncthreads();
+    stamp_if(true, 7);
+    if (threadIdx.x == 0 && blockIdx.x < 256) g_prof[blockIdx.x * 16 + 8] = (unsigned long long)nwn;
+  }
 }
 
 bool head_coop_supported(const HeadArgs& a) {
@@ -458,8 +469,13 @@ int head_coop_grid(int64_t R, int K) {
   return (int)(nwin < cap ? (nwin > 0 ? nwin : 1) : cap);
 }
 
-int launch_head_coop(const HeadArgs& a, int grid, hipStream_t s) {
-  if (!head_coop_supported(a)) return VQHMM_EUNSUPPORTED;
+int head_prof_copy(uint64_t* out, int64_t n) { return prof_copy(out, n); }
+
+int launch_head_coop(const HeadArgs& a0, int grid, hipStream_t s) {
+  if (!head_coop_supported(a0)) return VQHMM_EUNSUPPORTED;
+  static const int prof = prof_env("VQHMM_HEAD_PROF");
+  HeadArgs a = a0;
+  if (prof) a.dbg |= 16;  // phase stamps (prof.h)
   if (a.R == 0) return VQHMM_OK;
 #define VQHMM_HC(KV, HBWV, KPV)                                                                      \
   {                                                                                                  \

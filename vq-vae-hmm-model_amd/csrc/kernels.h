@@ -233,6 +233,7 @@ int launch_strip_bwd(const ConvArgs& pd, const ConvArgs& d2, const ConvArgs& f, 
 // phase stamps of the last profiled launch (prof.h): strip.hip (VQHMM_STRIP_PROF), conv2.hip (VQHMM_CONV_PROF)
 int strip_prof_copy(uint64_t* out, int64_t n);
 int conv2_prof_copy(uint64_t* out, int64_t n);
+int head_prof_copy(uint64_t* out, int64_t n);  // head_coop.hip (VQHMM_HEAD_PROF)
 int launch_wgrad(const WgradArgs& a, hipStream_t s);
 int64_t wgrad_chunks(int64_t R, int64_t tiles);
 bool wgrad2_supported(const WgradArgs& a);

@@ -357,7 +357,14 @@ __global__ __launch_bounds__(512) void strip_fwd_kernel(StripFwdArgs a) {
       f32x4 acc[4], acc2[4];
       pk_block(wD, sh.Xq + (16 * wave) * ST_XLD, a.K, lg4, l16, acc);
       pk_block(wD, sh.Xq + (16 * wave + 2) * ST_XLD, a.K, lg4, l16, acc2);
+      if constexpr (PROF > 0) {
+        if (it == 0) {
+          asm volatile("s_nop 0" : : "v"(acc[3][3]), "v"(acc2[3][3]));
+          stamp<PROF>(10);
+        }
+      }
       front_epi(acc, bD, rb - 1, R, T, lg4, l16, alo, ahi, a.g1, slot, nost);
+      if (it == 0) stamp<PROF>(11);
       front_epi(acc2, bD, rb + 1, R, T, lg4, l16, bown ? 14 : 16, bown ? 15 : 16, a.g1, slot + 2 * ST_LDW, nost);
     }
     __builtin_amdgcn_wave_barrier();
