@@ -170,7 +170,7 @@ torch.save({"grad": st.grad.cpu(), "flat": st.flat.cpu(), "m": st.exp_avg.cpu(),
 """
 
 
-def _run_both(tmp_path, env, dims, bt=(96, 150)):
+def _run_both(tmp_path, env, dims, bt=(96, 150), extra=None):
     """The same 4 steps in two fresh processes, env=1 and env=0 (the switches are read once per
     process); loss, gradient, moments and parameters must agree bit for bit."""
     import os
@@ -183,7 +183,7 @@ def _run_both(tmp_path, env, dims, bt=(96, 150)):
         f = str(tmp_path / f"{env}{flag}.pt")
         subprocess.run([sys.executable, "-c", _SPLIT_RUN, pkg, f, ",".join(map(str, dims)), ",".join(map(str, bt))],
                        check=True,
-                       timeout=300, env=dict(os.environ, **{env: flag}))
+                       timeout=300, env=dict(os.environ, **{env: flag}, **(extra or {})))
         out[flag] = torch.load(f, weights_only=True)
     for k in ("grad", "flat", "m", "v", "loss"):
         assert torch.equal(out["1"][k], out["0"][k]), k
@@ -206,8 +206,9 @@ def test_fused_conv_pairs_match_separate_launches(tmp_path, dims):
                                      ((5, 64, 3, 32), (256, 150))])  # 319 strips: workgroups run 2
 def test_strip_forward_matches_pair_launches(tmp_path, dims, bt):
     """The four forward convolutions as ONE strip launch (strip.hip: 128-row windows, 3 recomputed
-    halo rows a side, activations in LDS) against the pair launches (VQHMM_STRIP=0): same bits."""
-    _run_both(tmp_path, "VQHMM_STRIP", dims, bt)
+    halo rows a side, activations in LDS) against the pair launches (VQHMM_STRIP=0): same bits (the head
+    as its own launch in both: fused, its slab sums run in another order, test_strip_head_*)."""
+    _run_both(tmp_path, "VQHMM_STRIP", dims, bt, {"VQHMM_STRIP_HEAD": "0"})
 
 
 @pytest.mark.parametrize("dims,bt", [((5, 64, 3, 32), (96, 150)), ((8, 64, 2, 30), (40, 77)), ((5, 64, 4, 31), (8, 50)),
@@ -216,6 +217,60 @@ def test_strip_backward_matches_pair_launches(tmp_path, dims, bt):
     """The backward's data-gradient convolutions (to_params -> dec_conv2 -> dec_conv1 + softmax backward
     + to_logits -> enc_conv2) as ONE strip launch against the pair launches (VQHMM_STRIP_BWD=0): same bits."""
     _run_both(tmp_path, "VQHMM_STRIP_BWD", dims, bt)
+
+
+_HEAD_RUN = r"""
+import sys, torch
+sys.path.insert(0, sys.argv[1])
+import vqhmm
+D, H, K, H2, TH = (int(v) for v in sys.argv[3].split(","))
+B, T = (int(v) for v in sys.argv[4].split(","))
+gen = torch.Generator().manual_seed(7)
+x = torch.randn(B, D, T, generator=gen).cuda()
+u = torch.randn(B, 4, T, generator=gen).cuda()
+L = torch.randint(max(1, T // 3), T + 1, (B,), generator=gen)
+torch.manual_seed(3)
+m = vqhmm.VAE_HMM(D, H, K, H2, u_dim=4, trans_hidden=TH).cuda()
+st = vqhmm.TrainState(m, lr=1e-3)
+xs, us, Ls = st.prepare(x, u, L)
+out = {}
+for i in range(2):
+    st.forward_backward(xs, us, Ls, 0.5)
+    torch.cuda.synchronize()
+    out["loss%d" % i] = st.loss.detach().cpu().clone()
+    out["grad%d" % i] = st.grad.detach().cpu().clone()
+    st.apply_adam()
+loss = m.compute_loss(x, u, L, 0.5)  # the module path: forward with need_grad = 1 and backward
+loss.backward()
+out["mloss"] = loss.detach().cpu()
+out["mgrad"] = torch.cat([p.grad.detach().flatten() for p in m.parameters()]).cpu()
+torch.save(out, sys.argv[2])
+"""
+
+
+@pytest.mark.parametrize("dims,bt", [((5, 64, 3, 32, 128), (96, 150)), ((4, 64, 2, 16, 64), (40, 77)),
+                                     ((5, 64, 4, 32, 128), (256, 150))])
+def test_strip_head_matches_head_launch(tmp_path, dims, bt):
+    """The ELBO head fused into the forward strip launch (VQHMM_STRIP_HEAD=1, an A/B switch; its slabs / loss
+    partials per strip workgroup) against the head's own launch: per-row outputs feed the same backward, the
+    loss and the gradient differ only in the slab / partial summation order (1e-6 relative)."""
+    import os
+    import subprocess
+    import sys
+    from conftest import ROOT
+    pkg = os.path.join(ROOT, "vq-vae-hmm-model_amd")
+    out = {}
+    for flag in ("1", "0"):
+        f = str(tmp_path / f"h{flag}.pt")
+        subprocess.run([sys.executable, "-c", _HEAD_RUN, pkg, f, ",".join(map(str, dims)), ",".join(map(str, bt))],
+                       check=True, timeout=300, env=dict(os.environ, VQHMM_STRIP_HEAD=flag))
+        out[flag] = torch.load(f, weights_only=True)
+    for k in ("loss0", "loss1", "mloss"):
+        a, b = out["1"][k].double(), out["0"][k].double()
+        assert torch.allclose(a, b, rtol=1e-6, atol=0), (k, a, b)
+    for k in ("grad0", "grad1", "mgrad"):
+        a, b = out["1"][k].double(), out["0"][k].double()
+        assert (a - b).norm() <= 1e-6 * b.norm(), (k, ((a - b).norm() / b.norm()).item())
 
 
 def test_tail_rerun_after_one_forward_is_identical():

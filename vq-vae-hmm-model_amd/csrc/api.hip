@@ -67,6 +67,30 @@ int64_t wgroup_min_rows() {
   return v;
 }
 
+// VQHMM_STRIP=0: the forward convolutions as pair launches; VQHMM_STRIP_HEAD=1: the ELBO head fused into the
+// forward strip (A/B switches, read once).  The fused head is off by default: one 8-wave workgroup per CU runs
+// the head's phases in lockstep behind its barriers, where head_coop's two workgroups per CU overlap one's
+// VALU phase with the other's MFMA phase, so it measured slower (strip + head: B = 128 46.6 -> 43.2 us but the
+// step 0.1161 -> 0.1162 ms; cfg2 178 -> 199 us, 0.462 -> 0.488 ms; gpurun_out sq7)
+bool strip_fwd_env() {
+  static const bool on = [] {
+    const char* e = getenv("VQHMM_STRIP");
+    return !e || atoi(e) != 0;
+  }();
+  return on;
+}
+bool strip_head_on() {
+  static const bool on = [] {
+    const char* e = getenv("VQHMM_STRIP_HEAD");
+    return e && atoi(e) != 0;
+  }();
+  return on && strip_fwd_env();
+}
+// the shapes the forward strip covers (strip_fwd_supported on the plan's ConvArgs agrees)
+bool strip_fwd_shapes_ok(int D, int H, int H2, int K, int64_t R) {
+  return D >= 1 && 3 * D <= 16 && H == 64 && H2 >= 1 && H2 <= 32 && K >= 1 && K <= 4 && R > 0 && R < (1ll << 31);
+}
+
 bool dims_ok(const vqhmm_dims_t* d) {
   return d && d->input_dim > 0 && d->hidden_dim > 0 && d->K > 0 && d->hidden_dim2 > 0 && d->u_dim > 0 &&
          d->trans_hidden > 0;
@@ -99,6 +123,7 @@ struct ElboPlan {
   bool staged;
   bool wave_head;  // head_wave.hip (K <= 4, VQHMM_HEAD=wave)
   bool coop_head;  // head_coop.hip (K <= 8, the default); else head_mfma / head.hip
+  bool strip_head;  // the head runs inside the forward strip launch (strip.hip; slabs = its workgroups)
   float *hid, *lgA, *dhid, *nx, *dqc, *trw, *logpi;
   // backward
   float *dg2, *dg1, *dqd, *dlog, *dh2, *dh1, *dWc;
@@ -139,7 +164,13 @@ ElboPlan plan_elbo(const vqhmm_dims_t* d, int64_t B, int64_t T, void* ws) {
     p.coop_head = head_coop_supported(hc) && head_choice() == 0;
     p.wave_head = !p.coop_head && head_mfma_supported(hc) && p.U <= 4 && head_choice() == 1;
   }
-  p.hgrid = p.coop_head ? head_coop_grid(R, K) : p.wave_head ? head_wave_grid(R) : head_grid(R);
+  {
+    HeadArgs hc{};
+    hc.K = K; hc.U = p.U; hc.TH = p.TH; hc.D = D; hc.R = R;
+    p.strip_head = p.coop_head && strip_head_on() && strip_fwd_shapes_ok(D, H, H2, K, R) && strip_head_supported(hc);
+  }
+  p.hgrid = p.strip_head ? strip_fwd_grid(R)
+            : p.coop_head ? head_coop_grid(R, K) : p.wave_head ? head_wave_grid(R) : head_grid(R);
   p.dpar = c.take<float>(R * ld4(2 * D));
   p.dqx = c.take<float>(R * ld4(K));
   p.dlx = c.take<float>(R * ld4(K));
@@ -520,11 +551,7 @@ bool front_fused(const ElboPlan& p, const float* const* w, int st) {
 // The four forward convolutions as one strip launch (strip.hip) where its shapes apply; VQHMM_STRIP=0
 // keeps the two pair launches (A/B), read once
 bool strip_fwd_on(const ElboPlan& p) {
-  static const bool on = [] {
-    const char* e = getenv("VQHMM_STRIP");
-    return !e || atoi(e) != 0;
-  }();
-  return on && strip_fwd_supported(conv_of(p, nullptr, S_ENC1), conv_of(p, nullptr, S_ENC2),
+  return strip_fwd_env() && strip_fwd_supported(conv_of(p, nullptr, S_ENC1), conv_of(p, nullptr, S_ENC2),
                                    conv_of(p, nullptr, S_DEC1), conv_of(p, nullptr, S_DEC2));
 }
 
@@ -585,6 +612,20 @@ bool tail_fused_on() {
   return v;
 }
 
+HeadArgs head_args(const ElboPlan& p, const StepCtx& c) {
+  const float* const* w = c.w;
+  HeadArgs h{};
+  h.B = p.B; h.T = p.T; h.R = p.R; h.D = p.D; h.K = p.K; h.U = p.U; h.TH = p.TH;
+  h.x = p.xp; h.u = p.up;
+  h.lengths = c.lengths; h.par = p.par; h.logits = p.logits; h.q = p.q;
+  h.W1 = w[TN0_W]; h.b1 = w[TN0_B]; h.W2 = w[TN2_W]; h.b2 = w[TN2_B]; h.log_prior = w[LOG_PRIOR];
+  h.beta = c.beta; h.norm = c.norm; h.need_grad = c.need_grad;
+  if (c.need_grad == 2 && !c.norm) h.cnt_in = p.cnt;  // the prologue counted the batch (S_TOPCL)
+  h.dpar = p.dpar; h.dqx = p.dqx; h.dlx = p.dlx; h.part = p.part;
+  h.slab_W1 = p.sW1; h.slab_b1 = p.sb1; h.slab_W2 = p.sW2; h.slab_b2 = p.sb2; h.slab_q0 = p.sq0;
+  return h;
+}
+
 int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
   const float* const* w = c.w;
   switch (st) {
@@ -610,10 +651,13 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       if (front_fused(p, w, st + 1)) return VQHMM_OK;  // runs inside the next conv's launch
       return launch_conv(conv_of(p, w, st), s);
     case S_ENC2: case S_DEC2:
-      if (strip_fwd_on(p))
-        return st == S_DEC2 ? VQHMM_OK
-                            : launch_strip_fwd(conv_of(p, w, S_ENC1), conv_of(p, w, S_ENC2), conv_of(p, w, S_DEC1),
-                                               conv_of(p, w, S_DEC2), s);
+      if (strip_fwd_on(p)) {
+        if (st == S_DEC2) return VQHMM_OK;
+        const HeadArgs h = head_args(p, c);
+        return launch_strip_fwd(conv_of(p, w, S_ENC1), conv_of(p, w, S_ENC2), conv_of(p, w, S_DEC1), conv_of(p, w, S_DEC2),
+                                p.strip_head ? &h : nullptr, s);
+      }
+      if (p.strip_head) return VQHMM_EUNSUPPORTED;  // planned with the head in the strip: must not happen
       if (front_fused(p, w, st)) return launch_conv2_fused(fused_pair(p, w, st), s);
       return launch_conv(conv_of(p, w, st), s);
     case S_DEC2_DG:
@@ -648,15 +692,8 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
     }
     case S_HEAD: {
       if (p.staged) return run_staged_head(p, c, w, s);
-      HeadArgs h{};
-      h.B = p.B; h.T = p.T; h.R = p.R; h.D = p.D; h.K = p.K; h.U = p.U; h.TH = p.TH;
-      h.x = p.xp; h.u = p.up;
-      h.lengths = c.lengths; h.par = p.par; h.logits = p.logits; h.q = p.q;
-      h.W1 = w[TN0_W]; h.b1 = w[TN0_B]; h.W2 = w[TN2_W]; h.b2 = w[TN2_B]; h.log_prior = w[LOG_PRIOR];
-      h.beta = c.beta; h.norm = c.norm; h.need_grad = c.need_grad;
-      if (c.need_grad == 2 && !c.norm) h.cnt_in = p.cnt;  // the prologue counted the batch (S_TOPCL)
-      h.dpar = p.dpar; h.dqx = p.dqx; h.dlx = p.dlx; h.part = p.part;
-      h.slab_W1 = p.sW1; h.slab_b1 = p.sb1; h.slab_W2 = p.sW2; h.slab_b2 = p.sb2; h.slab_q0 = p.sq0;
+      if (p.strip_head) return VQHMM_OK;  // in S_ENC2's strip launch
+      const HeadArgs h = head_args(p, c);
       if (p.coop_head) return launch_head_coop(h, p.hgrid, s);
       if (p.wave_head) return launch_head_wave(h, p.hgrid, s);
       return launch_head(h, p.hgrid, s);
@@ -827,21 +864,24 @@ int vqhmm_elbo_stage_info(const vqhmm_dims_t* d, int64_t B, int64_t T, int stage
                            front_fused(plan_elbo(d, B, T, reinterpret_cast<void*>(4096)), nullptr, pair_of);
   const bool bwd_pair = bwd_pair_fused(plan_elbo(d, B, T, reinterpret_cast<void*>(4096)), nullptr, nullptr);
   const bool strip = strip_fwd_on(plan_elbo(d, B, T, reinterpret_cast<void*>(4096)));
-  const bool in_strip = strip && (stage == S_ENC1 || stage == S_ENC2 || stage == S_DEC1 || stage == S_DEC2);
+  const bool in_strip = strip && (stage == S_ENC1 || stage == S_ENC2 || stage == S_DEC1 || stage == S_DEC2 ||
+                                   (p.strip_head && stage == S_HEAD));
   const bool bstrip = strip_bwd_on(plan_elbo(d, B, T, reinterpret_cast<void*>(4096)));
   const bool in_bstrip = bstrip && (stage == S_PAR_DG || stage == S_DEC2_DG || stage == S_DEC1_DG ||
                                     stage == S_LOGIT_BWD || stage == S_LOGIT_DG || stage == S_ENC2_DG);
   if (name && name_len) {
     const char* nm = kStageNames[stage];
     if (in_strip)
-      nm = stage == S_ENC2 ? "strip_fwd(enc_conv1+enc_conv2+to_logits+dec_conv1+dec_conv2+to_params)"
-                           : "(in strip_fwd)";
+      nm = stage != S_ENC2 ? "(in strip_fwd)"
+           : p.strip_head ? "strip_fwd(enc_conv1+enc_conv2+to_logits+dec_conv1+dec_conv2+to_params+elbo_head)"
+                          : "strip_fwd(enc_conv1+enc_conv2+to_logits+dec_conv1+dec_conv2+to_params)";
+    if (p.strip_head && stage == S_HEAD) nm = "(elbo_head: in strip_fwd)";
     if (in_bstrip)
       nm = stage == S_ENC2_DG ? "strip_bwd(to_params_dgrad+dec_conv2_dgrad+dec_conv1_dgrad+logits_bwd+to_logits_dgrad+enc_conv2_dgrad)"
                               : "(in strip_bwd)";
     if (p.wgroup && stage == S_W_ENC1) nm = "wgrad_group(all 6 weight gradients)";
     else if (p.wgroup && stage >= S_W_PAR && stage < S_W_ENC1) nm = "(wgrad: in wgrad_group)";
-    else if (in_strip || in_bstrip) {
+    else if (in_strip || in_bstrip || (p.strip_head && stage == S_HEAD)) {
     } else if (fused_front && (stage == S_ENC1 || stage == S_DEC1 || stage == S_PAR_DG))
       nm = stage == S_ENC1 ? "(enc_conv1: in enc_conv2's launch)"
            : stage == S_DEC1 ? "(dec_conv1: in dec_conv2's launch)" : "(to_params_dgrad: in dec_conv2_dgrad's launch)";
@@ -871,6 +911,13 @@ int vqhmm_elbo_stage_info(const vqhmm_dims_t* d, int64_t B, int64_t T, int stage
       }
       const double R = (double)p.R;
       b = 4.0 * R * (ld4(p.D) + ld4(p.H) + ld4(p.H2) + 2 * ld4(p.K) + 2 * ld4(p.H) + ld4(2 * p.D));
+      if (p.strip_head) {  // + the head: its flops; HBM: u in, dpar / dqx / dlx out (its other inputs are on chip)
+        double f1, b1;
+        int m1;
+        stage_work(p, S_HEAD, &f1, &b1, &m1);
+        f += f1;
+        b += 4.0 * R * (ld4(p.U) + ld4(2 * p.D) + 2 * ld4(p.K));
+      }
     }
   } else if (in_bstrip) {  // S_ENC2_DG's launch does all six; HBM: dpar, the masks, q / dqx / dlx, h2 in, grads out
     f = 0; b = 0;

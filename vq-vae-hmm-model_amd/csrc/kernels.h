@@ -224,7 +224,12 @@ int launch_conv2(const ConvArgs& a, hipStream_t s);
 // -> dec_conv2 + to_params in ONE launch over 128-row strips, the activations between layers in LDS
 // (the four ConvArgs of the separate launches; packed-tap fronts, H = 64, H2 <= 32, K <= 4, 2D <= 16)
 bool strip_fwd_supported(const ConvArgs& e1, const ConvArgs& e2, const ConvArgs& d1, const ConvArgs& d2);
-int launch_strip_fwd(const ConvArgs& e1, const ConvArgs& e2, const ConvArgs& d1, const ConvArgs& d2, hipStream_t s);
+// h (nullable): the ELBO head fused after the decoder (strip_head_supported: K <= 4, U <= 4, TH in {64, 128},
+// D <= 8); its slabs / loss partials have strip_fwd_grid(R) rows
+bool strip_head_supported(const HeadArgs& h);
+int strip_fwd_grid(int64_t R);
+int launch_strip_fwd(const ConvArgs& e1, const ConvArgs& e2, const ConvArgs& d1, const ConvArgs& d2, const HeadArgs* h,
+                     hipStream_t s);
 // Backward strip kernel (strip.hip): to_params dgrad -> dec_conv2 dgrad -> composed dec_conv1 dgrad +
 // softmax backward + to_logits dgrad -> enc_conv2 dgrad in ONE launch (the four ConvArgs of those launches;
 // f = dec_conv1's ACT 3 args with lb_dh; H = 64, H2 in (16, 32], K <= 4, 2D <= 16)

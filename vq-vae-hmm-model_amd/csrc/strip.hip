@@ -54,13 +54,33 @@ struct StripFwdLds {
   static constexpr int NW2 = 16 * NB2;
   float We2[3 * NW2 * ST_LDW];  // enc_conv2 image
   float Wd2[3 * 64 * ST_LDW];   // dec_conv2 image
-  float Wf[2][3 * 64 * 8];      // enc_conv1 / dec_conv1 images, channels 0..7 ([tap][n][8])
   float Ee2[NW2 * 17 + 16];     // enc_conv2 bias | to_logits weight (16 x NW2) | bias
   float Ed2[64 * 17 + 16];      // dec_conv2 bias | to_params weight (16 x 64) | bias
-  float bf[2][64];              // enc_conv1 / dec_conv1 bias
+  float Wf[2][3 * 64 * 8];      // enc_conv1 / dec_conv1 images, channels 0..7 ([tap][n][8])
+  float bf[2][64];              // enc_conv1 / dec_conv1 bias (Wf | bf: the fused head's weights after startup)
   float Xx[ST_XR * ST_XLD];     // x rows s0 - 2 .. s0 + 129
   float Xq[ST_XR * ST_XLD];     // q rows s0 - 2 .. s0 + 129 (the 2 + 2 outer rows stay zero)
   float slot[8][18 * ST_LDW];   // per wave: the 64-wide conv's 18 input rows rb - 1 .. rb + 16
+  unsigned long long hcnt[8];   // fused head: per-wave valid counts
+};
+
+// The fused ELBO head's LDS (strip_fwd_kernel with HTH > 0): per strip in the slots region (free after
+// dec_conv2's loops), the Prior MLP weights in the constants' region (free once they are in registers).
+template <int TH>
+struct StripHeadW {
+  static constexpr int LDW2 = TH + 4;
+  float W2S[16 * LDW2];  // rows ij >= K^2 zero
+  float W1S[TH * 8];     // W1' = [W1 | b1 | 0]
+};
+struct StripHeadLds {
+  static constexpr int LDL = 20;  // lgS / dlgS row stride (16 ij + 4)
+  float uS[ST_WIN * 8];           // u' = [u, 1 at column U, 0]
+  float lgS[ST_WIN * LDL];        // transition logits of the window's rows
+  float dlgS[ST_WIN * LDL];       // their gradients (zero for ij >= K^2, non-owned rows)
+  float aS[ST_WIN * 4];           // A_i = sum_j q[j] log_A[i][j] per row
+  float wS[ST_WIN];               // pair weight (t - 1, t) per row
+  double red[8][4];
+  float q0w[8][4];
 };
 
 // row_bt's validity test with 32-bit arithmetic (R < 2^31): PCL row r is a sequence position
@@ -198,7 +218,10 @@ __device__ __forceinline__ void tail_epi(f32x4 (&acc)[NB], const TailConsts<NB>&
 #pragma unroll
     for (int v = 0; v < 4; ++v) qv[v] = valid ? e[v] / s : 0.f;
     if (st && c0 < ldt) *reinterpret_cast<f32x4*>(q_out + r * ldt + c0) = qv;
-    if (c0 < ST_XLD) *reinterpret_cast<f32x4*>(xq + l16 * ST_XLD + c0) = qv;
+    if (c0 == 0) {  // K <= 4: channels 0..3 of the row; the fused head reads the logits from 4..7
+      *reinterpret_cast<f32x4*>(xq + l16 * ST_XLD) = qv;
+      *reinterpret_cast<f32x4*>(xq + l16 * ST_XLD + 4) = z;
+    }
   }
 }
 
@@ -214,14 +237,45 @@ __device__ __forceinline__ float es_val(const float* bias, int N, const float* t
   return c2 < C2 ? tb[c2] : 0.f;
 }
 
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __builtin_bit_cast(float, dpp_u32<CTRL>(__builtin_bit_cast(uint32_t, v)));
+}
+// reductions over the 4 lanes of a head row (lane % 4 = source state), as head_coop.hip's row_* (KP = 4)
+__device__ __forceinline__ float row4_sum(float v) {
+  v += dppf<0xB1>(v);
+  v += dppf<0x4E>(v);
+  return v;
+}
+__device__ __forceinline__ float row4_max(float v) {
+  v = fmaxf(v, dppf<0xB1>(v));
+  v = fmaxf(v, dppf<0x4E>(v));
+  return v;
+}
+__device__ __forceinline__ float row4_reduce_scatter(const float (&c)[4], int i) {
+  const bool hi2 = i & 2, hi1 = i & 1;
+  float h2[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const float send = hi2 ? c[k] : c[2 + k];
+    h2[k] = (hi2 ? c[2 + k] : c[k]) + dppf<0x4E>(send);
+  }
+  const float send = hi1 ? h2[0] : h2[1];
+  return (hi1 ? h2[1] : h2[0]) + dppf<0xB1>(send);
+}
+
 __device__ __forceinline__ void dma16(const float* src, float* dst) {
   __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint32_t*>(src), (__attribute__((address_space(3))) void*)dst,
                                    16, 0, 0);
 }
 }  // namespace
 
-template <int NB2, int PROF>
-__global__ __launch_bounds__(512) void strip_fwd_kernel(StripFwdArgs a) {
+// HTH > 0: the ELBO head (head_coop.hip's phases, VQ_VAE_HMM_fixed.py:59-71 Prior MLP, :106-137 loss) runs
+// on each strip's owned rows after its decoder, on the activations still in LDS (q, logits) or just written
+// (mu | logvar): K <= 4, U <= 4, TH = HTH in {64, 128}, D <= 8; h = the head launch's arguments, its slabs
+// and loss partials indexed by workgroup (grid = the head's slab count).
+template <int NB2, int PROF, int HTH>
+__global__ __launch_bounds__(512) void strip_fwd_kernel(StripFwdArgs a, HeadArgs h) {
   using S = StripFwdLds<NB2>;
   constexpr int NW2 = S::NW2;
   extern __shared__ float4 smem4[];
@@ -249,6 +303,37 @@ __global__ __launch_bounds__(512) void strip_fwd_kernel(StripFwdArgs a) {
     }
   };
 
+  // ---- fused head (HTH > 0): thread = (row prow, source state si) in the head phases
+  constexpr int HKP = 4, HB = HTH > 0 ? HTH / 16 : 1, HLDW2 = HTH + 4, HNW = HTH > 0 ? 16 * HLDW2 + HTH * 8 : 1;
+  constexpr int HNJ = (HNW + 511) / 512;
+  const int prow = tid >> 2, si = tid & 3;
+  float hwv[HNJ];  // the Prior MLP weights as StripHeadW lays them out (LDS after the first q exchange)
+  if constexpr (HTH > 0) {
+    const int KK = h.K * h.K;
+#pragma unroll
+    for (int j = 0; j < HNJ; ++j) {
+      const int i = tid + 512 * j;
+      float v = 0.f;
+      if (i < 16 * HLDW2) {
+        const int ij = i / HLDW2, hh = i - ij * HLDW2;
+        v = (ij < KK && hh < HTH) ? h.W2[ij * HTH + hh] : 0.f;
+      } else if (i < HNW) {
+        const int k = i - 16 * HLDW2, hh = k >> 3, c = k & 7;
+        v = c < h.U ? h.W1[hh * h.U + c] : (c == h.U ? h.b1[hh] : 0.f);
+      }
+      hwv[j] = v;
+    }
+    if (!h.norm && !h.cnt_in) {  // valid positions of the batch (mask.sum(), :120)
+      unsigned long long c = 0;
+      for (int64_t b = tid; b < h.B; b += 512) {
+        const int64_t L = h.lengths[b];
+        c += (unsigned long long)(L <= 0 ? 0 : (L < T ? L : T));
+      }
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o);
+      if (lane == 0) sh.hcnt[wave] = c;
+    }
+  }
   stamp<PROF>(0);
   // ---- once.  vmcnt retires in order, so: the front images (LDS DMA) first, then x and the epilogue
   // constants (registers), then the two 64-wide images (LDS DMA): waiting for x / the constants never
@@ -283,11 +368,13 @@ __global__ __launch_bounds__(512) void strip_fwd_kernel(StripFwdArgs a) {
       if (i < (first ? N1 : N2)) dma16((first ? a.img_e2 : a.img_d2) + 4 * i, (first ? sh.We2 : sh.Wd2) + cc * 256);
     }
   }
-  static_assert(offsetof(S, Ed2) == offsetof(S, Ee2) + NE * 4 && offsetof(S, bf) == offsetof(S, Ed2) + ND * 4,
-                "constant blocks must be contiguous");
+  static_assert(offsetof(S, Ed2) == offsetof(S, Ee2) + NE * 4, "constant blocks must be contiguous");
 #pragma unroll
-  for (int j = 0; j < NCJ; ++j)
-    if (tid + 512 * j < NC) sh.Ee2[tid + 512 * j] = cv[j];
+  for (int j = 0; j < NCJ; ++j) {
+    const int i = tid + 512 * j;
+    if (i < NE + ND) sh.Ee2[i] = cv[j];
+    else if (i < NC) sh.bf[0][i - NE - ND] = cv[j];
+  }
   if (tid < 4 * ST_XLD) sh.Xq[(tid < 2 * ST_XLD ? 0 : (ST_XR - 4) * ST_XLD) + tid] = 0.f;  // rows never written
   store_x(s * ST_OWN - ST_HALO, px);
   lds_barrier();  // LDS only: the big images stay in flight (the front images are older than x: landed)
@@ -303,10 +390,37 @@ __global__ __launch_bounds__(512) void strip_fwd_kernel(StripFwdArgs a) {
     bE[nb] = f32x4{e4.x, e4.y, e4.z, e4.w};
     bD[nb] = f32x4{d4.x, d4.y, d4.z, d4.w};
   }
+  // the tail epilogues' constants: registers, or (with the fused head, whose phases need the registers)
+  // re-read from LDS for every tile
   TailConsts<NB2> kE;
   TailConsts<4> kD;
-  kE.load(sh.Ee2, lg4, l16);
-  kD.load(sh.Ed2, lg4, l16);
+  if constexpr (HTH == 0) {
+    kE.load(sh.Ee2, lg4, l16);
+    kD.load(sh.Ed2, lg4, l16);
+  }
+  static_assert(HTH == 0 || (offsetof(S, Xx) == offsetof(S, bf) + 2 * 64 * 4 &&
+                             sizeof(StripHeadW<HTH>) <= offsetof(S, Xx) - offsetof(S, Wf) &&
+                             sizeof(StripHeadLds) <= sizeof(float) * 8 * 18 * ST_LDW),
+                "the head's LDS fits the regions it reuses");
+  float lp_i = 0.f, inv_n = 1.f, cpri = 0.f, cent = 0.f;
+  const bool hgrad = h.need_grad != 0;
+  if constexpr (HTH > 0) {
+    unsigned long long cnt;
+    if (h.norm) cnt = (unsigned long long)h.norm[0];
+    else if (h.cnt_in) cnt = (unsigned long long)*h.cnt_in;
+    else cnt = ((((((sh.hcnt[0] + sh.hcnt[1]) + sh.hcnt[2]) + sh.hcnt[3]) + sh.hcnt[4]) + sh.hcnt[5]) + sh.hcnt[6]) + sh.hcnt[7];
+    inv_n = 1.0f / fmaxf((float)(cnt * (unsigned long long)h.D), 1.0f);
+    const float Bn = loss_norm_batch(h.norm, h.B);
+    cpri = -h.beta / Bn;
+    cent = h.beta / Bn;
+    float m = -__builtin_inff();
+    for (int k = 0; k < h.K; ++k) m = fmaxf(m, h.log_prior[k]);
+    float se = 0.f;
+    for (int k = 0; k < h.K; ++k) se += __expf(h.log_prior[k] - m);
+    if (si < h.K) lp_i = h.log_prior[si] - (m + __logf(se));
+  }
+  float s_rec = 0.f, s_ent = 0.f, s_tr = 0.f, s_init = 0.f, q0acc = 0.f, db2acc = 0.f;
+  f32x4 gW2 = f32x4{0.f, 0.f, 0.f, 0.f}, gW1 = gW2;  // this wave's hidden block (hb = wave, HB <= 8)
 
   // this wave's block: window rows 16 w .. 16 w + 15.  Stored rows (window rows ST_HALO .. ST_HALO +
   // ST_OWN - 1): the 64-wide convs' l16 range; the fronts' block A (rows 16w - 1 + l16) stores rows
@@ -347,11 +461,20 @@ __global__ __launch_bounds__(512) void strip_fwd_kernel(StripFwdArgs a) {
       f32x4 y[NB2];
 #pragma unroll
       for (int nb = 0; nb < NB2; ++nb) y[nb] = acc[nb][0];
+      if constexpr (HTH > 0) kE.load(sh.Ee2, lg4, l16);
       tail_epi<NB2, true>(y, kE, rb, R, T, lg4, l16, slo, shi, a.H2, a.h2e, a.K, a.logits, a.q,
                           sh.Xq + (16 * wave + 2) * ST_XLD, nost);
     }
     lds_barrier();  // q of every block; everyone is done with Xx
     if (it == 0) stamp<PROF>(2);
+    if constexpr (HTH > 0) {
+      if (it == 0) {  // every wave read its constants into registers before this strip: the region is free
+        float* hw = &sh.Wf[0][0];
+#pragma unroll
+        for (int j = 0; j < HNJ; ++j)
+          if (tid + 512 * j < HNW) hw[tid + 512 * j] = hwv[j];
+      }
+    }
     // ---- composed dec_conv1 + ReLU for rows rb - 1 .. rb + 16 (g1: owned rows) -> slot
     {
       f32x4 acc[4], acc2[4];
@@ -384,6 +507,7 @@ __global__ __launch_bounds__(512) void strip_fwd_kernel(StripFwdArgs a) {
           stamp<PROF>(5);
         }
       }
+      if constexpr (HTH > 0) kD.load(sh.Ed2, lg4, l16);
       tail_epi<4, false>(y, kD, rb, R, T, lg4, l16, slo, shi, 64, a.g2, a.P, a.par, nullptr, nullptr, nost);
     }
     if (it == 0) stamp<PROF>(6);
@@ -392,9 +516,249 @@ __global__ __launch_bounds__(512) void strip_fwd_kernel(StripFwdArgs a) {
       const int64_t nx = s + gridDim.x;
       store_x((nx < a.nstrip ? nx : s) * ST_OWN - ST_HALO, px);
     }
-    lds_barrier();  // Xx written; Xq and the slots free again
+    if constexpr (HTH > 0) __syncthreads();  // + mu | logvar (HBM) of every block, for the head
+    else lds_barrier();                      // Xx written; Xq and the slots free again
     if (it == 0) stamp<PROF>(3);
+    if constexpr (HTH > 0) {
+      // ================= fused ELBO head on window rows ST_HALO .. ST_HALO + ST_OWN (the last one = the
+      // halo row whose log_A the last owned row's t -> t+1 term needs): head_coop.hip's phases, WR = 128
+      StripHeadLds& hs = *reinterpret_cast<StripHeadLds*>(&sh.slot[0][0]);
+      const StripHeadW<HTH>& hw = *reinterpret_cast<const StripHeadW<HTH>*>(&sh.Wf[0][0]);
+      constexpr int LDL = StripHeadLds::LDL;
+      const int K = h.K, U = h.U, D = h.D, KK = K * K;
+      const int ldp = ld4(2 * D), ldxh = ld4(D), ldu = ld4(U);
+      const int64_t r = s0 + ST_HALO + prow;
+      const unsigned Tp = (unsigned)T + 2u;
+      const unsigned rcl = (unsigned)(r < R ? r : R - 1);
+      const int b = (int)(rcl / Tp);
+      const int t = (int)(rcl - (unsigned)b * Tp) - 1;
+      const bool valid = r < R && prow <= ST_OWN && t >= 0 && t < T;
+      const bool own = prow < ST_OWN && r < R;
+      const int64_t L = h.lengths[b];
+      const bool m = valid && t < L;
+      const float wgt = (valid && t >= 1 && t < L) ? 1.f : 0.f;  // pair (t-1, t) inside the length
+      const float* qrow = sh.Xq + (ST_HALO + prow + 2) * ST_XLD;  // q | logits of the row
+      float qv[HKP];
+#pragma unroll
+      for (int k = 0; k < HKP; ++k) qv[k] = (valid && k < K) ? qrow[k] : 0.f;
+      const float qp = (valid && t >= 1 && si < K) ? qrow[si - ST_XLD] : 0.f;  // q[t-1][i]
+      float qi = 0.f;
+#pragma unroll
+      for (int k = 0; k < HKP; ++k) qi = si == k ? qv[k] : qi;
+      float mu[2], lv[2], xv[2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int c = min(si + HKP * k, D - 1);
+        mu[k] = h.par[(int64_t)rcl * ldp + c];
+        lv[k] = h.par[(int64_t)rcl * ldp + D + c];
+        xv[k] = h.x[(int64_t)rcl * ldxh + c];
+      }
+      const float uu = h.u[(int64_t)rcl * ldu + min(si, ldu - 1)];
+      // ---- L: u' rows; dlgS's columns past K^2 zero
+#pragma unroll
+      for (int c = si; c < 8; c += HKP) hs.uS[prow * 8 + c] = c < U ? (valid ? uu : 0.f) : (c == U ? 1.f : 0.f);
+      for (int i = tid; i < ST_WIN * LDL; i += 512)
+        if (i % LDL >= KK) hs.dlgS[i] = 0.f;
+      lds_barrier();
+      // ---- A: transition logits lg^T = W2 relu(W1' u'^T) + b2, wave w = row block w (ij block 0: K^2 <= 16)
+      {
+        f32x4 lg;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int ij = 4 * lg4 + v;
+          lg[v] = ij < KK ? h.b2[ij] : 0.f;
+        }
+        const float ub = hs.uS[(wave * 16 + l16) * 8 + lg4];
+#pragma unroll 2
+        for (int hb = 0; hb < HB; ++hb) {
+          const float w1a = lg4 < U ? hw.W1S[(hb * 16 + l16) * 8 + lg4] : 0.f;
+          f32x4 bb;
+#pragma unroll
+          for (int v = 0; v < 4; ++v) bb[v] = hw.W1S[(hb * 16 + 4 * lg4 + v) * 8 + U];
+          const f32x4 w2v = *reinterpret_cast<const f32x4*>(&hw.W2S[l16 * HLDW2 + hb * 16 + 4 * lg4]);
+          const f32x4 hc = mfma16x16x4(w1a, ub, bb);  // hid^T (h x rows), bias start
+#pragma unroll
+          for (int v = 0; v < 4; ++v) lg = mfma16x16x4(w2v[v], relu_f(hc[v]), lg);
+        }
+        *reinterpret_cast<f32x4*>(&hs.lgS[(wave * 16 + l16) * LDL + 4 * lg4]) = lg;
+      }
+      lds_barrier();
+      // ---- B: log_softmax rows, transition term, d log_A -> d logits, recon NLL, entropy, init term
+      float rsj = 0.f;
+      {
+        float la[HKP];
+        float A_i = 0.f;
+        const float* lr = &hs.lgS[prow * LDL + (si < K ? si : 0) * K];
+        float mx = -__builtin_inff();
+#pragma unroll
+        for (int j = 0; j < HKP; ++j) {
+          la[j] = j < K ? lr[j] : 0.f;
+          if (j < K) mx = fmaxf(mx, la[j]);
+        }
+        float se = 0.f;
+#pragma unroll
+        for (int j = 0; j < HKP; ++j)
+          if (j < K) se += __expf(la[j] - mx);
+        const float ls = mx + __logf(se);
+#pragma unroll
+        for (int j = 0; j < HKP; ++j)
+          if (j < K) la[j] -= ls;
+#pragma unroll
+        for (int j = 0; j < HKP; ++j)
+          if (j < K) A_i = fmaf(qv[j], la[j], A_i);
+        if (si >= K) A_i = 0.f;
+        float c[HKP];
+#pragma unroll
+        for (int j = 0; j < HKP; ++j) c[j] = (j < K && si < K) ? qp * la[j] : 0.f;
+        rsj = row4_reduce_scatter(c, si);
+        if (own && si < K) s_tr = fmaf(wgt * qp, A_i, s_tr);
+        hs.aS[prow * HKP + si] = A_i;
+        if (si == 0) hs.wS[prow] = wgt;
+        if (hgrad && si < K) {
+          float qs = 0.f;
+#pragma unroll
+          for (int j = 0; j < HKP; ++j)
+            if (j < K) qs += qv[j];
+          const float g = own ? cpri * wgt * qp : 0.f;
+          const float rs = g * qs;
+          float* dl = &hs.dlgS[prow * LDL + si * K];
+#pragma unroll
+          for (int j = 0; j < HKP; ++j)
+            if (j < K) dl[j] = g * qv[j] - __expf(la[j]) * rs;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int ch = si + HKP * k;
+        float dmu = 0.f, dlv = 0.f;
+        if (own && m && ch < D) {
+          const float ev = __expf(lv[k]);
+          const float var = ev < 1e-8f ? 1e-8f : ev;  // clamp(min=1e-8), NaN stays NaN
+          const float df = mu[k] - xv[k];
+          const float r2 = df * df / var;
+          s_rec += 0.5f * (__logf(6.2831855f * var) + r2);
+          dmu = df / var * inv_n;
+          dlv = (ev >= 1e-8f) ? 0.5f * (1.f - r2) * inv_n : 0.f;
+        }
+        if (hgrad && own && ch < D) {
+          h.dpar[r * ldp + ch] = dmu;
+          h.dpar[r * ldp + D + ch] = dlv;
+        }
+      }
+      if (hgrad && own && 2 * D + si < ldp) h.dpar[r * ldp + 2 * D + si] = 0.f;
+      {
+        const float lgv = (valid && si < K) ? qrow[4 + si] : 0.f;
+        const float mx = row4_max(si < K ? lgv : -__builtin_inff());
+        const float lse = mx + __logf(row4_sum(si < K ? __expf(lgv - mx) : 0.f));
+        const float f = row4_sum(si < K ? qi * (lgv - lse) : 0.f);
+        if (own && m && si == 0) s_ent -= f;
+        if (hgrad && own) h.dlx[r * HKP + si] = (m && si < K) ? cent * qi * ((lgv - lse) - f) : 0.f;
+      }
+      if (own && valid && t == 0 && si < K) {
+        s_init = fmaf(qi, lp_i, s_init);
+        q0acc += qi;
+      }
+      lds_barrier();  // dlgS, aS, wS of every row
+      // ---- B2: dq
+      if (hgrad && own) {
+        float v = cpri * (wgt * rsj + hs.wS[prow + 1] * hs.aS[(prow + 1) * HKP + si]);
+        if (valid && t == 0) v = fmaf(cpri, lp_i, v);
+        h.dqx[r * HKP + si] = (valid && si < K) ? v : 0.f;
+      }
+      // ---- C: MLP backward, wave w = hidden block w
+      if (hgrad) {
+        if (wave == 0) {  // db2: column sums of dlg, ij = l16
+#pragma unroll 8
+          for (int k = 0; k < ST_WIN / 4; ++k) db2acc += hs.dlgS[(lg4 * (ST_WIN / 4) + k) * LDL + l16];
+        }
+        if (wave < HB) {
+          const int hb = wave;
+          const float w1 = hw.W1S[(hb * 16 + l16) * 8 + lg4];
+          const float bb1 = hw.W1S[(hb * 16 + l16) * 8 + U];
+          float w2c[4];
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) w2c[s4] = hw.W2S[(4 * s4 + lg4) * HLDW2 + hb * 16 + l16];
+          const int SD = (KK + 3) / 4;
+#pragma unroll 2
+          for (int rb = 0; rb < ST_WIN / 16; ++rb) {
+            const float ua = lg4 < U ? hs.uS[(rb * 16 + l16) * 8 + lg4] : 0.f;
+            float dla[4], dlt[4], ubv[4];
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) {
+              dla[s4] = s4 < SD ? hs.dlgS[(rb * 16 + l16) * LDL + 4 * s4 + lg4] : 0.f;
+              const int row = rb * 16 + 4 * lg4 + s4;
+              dlt[s4] = hs.dlgS[row * LDL + l16];
+              const float uv = hs.uS[row * 8 + (l16 & 7)];
+              ubv[s4] = l16 < 8 ? uv : 0.f;
+            }
+            const f32x4 hh = mfma16x16x4(ua, w1, f32x4{bb1, bb1, bb1, bb1});  // (rows x h), bias start
+            f32x4 dh = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4)
+              if (s4 < SD) dh = mfma16x16x4(dla[s4], w2c[s4], dh);  // dlg @ W2
+            f32x4 hr, dm;
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+              hr[v] = relu_f(hh[v]);
+              dm[v] = hh[v] > 0.f ? dh[v] : 0.f;
+            }
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) {
+              gW2 = mfma16x16x4(dlt[s4], hr[s4], gW2);  // dlg^T hid
+              gW1 = mfma16x16x4(dm[s4], ubv[s4], gW1);  // dhid^T u'
+            }
+          }
+        }
+      }
+      lds_barrier();  // the head's LDS reads are done before the next strip writes the slots and Xq
+    }
     ++it;
+  }
+  if constexpr (HTH > 0) {
+    // ---- head epilogue: loss partials, q0 / db2 sums, weight-gradient partials (fixed order), as head_coop
+    StripHeadLds& hs = *reinterpret_cast<StripHeadLds*>(&sh.slot[0][0]);
+    double ds[4] = {(double)s_rec, (double)s_init, (double)s_tr, (double)s_ent};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ds[k] = wave_sum_dpp(ds[k]);
+    q0acc += __shfl_xor(q0acc, 4);
+    q0acc += __shfl_xor(q0acc, 8);
+    q0acc += xor16(q0acc);
+    q0acc += xor32(q0acc);
+    db2acc += xor16(db2acc);
+    db2acc += xor32(db2acc);
+    if (lane == 0)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) hs.red[wave][k] = ds[k];
+    if (lane < HKP) hs.q0w[wave][lane] = q0acc;
+    __syncthreads();
+    const int K = h.K, KK = K * K;
+    if (tid < 4) {
+      double v = 0.0;
+      for (int w = 0; w < 8; ++w) v += hs.red[w][tid];
+      h.part[blockIdx.x * 4 + tid] = v;
+    }
+    if (hgrad) {
+      if (tid < K) {
+        float v = 0.f;
+        for (int w = 0; w < 8; ++w) v += hs.q0w[w][tid];
+        h.slab_q0[(int64_t)blockIdx.x * K + tid] = v;
+      }
+      if (wave == 0 && lane < 16 && lane < KK) h.slab_b2[(int64_t)blockIdx.x * KK + lane] = db2acc;
+      if (wave < HB) {
+        float* sW2 = h.slab_W2 + (int64_t)blockIdx.x * KK * HTH;
+        float* sW1 = h.slab_W1 + (int64_t)blockIdx.x * HTH * h.U;
+        float* sb1 = h.slab_b1 + (int64_t)blockIdx.x * HTH;
+        const int hb = wave;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int ij = 4 * lg4 + v;
+          if (ij < KK) sW2[ij * HTH + hb * 16 + l16] = gW2[v];
+          const int hh = hb * 16 + 4 * lg4 + v;  // gW1' lane -> (h, c' = l16); c' == U is db1
+          if (l16 < h.U) sW1[hh * h.U + l16] = gW1[v];
+          else if (l16 == h.U) sb1[hh] = gW1[v];
+        }
+      }
+    }
   }
   if constexpr (PROF > 0) {
     __syncthreads();
@@ -663,17 +1027,34 @@ bool strip_fwd_supported(const ConvArgs& e1, const ConvArgs& e2, const ConvArgs&
 
 int strip_prof_copy(uint64_t* out, int64_t n) { return prof_copy(out, n); }
 
-int launch_strip_fwd(const ConvArgs& e1, const ConvArgs& e2, const ConvArgs& d1, const ConvArgs& d2, hipStream_t s) {
+bool strip_head_supported(const HeadArgs& h) {
+  return h.K >= 1 && h.K <= 4 && h.U >= 1 && h.U <= 4 && (h.TH == 64 || h.TH == 128) && h.D >= 1 && h.D <= 8 &&
+         h.R < (1ll << 31);
+}
+
+int strip_fwd_grid(int64_t R) {
+  const int64_t n = cdiv(R, ST_OWN);
+  return (int)(n < 256 ? (n > 0 ? n : 1) : 256);
+}
+
+int launch_strip_fwd(const ConvArgs& e1, const ConvArgs& e2, const ConvArgs& d1, const ConvArgs& d2, const HeadArgs* h,
+                     hipStream_t s) {
   if (!strip_fwd_supported(e1, e2, d1, d2)) return VQHMM_EUNSUPPORTED;
+  if (h && (!strip_head_supported(*h) || h->K != e2.C2 || h->R != e1.R || h->D != e1.Kc)) return VQHMM_EUNSUPPORTED;
   const StripFwdArgs a = strip_fwd_args(e1, e2, d1, d2);
-  const unsigned grid = (unsigned)(a.nstrip < 256 ? a.nstrip : 256);
-#define VQHMM_SF(NB2, P) strip_fwd_kernel<NB2, P><<<grid, 512, sizeof(StripFwdLds<NB2>), s>>>(a)
+  const unsigned grid = (unsigned)strip_fwd_grid(e1.R);
+  const HeadArgs hv = h ? *h : HeadArgs{};
+  const int hth = h ? h->TH : 0;
+#define VQHMM_SF(NB2, P, HT) strip_fwd_kernel<NB2, P, HT><<<grid, 512, sizeof(StripFwdLds<NB2>), s>>>(a, hv)
+#define VQHMM_SF_H(NB2, P) \
+  if (hth == 128) VQHMM_SF(NB2, P, 128); else if (hth == 64) VQHMM_SF(NB2, P, 64); else VQHMM_SF(NB2, P, 0);
   const bool prof = prof_on() != 0;
   if (c2_nb(e2.N) == 1) {
-    if (prof) VQHMM_SF(1, 1); else VQHMM_SF(1, 0);
+    if (prof) { VQHMM_SF_H(1, 1) } else { VQHMM_SF_H(1, 0) }
   } else {
-    if (prof) VQHMM_SF(2, 1); else VQHMM_SF(2, 0);
+    if (prof) { VQHMM_SF_H(2, 1) } else { VQHMM_SF_H(2, 0) }
   }
+#undef VQHMM_SF_H
 #undef VQHMM_SF
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
