@@ -128,6 +128,7 @@ struct ElboPlan {
   // backward
   float *dg2, *dg1, *dqd, *dlog, *dh2, *dh1, *dWc;
   float *Ecopy, *Wcopy;  // the prologue's copies of decoder.embeddings / decoder.conv1 weights (compose_adam)
+  float* himg;           // the cooperative head's weight image (built by the prologue), or null
   bool wgroup;           // the six weight gradients run as one grouped launch (wgrad2_group)
   int nwl;
   WLayer wl[8];  // 0 to_params, 1 dec2, 2 dec1', 3 to_logits, 4 enc2, 5 enc1, [6 Prior W1, 7 Prior W2]
@@ -207,6 +208,7 @@ ElboPlan plan_elbo(const vqhmm_dims_t* d, int64_t B, int64_t T, void* ws) {
   p.dh2 = c.take<float>(R * ld4(H2));
   p.dh1 = c.take<float>(R * ld4(H));
   p.dWc = c.take<float>((size_t)H * K * 3);
+  p.himg = p.coop_head ? c.take<float>((size_t)head_coop_image_floats(K, p.TH)) : nullptr;
   p.Ecopy = c.take<float>((size_t)K * H);
   p.Wcopy = c.take<float>((size_t)H * H * 3);
   const int shapes[8][3] = {{2 * D, H, 1}, {H, H, 3}, {H, K, 3}, {K, H2, 1}, {H2, H, 3}, {H, D, 3},
@@ -623,6 +625,7 @@ HeadArgs head_args(const ElboPlan& p, const StepCtx& c) {
   if (c.need_grad == 2 && !c.norm) h.cnt_in = p.cnt;  // the prologue counted the batch (S_TOPCL)
   h.dpar = p.dpar; h.dqx = p.dqx; h.dlx = p.dlx; h.part = p.part;
   h.slab_W1 = p.sW1; h.slab_b1 = p.sb1; h.slab_W2 = p.sW2; h.slab_b2 = p.sb2; h.slab_q0 = p.sq0;
+  h.himg = p.himg;  // the prologue built it (S_TOPCL runs in every forward)
   return h;
 }
 
@@ -642,6 +645,9 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       a.Wcopy = p.Wcopy;
       if (c.need_grad == 2 && !c.norm) { a.lengths = c.lengths; a.cnt = p.cnt; }
       a.sync = p.sync;
+      if (p.himg) {
+        a.hW1 = w[TN0_W]; a.hb1 = w[TN0_B]; a.hW2 = w[TN2_W]; a.hTH = p.TH; a.himg = p.himg;
+      }
       return launch_prologue(a, s);
     }
     case S_COMPOSE:  // runs inside S_TOPCL's launch

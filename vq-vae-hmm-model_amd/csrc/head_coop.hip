@@ -16,6 +16,8 @@
 // K <= 4, 40 at K = 8, TH = 128), so there are no cross-wave sums; the slabs have head_wave.hip's
 // layout (same tail reduction).  WR = 256 / KP: 64 rows (4 row blocks) at K <= 4, 32 (2) at K <= 8.
 // Summation order differs from the reference's autograd; the tests hold it to 1e-5 relative.
+#include <stddef.h>
+
 #include "kernels.h"
 #include "prof.h"
 
@@ -150,16 +152,28 @@ __global__ __launch_bounds__(256, 2) void elbo_head_coop_kernel(HeadArgs a) {
   int64_t w = blockIdx.x;
   if (w < nwin) load_row(w * WOWN, cur);
 
-  // ---- one-time: weights to LDS, zero the gradient pads, log_pi, valid count
+  // ---- one-time: weights to LDS (the prologue's image by LDS DMA, waited for by the barrier below, or
+  // packed here), zero the gradient pads, log_pi, valid count
+  static_assert(offsetof(S, W1S) == offsetof(S, W2S) + sizeof(float) * 16 * KB * S::LDW2, "W2S | W1S contiguous");
+  if (a.himg) {
+    constexpr int N4 = (16 * KB * S::LDW2 + TH * 8) / 4;  // float4s (LDW2, TH multiples of 4)
+    for (int c = wave; c * 64 < N4; c += 4) {
+      const int i = c * 64 + lane;
+      if (i < N4)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint32_t*>(a.himg) + 4 * i,
+                                         (__attribute__((address_space(3))) void*)(sh.W2S + c * 256), 16, 0, 0);
+    }
+  } else {
 #pragma unroll 8
-  for (int i = tid; i < 16 * KB * S::LDW2; i += 256) {
-    const int ij = i / S::LDW2, h = i - ij * S::LDW2;
-    sh.W2S[i] = (ij < KK && h < TH) ? a.W2[ij * TH + h] : 0.f;
-  }
+    for (int i = tid; i < 16 * KB * S::LDW2; i += 256) {
+      const int ij = i / S::LDW2, h = i - ij * S::LDW2;
+      sh.W2S[i] = (ij < KK && h < TH) ? a.W2[ij * TH + h] : 0.f;
+    }
 #pragma unroll 8
-  for (int i = tid; i < TH * 8; i += 256) {
-    const int h = i >> 3, c = i & 7;
-    sh.W1S[i] = c < U ? a.W1[h * U + c] : (c == U ? a.b1[h] : 0.f);
+    for (int i = tid; i < TH * 8; i += 256) {
+      const int h = i >> 3, c = i & 7;
+      sh.W1S[i] = c < U ? a.W1[h * U + c] : (c == U ? a.b1[h] : 0.f);
+    }
   }
   for (int i = tid; i < WR * LDL; i += 256) sh.dlgS[i] = 0.f;
   if (tid == 0) sh.cnt = a.norm ? (unsigned long long)a.norm[0] : a.cnt_in ? (unsigned long long)*a.cnt_in : 0ull;
@@ -451,6 +465,8 @@ __global__ __launch_bounds__(256, 2) void elbo_head_coop_kernel(HeadArgs a) {
     if (threadIdx.x == 0 && blockIdx.x < 256) g_prof[blockIdx.x * 16 + 8] = (unsigned long long)nwn;
   }
 }
+
+int64_t head_coop_image_floats(int K, int TH) { return (int64_t)16 * ((K * K + 15) / 16) * (TH + 4) + (int64_t)TH * 8; }
 
 bool head_coop_supported(const HeadArgs& a) {
   return a.K >= 1 && a.K <= 8 && a.U >= 1 && a.U <= 4 && (a.TH == 64 || a.TH == 128 || a.TH == 256) && a.D >= 1 &&

@@ -155,6 +155,7 @@ struct HeadArgs {
   float* slab_W2;        // [grid][K*K*TH]
   float* slab_b2;        // [grid][K*K]
   float* slab_q0;        // [grid][K]  sum_b q[b, :, 0]
+  const float* himg;     // head_coop: the prologue's image of the Prior MLP weights (LDS DMA), or null
   int64_t ntiles;
 };
 
@@ -289,6 +290,8 @@ int launch_head_mfma(const HeadArgs& a, int grid, hipStream_t s);
 // workgroup-cooperative MFMA head (head_coop.hip): K <= 8, U <= 4, TH in {64, 128, 256}, D <= 16; its
 // grid / slab count
 bool head_coop_supported(const HeadArgs& a);
+// floats of the head image the prologue builds for elbo_head_coop_kernel (PrologueArgs::himg)
+int64_t head_coop_image_floats(int K, int TH);
 int head_coop_grid(int64_t R, int K);
 int launch_head_coop(const HeadArgs& a, int grid, hipStream_t s);
 int launch_head(const HeadArgs& a, int grid, hipStream_t s);
@@ -377,6 +380,12 @@ struct PrologueArgs {  // step prologue: x, u -> PCL, the composed decoder conv1
   const int64_t* lengths;  // with cnt: the last block writes the batch's valid count
   int64_t* cnt;            // (sum_b min(max(L_b, 0), T)) for a loss finalized in the backward, or null
   unsigned long long* sync;  // zeroed: the backward tail's in-launch counter (launch_tail), or null
+  // the cooperative head's Prior MLP weights in its LDS layout (head_coop_image_floats), or himg = null:
+  // [W2 rows ij (16 * ceil(K^2 / 16) of them, zero past K^2) x (TH + 4) | W1' = [W1 | b1 | 0] (TH x 8)]
+  const float *hW1, *hb1, *hW2;
+  int hTH;
+  float* himg;
+  unsigned nbh;                     // set by launch_prologue
   unsigned nbx, nbu;                // set by launch_prologue
   unsigned img_blk0[MAX_WIMG + 1];  // set by launch_prologue: first block of each image
 };

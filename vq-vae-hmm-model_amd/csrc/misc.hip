@@ -710,6 +710,23 @@ __device__ __forceinline__ void wimg_slice(const WImgJob& j, int64_t i0) {
   j.img[i] = v;
 }
 
+// One 256-entry slice of the cooperative head's weight image (PrologueArgs::himg, head_coop.hip CoopLds
+// W2S | W1S): 16 * KB rows of W2 (ij >= K^2 zero) with stride TH + 4, then W1' = [W1 | b1 | 0] (TH x 8)
+__device__ __forceinline__ void himg_slice(const PrologueArgs& a, int64_t i0) {
+  const int KK = a.K * a.K, KB = (KK + 15) / 16, TH = a.hTH, LDW2 = TH + 4;
+  const int64_t n2 = (int64_t)16 * KB * LDW2, i = i0 + threadIdx.x;
+  if (i >= n2 + (int64_t)TH * 8) return;
+  float v = 0.f;
+  if (i < n2) {
+    const int ij = (int)(i / LDW2), h = (int)(i - (int64_t)ij * LDW2);
+    v = (ij < KK && h < TH) ? a.hW2[ij * TH + h] : 0.f;
+  } else {
+    const int k = (int)(i - n2), h = k >> 3, c = k & 7;
+    v = c < a.U ? a.hW1[h * a.U + c] : (c == a.U ? a.hb1[h] : 0.f);
+  }
+  a.himg[i] = v;
+}
+
 // Step prologue in ONE launch (the step's first tiny pieces of work): blocks
 // [0, nbx) convert x and [nbx, nbx + nbu) convert u to PCL (to_pcl_kernel), the next H
 // blocks compose the decoder conv1 weight (compose_fwd_kernel), the rest pack the conv
@@ -729,6 +746,8 @@ __global__ __launch_bounds__(256) void prologue_kernel(PrologueArgs a) {
     int j = 0;
     while (j + 1 < a.nimg && ib >= a.img_blk0[j + 1]) ++j;
     wimg_slice(a.img[j], (int64_t)(ib - a.img_blk0[j]) * 256);
+  } else if (bx < a.nbx + a.nbu + (unsigned)a.H + a.img_blk0[a.nimg] + a.nbh) {
+    himg_slice(a, (int64_t)(bx - a.nbx - a.nbu - (unsigned)a.H - a.img_blk0[a.nimg]) * 256);
   } else {  // the batch's valid count mask.sum() (VQ_VAE_HMM_fixed.py:111,:120), fixed order
     __shared__ unsigned long long cred[256];
     unsigned long long c = 0;
@@ -753,8 +772,9 @@ int launch_prologue(PrologueArgs a, hipStream_t s) {
   a.img_blk0[0] = 0;
   for (int j = 0; j < a.nimg; ++j)
     a.img_blk0[j + 1] = a.img_blk0[j] + (unsigned)cdiv(c2_image_floats(a.img[j].N, a.img[j].Kc, a.img[j].ks), 256);
+  a.nbh = a.himg ? (unsigned)cdiv(head_coop_image_floats(a.K, a.hTH), 256) : 0u;
   const size_t lds = (size_t)(a.H * 3 + a.K * a.H) * 4;
-  prologue_kernel<<<a.nbx + a.nbu + (unsigned)a.H + a.img_blk0[a.nimg] + (a.cnt ? 1u : 0u), 256, lds, s>>>(a);
+  prologue_kernel<<<a.nbx + a.nbu + (unsigned)a.H + a.img_blk0[a.nimg] + a.nbh + (a.cnt ? 1u : 0u), 256, lds, s>>>(a);
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
 }
