@@ -600,7 +600,11 @@ bool strip_bwd_on(const ElboPlan& p) {
   }();
   // measured (tools/gpu_stripab.sh): B = 128 0.124 -> 0.116 ms, 256 0.1765 -> 0.1715, 512 0.2784 -> 0.2761,
   // cfg2 (207k rows) 0.462 -> 0.467: below 2^17 rows only, as the backward pair
-  return on && p.R < ((int64_t)1 << 17) && logits_dg_fused(p) &&
+  static const int64_t max_rows = [] {  // A/B: VQHMM_STRIP_BWD_ROWS
+    const char* e = getenv("VQHMM_STRIP_BWD_ROWS");
+    return e ? (int64_t)atoll(e) : (int64_t)1 << 17;
+  }();
+  return on && p.R < max_rows && logits_dg_fused(p) &&
          strip_bwd_supported(conv_of(p, nullptr, S_PAR_DG), conv_of(p, nullptr, S_DEC2_DG), dec1_dg_args(p, nullptr, nullptr),
                              conv_of(p, nullptr, S_ENC2_DG));
 }
