@@ -26,7 +26,7 @@ def run(B, T=200, D=5, H=64, K=3, H2=32):
     m = vqhmm.VAE_HMM(D, H, K, H2, u_dim=4, trans_hidden=128).cuda()
     st = vqhmm.TrainState(m, lr=1e-3)
     xs, us, Ls = st.prepare(x, u, L)
-    for _ in range(5):
+    for _ in range(int(os.environ.get("STRIP_PROF_STEPS", "5"))):
         st.forward_backward(xs, us, Ls, 1.0)
     torch.cuda.synchronize()
     buf = np.zeros(256 * 16, dtype=np.uint64)
@@ -49,6 +49,9 @@ def run(B, T=200, D=5, H=64, K=3, H2=32):
         print("  wave 0, second phase: front %.2f, dec_conv2 loop %.2f, tail %.2f, to barrier %.2f us" % tuple(dw))
         fw = np.median(np.diff(t[:, [2, 10, 11, 4]].astype(np.int64), axis=1), axis=0) * 0.01
         print("    front: LDS reads + 32 MFMAs %.2f, epilogue A %.2f, epilogue B + wave barrier %.2f us" % tuple(fw))
+    if names is NAMES and t[:, 14].max() > 0:  # s_memtime around the launch: the in-kernel clock
+        ghz = (t[:, 14] - t[:, 13]) / ((t[:, 7] - t[:, 0]) * 10.0)
+        print(f"  in-kernel clock median {np.median(ghz):.3f} GHz (min {ghz.min():.3f}, max {ghz.max():.3f})")
     if t[:, 9].max() > 0:  # VQHMM_STRIP_PROF=2: serialised latency probes from the kernel's start
         for k, n in ((9, "x load"), (10, "+ constants"), (11, "+ front weights"), (12, "+ image DMA")):
             print(f"  {n:18s} at {np.median(t[:, k] - t[:, 0]) * 0.01:7.2f} us")

@@ -335,6 +335,7 @@ __global__ __launch_bounds__(512) void strip_fwd_kernel(StripFwdArgs a, HeadArgs
     }
   }
   stamp<PROF>(0);
+  if constexpr (PROF > 0) { if (threadIdx.x == 0 && blockIdx.x < 256) g_prof[blockIdx.x * 16 + 13] = __builtin_amdgcn_s_memtime(); }
   // ---- once.  vmcnt retires in order, so: the front images (LDS DMA) first, then x and the epilogue
   // constants (registers), then the two 64-wide images (LDS DMA): waiting for x / the constants never
   // waits for the big images, which stay in flight through the first enc_conv1.
@@ -763,6 +764,7 @@ __global__ __launch_bounds__(512) void strip_fwd_kernel(StripFwdArgs a, HeadArgs
   if constexpr (PROF > 0) {
     __syncthreads();
     stamp<PROF>(7);
+    if constexpr (PROF > 0) { if (threadIdx.x == 0 && blockIdx.x < 256) g_prof[blockIdx.x * 16 + 14] = __builtin_amdgcn_s_memtime(); }
     if (threadIdx.x == 0 && blockIdx.x < 256) g_prof[blockIdx.x * 16 + 8] = (unsigned long long)it;
   }
 }
