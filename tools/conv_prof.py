@@ -36,7 +36,9 @@ def run(B, T=200, D=5, H=64, K=3, H2=32):
     t0 = t[:, 0].min()
     print(f"B={B}: {len(t)} workgroups, wave-0 {'windows' if HEAD else 'tiles'} {t[:, 8].min()}..{t[:, 8].max()}, span {(t[:, 7].max() - t0) * 0.01:.2f} us, "
           f"start skew {(t[:, 0].max() - t0) * 0.01:.2f} us")
-    ph = ((0, 1, "staging"), (1, 2, "first window"), (2, 3, "other windows"), (3, 7, "slab epilogue")) if HEAD else \
+    ph = ((0, 1, "staging"), (1, 2, "first window"), (1, 9, "  u' to LDS"), (9, 10, "  A: transition logits"),
+          (10, 11, "  B: rows"), (11, 12, "  B2: dq + prefetch"), (12, 2, "  C: MLP backward"),
+          (2, 3, "other windows"), (3, 7, "slab epilogue")) if HEAD else \
         ((0, 1, "staging"), (1, 2, "first tile (wave 0)"), (2, 7, "rest + drain"))
     for a, b, n in ph:
         d = (t[:, b] - t[:, a]) * 0.01

@@ -40,6 +40,7 @@ struct CoopLds {
   float dlgS[WR * LDL];                          // their gradients (zero for ij >= KK, non-owned rows)
   float aS[WR * KP];                             // A_i = sum_j q[j] log_A[i][j] per row (next row's dq)
   float wS[WR];                                  // pair weight (t-1, t) per row
+  float b2S[16 * KB];                            // b2, zero for ij >= KK (phase A's accumulator start)
   double red[4][4];
   float q0w[4][KP];
   unsigned long long cnt;
@@ -176,6 +177,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_coop_kernel(HeadArgs a) {
     }
   }
   for (int i = tid; i < WR * LDL; i += 256) sh.dlgS[i] = 0.f;
+  for (int i = tid; i < 16 * KB; i += 256) sh.b2S[i] = i < KK ? a.b2[i] : 0.f;
   if (tid == 0) sh.cnt = a.norm ? (unsigned long long)a.norm[0] : a.cnt_in ? (unsigned long long)*a.cnt_in : 0ull;
   float lp_i = 0.f;  // log_pi[i]
   {
@@ -200,6 +202,37 @@ __global__ __launch_bounds__(256, 2) void elbo_head_coop_kernel(HeadArgs a) {
   const float inv_n = 1.0f / fmaxf((float)(sh.cnt * (unsigned long long)D), 1.0f);
   stamp_if(a.dbg & 16, 1);
   int nwn = 0;
+  // AREG (one phase-A task per wave, TH <= 128): the wave's phase-A operands (W1' column block, b1, its
+  // W2 ij block, b2) are window-invariant, so they live in registers for the whole launch and the
+  // per-window chain is MFMAs and ReLUs only
+  constexpr bool AREG = KB != 4 && NT <= 4 && HB <= 8;
+  constexpr int NAR = AREG ? HB : 1;
+  float w1r[NAR];
+  f32x4 bbr[NAR], w2r[NAR], b2r;
+  if constexpr (AREG) {
+    const int ijb = wave % KB;
+#pragma unroll
+    for (int hb = 0; hb < HB; ++hb) {
+      w1r[hb] = lg4 < U ? sh.W1S[(hb * 16 + l16) * 8 + lg4] : 0.f;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) bbr[hb][v] = sh.W1S[(hb * 16 + 4 * lg4 + v) * 8 + U];
+      w2r[hb] = *reinterpret_cast<const f32x4*>(&sh.W2S[(ijb * 16 + l16) * S::LDW2 + hb * 16 + 4 * lg4]);
+    }
+#pragma unroll
+    for (int v = 0; v < 4; ++v) b2r[v] = sh.b2S[16 * ijb + 4 * lg4 + v];
+  }
+  // CREG: phase C's weight operands of this wave's hidden blocks in registers too (window-invariant)
+  constexpr bool CREG = HBW * SD <= 8;
+  float w1c[HBW], bb1c[HBW], w2c[HBW][CREG ? SD : 1];
+  if constexpr (CREG)
+#pragma unroll
+    for (int hl = 0; hl < HBW; ++hl) {
+      const int hb = wave * HBW + hl;
+      w1c[hl] = sh.W1S[(hb * 16 + l16) * 8 + lg4];
+      bb1c[hl] = sh.W1S[(hb * 16 + l16) * 8 + U];
+#pragma unroll
+      for (int s = 0; s < SD; ++s) w2c[hl][s] = sh.W2S[(4 * s + lg4) * S::LDW2 + hb * 16 + l16];
+    }
 
   float s_rec = 0.f, s_ent = 0.f, s_tr = 0.f, s_init = 0.f, q0acc = 0.f, db2acc = 0.f;
   f32x4 gW2[KB][HBW], gW1[HBW];
@@ -234,6 +267,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_coop_kernel(HeadArgs a) {
 #pragma unroll
     for (int c = si; c < 8; c += KP) sh.uS[prow * 8 + c] = c < U ? (valid ? cur.u : 0.f) : (c == U ? 1.f : 0.f);
     lds_barrier();
+    if (nwn == 0) stamp_if(a.dbg & 16, 9);
     // ---------------- A: tasks (ij block, 16-row block) over the waves; with 4 ij blocks (K > 6) wave w
     // takes block w for every row block in one pass (the W2 operands read once for all of them)
     if constexpr (KB == 4) {
@@ -244,7 +278,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_coop_kernel(HeadArgs a) {
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
           const int ij = 16 * wave + 4 * lg4 + v;
-          lg[rb][v] = ij < KK ? a.b2[ij] : 0.f;
+          lg[rb][v] = sh.b2S[ij];
         }
         ub[rb] = sh.uS[(rb * 16 + l16) * 8 + lg4];
       }
@@ -266,6 +300,19 @@ __global__ __launch_bounds__(256, 2) void elbo_head_coop_kernel(HeadArgs a) {
 #pragma unroll
       for (int rb = 0; rb < NRB; ++rb)
         *reinterpret_cast<f32x4*>(&sh.lgS[(rb * 16 + l16) * LDL + wave * 16 + 4 * lg4]) = lg[rb];
+    } else if constexpr (AREG) {
+      if (wave < NT) {
+        const int ijb = wave % KB, rb = wave / KB;
+        f32x4 lg = b2r;
+        const float ub = sh.uS[(rb * 16 + l16) * 8 + lg4];
+#pragma unroll
+        for (int hb = 0; hb < HB; ++hb) {
+          const f32x4 hc = mfma16x16x4(w1r[hb], ub, bbr[hb]);  // hid^T (h x rows), bias start
+#pragma unroll
+          for (int v = 0; v < 4; ++v) lg = mfma16x16x4(w2r[hb][v], relu_f(hc[v]), lg);
+        }
+        *reinterpret_cast<f32x4*>(&sh.lgS[(rb * 16 + l16) * LDL + ijb * 16 + 4 * lg4]) = lg;
+      }
     } else
     for (int tk = wave; tk < NT; tk += 4) {
       const int ijb = tk % KB, rb = tk / KB;
@@ -273,7 +320,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_coop_kernel(HeadArgs a) {
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         const int ij = 16 * ijb + 4 * lg4 + v;
-        lg[v] = ij < KK ? a.b2[ij] : 0.f;
+        lg[v] = sh.b2S[ij];
       }
       const float ub = sh.uS[(rb * 16 + l16) * 8 + lg4];
 #pragma unroll 2
@@ -291,6 +338,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_coop_kernel(HeadArgs a) {
       *reinterpret_cast<f32x4*>(&sh.lgS[(rb * 16 + l16) * LDL + ijb * 16 + 4 * lg4]) = lg;
     }
     lds_barrier();
+    if (nwn == 0) stamp_if(a.dbg & 16, 10);
     // ---------------- B: thread = (row prow, state si)
     float la[KP];
     float A_i = 0.f;
@@ -364,6 +412,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_coop_kernel(HeadArgs a) {
       q0acc += qi;
     }
     lds_barrier();  // dlgS, aS, wS of every row
+    if (nwn == 0) stamp_if(a.dbg & 16, 11);
     // ---------------- B2: dq (lane si = state j), then prefetch the next window's rows
     if (grad && own) {
       float v = cpri * (wgt * rsj + sh.wS[prow + 1] * sh.aS[(prow + 1) * KP + si]);
@@ -371,6 +420,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_coop_kernel(HeadArgs a) {
       a.dqx[r * KP + si] = (valid && si < K) ? v : 0.f;
     }
     if (w + gridDim.x < nwin) load_row((w + gridDim.x) * WOWN, cur);
+    if (nwn == 0) stamp_if(a.dbg & 16, 12);
     if (!grad) continue;
     // ---------------- C: MLP backward on this wave's hidden blocks
     if (wave < KB) {  // db2: column sums of dlg, ij = 16 wave + l16, rows lg4 * WR / 4 ..
@@ -394,13 +444,15 @@ __global__ __launch_bounds__(256, 2) void elbo_head_coop_kernel(HeadArgs a) {
 #pragma unroll
       for (int hl = 0; hl < HBW; ++hl) {
         const int hb = wave * HBW + hl;
-        const float w1 = sh.W1S[(hb * 16 + l16) * 8 + lg4];
-        const float bb1 = sh.W1S[(hb * 16 + l16) * 8 + U];
+        const float w1 = CREG ? w1c[hl] : sh.W1S[(hb * 16 + l16) * 8 + lg4];
+        const float bb1 = CREG ? bb1c[hl] : sh.W1S[(hb * 16 + l16) * 8 + U];
         f32x4 h = mfma16x16x4(ua, w1, f32x4{bb1, bb1, bb1, bb1});  // (rows x h), bias start
         f32x4 dh = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int s = 0; s < SD; ++s)
-          dh = mfma16x16x4(dla[s], sh.W2S[(4 * s + lg4) * S::LDW2 + hb * 16 + l16], dh);  // dlg @ W2
+        for (int s = 0; s < SD; ++s) {
+          const float w2 = CREG ? w2c[hl][CREG ? s : 0] : sh.W2S[(4 * s + lg4) * S::LDW2 + hb * 16 + l16];
+          dh = mfma16x16x4(dla[s], w2, dh);  // dlg @ W2
+        }
         f32x4 hr, dm;
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
