@@ -209,17 +209,21 @@ __global__ __launch_bounds__(256, 2) void elbo_head_coop_kernel(HeadArgs a) {
   constexpr int NAR = AREG ? HB : 1;
   float w1r[NAR];
   f32x4 bbr[NAR], w2r[NAR], b2r;
+  // (only where this workgroup runs two or more windows: for one window the preload costs more than it saves)
+  const bool areg = AREG && (int64_t)blockIdx.x + gridDim.x < nwin;
   if constexpr (AREG) {
-    const int ijb = wave % KB;
+    if (areg) {
+      const int ijb = wave % KB;
 #pragma unroll
-    for (int hb = 0; hb < HB; ++hb) {
-      w1r[hb] = lg4 < U ? sh.W1S[(hb * 16 + l16) * 8 + lg4] : 0.f;
+      for (int hb = 0; hb < HB; ++hb) {
+        w1r[hb] = lg4 < U ? sh.W1S[(hb * 16 + l16) * 8 + lg4] : 0.f;
 #pragma unroll
-      for (int v = 0; v < 4; ++v) bbr[hb][v] = sh.W1S[(hb * 16 + 4 * lg4 + v) * 8 + U];
-      w2r[hb] = *reinterpret_cast<const f32x4*>(&sh.W2S[(ijb * 16 + l16) * S::LDW2 + hb * 16 + 4 * lg4]);
+        for (int v = 0; v < 4; ++v) bbr[hb][v] = sh.W1S[(hb * 16 + 4 * lg4 + v) * 8 + U];
+        w2r[hb] = *reinterpret_cast<const f32x4*>(&sh.W2S[(ijb * 16 + l16) * S::LDW2 + hb * 16 + 4 * lg4]);
+      }
+#pragma unroll
+      for (int v = 0; v < 4; ++v) b2r[v] = sh.b2S[16 * ijb + 4 * lg4 + v];
     }
-#pragma unroll
-    for (int v = 0; v < 4; ++v) b2r[v] = sh.b2S[16 * ijb + 4 * lg4 + v];
   }
   // CREG: phase C's weight operands of this wave's hidden blocks in registers too (window-invariant)
   constexpr bool CREG = HBW * SD <= 8;
@@ -300,18 +304,20 @@ __global__ __launch_bounds__(256, 2) void elbo_head_coop_kernel(HeadArgs a) {
 #pragma unroll
       for (int rb = 0; rb < NRB; ++rb)
         *reinterpret_cast<f32x4*>(&sh.lgS[(rb * 16 + l16) * LDL + wave * 16 + 4 * lg4]) = lg[rb];
-    } else if constexpr (AREG) {
-      if (wave < NT) {
-        const int ijb = wave % KB, rb = wave / KB;
-        f32x4 lg = b2r;
-        const float ub = sh.uS[(rb * 16 + l16) * 8 + lg4];
+    } else if (areg) {
+      if constexpr (AREG) {
+        if (wave < NT) {
+          const int ijb = wave % KB, rb = wave / KB;
+          f32x4 lg = b2r;
+          const float ub = sh.uS[(rb * 16 + l16) * 8 + lg4];
 #pragma unroll
-        for (int hb = 0; hb < HB; ++hb) {
-          const f32x4 hc = mfma16x16x4(w1r[hb], ub, bbr[hb]);  // hid^T (h x rows), bias start
+          for (int hb = 0; hb < HB; ++hb) {
+            const f32x4 hc = mfma16x16x4(w1r[hb], ub, bbr[hb]);  // hid^T (h x rows), bias start
 #pragma unroll
-          for (int v = 0; v < 4; ++v) lg = mfma16x16x4(w2r[hb][v], relu_f(hc[v]), lg);
+            for (int v = 0; v < 4; ++v) lg = mfma16x16x4(w2r[hb][v], relu_f(hc[v]), lg);
+          }
+          *reinterpret_cast<f32x4*>(&sh.lgS[(rb * 16 + l16) * LDL + ijb * 16 + 4 * lg4]) = lg;
         }
-        *reinterpret_cast<f32x4*>(&sh.lgS[(rb * 16 + l16) * LDL + ijb * 16 + 4 * lg4]) = lg;
       }
     } else
     for (int tk = wave; tk < NT; tk += 4) {
