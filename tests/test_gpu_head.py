@@ -1,9 +1,12 @@
 """The fused ELBO heads across the shapes that select them (csrc/api.hip plan_elbo):
 
-  head_wave.hip  K <= 4, U <= 4, TH in {64, 128}      (cfg1 / cfg2)
-  head_k8.hip    5 <= K <= 8, U <= 4, TH 64/128/256   (cfg4: K = 8, D = 16)
+  head_coop.hip  K <= 8, U <= 4, TH in {64, 128, 256}, D <= 16   (cfg1 / cfg2 / cfg4; the default)
   head_mfma.hip  K <= 4, U in 5..7, TH in {64, 128}
   staged         everything else (cfg3: K = 32)
+
+head_coop keeps a wave's window-invariant phase-A operands in registers where its workgroup runs two or
+more windows (more than 512 windows: 63 rows each at K <= 4, 31 at K <= 8), so the cases marked "loops"
+run both forms in one launch.
 
 Each case is one training step's loss (1e-5 relative vs the fp32 CPU oracle) and all 18
 gradients (normwise vs the fp64 oracle on the device forward's ReLU branch), through
@@ -19,6 +22,9 @@ CASES = [
     # (D, H, K, H2, U, TH), B, T
     ((16, 32, 8, 16, 4, 128), 24, 70),
     ((16, 32, 8, 16, 4, 128), 96, 200),    # > 512 windows: workgroups loop over windows
+    ((5, 32, 3, 16, 4, 128), 256, 200),    # loops, K <= 4 (register-resident phase-A operands)
+    ((5, 32, 5, 16, 4, 64), 96, 200),      # loops, K = 5
+    ((5, 32, 3, 16, 2, 64), 200, 180),     # loops, U < 4
     ((5, 32, 5, 16, 4, 64), 24, 70),
     ((7, 32, 6, 16, 3, 256), 16, 60),
     ((16, 32, 7, 16, 2, 128), 20, 45),
