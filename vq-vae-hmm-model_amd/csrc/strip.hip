@@ -128,10 +128,12 @@ __device__ __forceinline__ void pk_block(const float (&w)[4][4], const float* Xw
 }
 
 // conv2_epilogue's ACT = 1 arithmetic on a 64-wide block (bias, ReLU, pad rows 0): rows r0 + l16;
-// rows l16 in [slo, shi) are stored to out (PCL, 64 channels); every row goes to the LDS slot rows xs.
+// rows l16 in [slo, shi) are stored to out (PCL, 64 channels); rows go to the LDS slot rows xs (every row,
+// or only row `only` when only >= 0), row 0 also to the row xlo and row 15 to the row xhi (when given).
 __device__ __forceinline__ void front_epi(f32x4 (&acc)[4], const f32x4 (&bias)[4], int64_t r0, int64_t R, int T,
                                           int lg4, int l16, int slo, int shi, float* out, float* xs,
-                                          bool nostore) {
+                                          bool nostore, int only = -1, float* xlo = nullptr,
+                                          float* xhi = nullptr) {
   const int64_t r = r0 + l16;
   const bool valid = row_valid(r, R, T);
   const bool st = l16 >= slo && l16 < shi && r < R && !nostore;
@@ -145,7 +147,9 @@ __device__ __forceinline__ void front_epi(f32x4 (&acc)[4], const f32x4 (&bias)[4
     }
     acc[nb] = y;
     if (st) *reinterpret_cast<f32x4*>(out + r * 64 + nb * 16 + 4 * lg4) = y;
-    *reinterpret_cast<f32x4*>(xs + l16 * ST_LDW + nb * 16 + 4 * lg4) = y;
+    if (only < 0 || l16 == only) *reinterpret_cast<f32x4*>(xs + l16 * ST_LDW + nb * 16 + 4 * lg4) = y;
+    if (xlo && l16 == 0) *reinterpret_cast<f32x4*>(xlo + nb * 16 + 4 * lg4) = y;
+    if (xhi && l16 == 15) *reinterpret_cast<f32x4*>(xhi + nb * 16 + 4 * lg4) = y;
   }
 }
 
@@ -423,13 +427,10 @@ __global__ __launch_bounds__(512) void strip_fwd_kernel(StripFwdArgs a, HeadArgs
   float s_rec = 0.f, s_ent = 0.f, s_tr = 0.f, s_init = 0.f, q0acc = 0.f, db2acc = 0.f;
   f32x4 gW2 = f32x4{0.f, 0.f, 0.f, 0.f}, gW1 = gW2;  // this wave's hidden block (hb = wave, HB <= 8)
 
-  // this wave's block: window rows 16 w .. 16 w + 15.  Stored rows (window rows ST_HALO .. ST_HALO +
-  // ST_OWN - 1): the 64-wide convs' l16 range; the fronts' block A (rows 16w - 1 + l16) stores rows
-  // 16w .. 16w + 14, block B (rows 16w + 1 + l16) row 16w + 15
+  // this wave's block: window rows 16 w .. 16 w + 15 in every layer.  Stored rows (window rows ST_HALO ..
+  // ST_HALO + ST_OWN - 1): l16 in [slo, shi)
   const int mlo = ST_HALO - 16 * wave, mhi = ST_HALO + ST_OWN - 16 * wave;  // in block-row units
   const int slo = max(0, mlo), shi = min(16, mhi);
-  const int alo = max(1, mlo + 1), ahi = min(16, mhi + 1);
-  const bool bown = 15 >= mlo && 15 < mhi;
   const bool nost = a.dbg & 1;
   int it = 0;
   for (; s < a.nstrip; s += gridDim.x) {
@@ -439,20 +440,25 @@ __global__ __launch_bounds__(512) void strip_fwd_kernel(StripFwdArgs a, HeadArgs
       const int64_t nx = s + gridDim.x;
       px = load_x((nx < a.nstrip ? nx : s) * ST_OWN - ST_HALO);  // the next strip's x, in flight
     }
-    // ---- enc_conv1 + ReLU for rows rb - 1 .. rb + 16 (h1e: owned rows) -> slot
+    // ---- enc_conv1 + ReLU for rows rb .. rb + 15 (h1e: owned rows) -> slot rows 1..16, row rb to the
+    // previous wave's slot row 17, row rb + 15 to the next wave's slot row 0; the window's outer rows -1
+    // and 128 (slot 0 row 0, slot 7 row 17) by waves 5 and 6 (SIMDs 1 and 2: no SIMD runs three blocks
+    // twice as long as another)
     {
-      f32x4 acc[4], acc2[4];
-      pk_block(wE, sh.Xx + (16 * wave) * ST_XLD, a.D, lg4, l16, acc);
-      pk_block(wE, sh.Xx + (16 * wave + 2) * ST_XLD, a.D, lg4, l16, acc2);
-      front_epi(acc, bE, rb - 1, R, T, lg4, l16, alo, ahi, a.h1e, slot, nost);
-      front_epi(acc2, bE, rb + 1, R, T, lg4, l16, bown ? 14 : 16, bown ? 15 : 16, a.h1e, slot + 2 * ST_LDW, nost);
+      f32x4 acc[4];
+      pk_block(wE, sh.Xx + (16 * wave + 1) * ST_XLD, a.D, lg4, l16, acc);
+      front_epi(acc, bE, rb, R, T, lg4, l16, slo, shi, a.h1e, slot + ST_LDW, nost, -1,
+                wave > 0 ? sh.slot[wave - 1] + 17 * ST_LDW : nullptr, wave < 7 ? sh.slot[wave + 1] : nullptr);
+      if (wave == 5 || wave == 6) {
+        const bool lo = wave == 5;
+        f32x4 acc2[4];
+        pk_block(wE, sh.Xx + (lo ? 0 : 16 * 7 + 2) * ST_XLD, a.D, lg4, l16, acc2);
+        front_epi(acc2, bE, lo ? s0 - 1 : s0 + 16 * 7 + 1, R, T, lg4, l16, 0, 0, a.h1e,
+                  lo ? sh.slot[0] : sh.slot[7] + 2 * ST_LDW, true, lo ? 0 : 15);
+      }
     }
-    if (it == 0) {  // the first strip: every wave's share of the image DMA has landed
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      lds_barrier();
-    } else {
-      __builtin_amdgcn_wave_barrier();
-    }
+    if (it == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the first strip: the image DMA
+    lds_barrier();  // every slot's rows (and, first strip, every wave's share of the images)
     // ---- enc_conv2 + ReLU (h2e) + to_logits (logits) + softmax (q; all 16 rows -> Xq)
     {
       f32x4 acc[NB2][1];
@@ -476,22 +482,28 @@ __global__ __launch_bounds__(512) void strip_fwd_kernel(StripFwdArgs a, HeadArgs
           if (tid + 512 * j < HNW) hw[tid + 512 * j] = hwv[j];
       }
     }
-    // ---- composed dec_conv1 + ReLU for rows rb - 1 .. rb + 16 (g1: owned rows) -> slot
+    // ---- composed dec_conv1 + ReLU for rows rb .. rb + 15 (g1: owned rows) -> slots, as enc_conv1
     {
-      f32x4 acc[4], acc2[4];
-      pk_block(wD, sh.Xq + (16 * wave) * ST_XLD, a.K, lg4, l16, acc);
-      pk_block(wD, sh.Xq + (16 * wave + 2) * ST_XLD, a.K, lg4, l16, acc2);
+      f32x4 acc[4];
+      pk_block(wD, sh.Xq + (16 * wave + 1) * ST_XLD, a.K, lg4, l16, acc);
       if constexpr (PROF > 0) {
         if (it == 0) {
-          asm volatile("s_nop 0" : : "v"(acc[3][3]), "v"(acc2[3][3]));
+          asm volatile("s_nop 0" : : "v"(acc[3][3]));
           stamp<PROF>(10);
         }
       }
-      front_epi(acc, bD, rb - 1, R, T, lg4, l16, alo, ahi, a.g1, slot, nost);
+      front_epi(acc, bD, rb, R, T, lg4, l16, slo, shi, a.g1, slot + ST_LDW, nost, -1,
+                wave > 0 ? sh.slot[wave - 1] + 17 * ST_LDW : nullptr, wave < 7 ? sh.slot[wave + 1] : nullptr);
       if (it == 0) stamp<PROF>(11);
-      front_epi(acc2, bD, rb + 1, R, T, lg4, l16, bown ? 14 : 16, bown ? 15 : 16, a.g1, slot + 2 * ST_LDW, nost);
+      if (wave == 5 || wave == 6) {
+        const bool lo = wave == 5;
+        f32x4 acc2[4];
+        pk_block(wD, sh.Xq + (lo ? 0 : 16 * 7 + 2) * ST_XLD, a.K, lg4, l16, acc2);
+        front_epi(acc2, bD, lo ? s0 - 1 : s0 + 16 * 7 + 1, R, T, lg4, l16, 0, 0, a.g1,
+                  lo ? sh.slot[0] : sh.slot[7] + 2 * ST_LDW, true, lo ? 0 : 15);
+      }
     }
-    __builtin_amdgcn_wave_barrier();
+    lds_barrier();  // every slot's rows
     if (it == 0) stamp<PROF>(4);
     // ---- dec_conv2 + ReLU (g2) + to_params (par)
     {
