@@ -819,9 +819,11 @@ struct StripBwdLds {
 static_assert(8 * 18 * ST_LDW >= (ST_WIN + 2) * ST_LDW, "dg1 rows alias the slots");
 
 // conv2_epilogue's ACT = 2 arithmetic (scale, no bias, ReLU-backward mask, pad rows 0) on a 64-wide
-// block: rows r0 + l16, stored (PCL, 64 channels) for l16 in [slo, shi), optionally to LDS rows xs
+// block: rows r0 + l16, stored (PCL, 64 channels) for l16 in [slo, shi), optionally to LDS rows xs (every
+// row, or only row `only` when only >= 0), row 0 also to the row xlo and row 15 to the row xhi (when given)
 __device__ __forceinline__ void mask_epi(f32x4 (&acc)[4], const float4 (&aux)[4], float sc, int64_t r0, int64_t R,
-                                         int T, int lg4, int l16, int slo, int shi, float* out, float* xs, int xld) {
+                                         int T, int lg4, int l16, int slo, int shi, float* out, float* xs, int xld,
+                                         int only = -1, float* xlo = nullptr, float* xhi = nullptr) {
   const int64_t r = r0 + l16;
   const bool valid = row_valid(r, R, T);
   const bool st = l16 >= slo && l16 < shi && r < R;
@@ -837,7 +839,9 @@ __device__ __forceinline__ void mask_epi(f32x4 (&acc)[4], const float4 (&aux)[4]
     }
     acc[nb] = y;
     if (st) *reinterpret_cast<f32x4*>(out + r * 64 + nb * 16 + 4 * lg4) = y;
-    if (xs) *reinterpret_cast<f32x4*>(xs + l16 * xld + nb * 16 + 4 * lg4) = y;
+    if (xs && (only < 0 || l16 == only)) *reinterpret_cast<f32x4*>(xs + l16 * xld + nb * 16 + 4 * lg4) = y;
+    if (xlo && l16 == 0) *reinterpret_cast<f32x4*>(xlo + nb * 16 + 4 * lg4) = y;
+    if (xhi && l16 == 15) *reinterpret_cast<f32x4*>(xhi + nb * 16 + 4 * lg4) = y;
   }
 }
 
@@ -887,50 +891,51 @@ __global__ __launch_bounds__(512) void strip_bwd_kernel(StripBwdArgs a, ConvArgs
 
   const int mlo = ST_HALO - 16 * wave, mhi = ST_HALO + ST_OWN - 16 * wave;
   const int slo = max(0, mlo), shi = min(16, mhi);
-  const int alo = max(1, mlo + 1), ahi = min(16, mhi + 1);
-  const bool bown = 15 >= mlo && 15 < mhi;
   int it = 0;
   for (int64_t s = blockIdx.x; s < a.nstrip; s += gridDim.x) {
     const int64_t s0 = s * ST_OWN - ST_HALO;
     const int64_t rb = s0 + 16 * wave;
-    // ---- to_params dgrad (1x1, x scale, mask g2) for rows rb - 1 .. rb + 16: two blocks -> dg2, slot
+    // ---- to_params dgrad (1x1, x scale, mask g2) for rows rb .. rb + 15 -> dg2, slot rows 1..16, the
+    // neighbours' halo rows (17 / 0); the window's outer rows -1 / 128 by waves 5 / 6 (as the forward strip)
     {
-      float4 mA[4], mB[4], xA, xB;
-      load_mask(a.g2, rb - 1, R, lg4, l16, mA);
-      load_mask(a.g2, rb + 1, R, lg4, l16, mB);
       auto ld_dpar = [&](int64_t r) {  // row r, channels 4 lg4 .. (x_mask: rows outside / pad channels 0)
         const int64_t rc = r < 0 ? 0 : (r >= R ? R - 1 : r);
         const float4 v = *reinterpret_cast<const float4*>(a.dpar + rc * a.ldp + min(4 * lg4, a.ldp - 4));
         return (r >= 0 && r < R && 4 * lg4 < a.ldp) ? v : make_float4(0.f, 0.f, 0.f, 0.f);
       };
-      xA = ld_dpar(rb - 1 + l16);
-      xB = ld_dpar(rb + 1 + l16);
-      f32x4 acc[4], acc2[4];
-      const float bA[4] = {xA.x, xA.y, xA.z, xA.w}, bB[4] = {xB.x, xB.y, xB.z, xB.w};
+      auto front = [&](int64_t r0, float4 (&m)[4], const float4 x, f32x4 (&acc)[4]) {
+        const float b[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
-      for (int nb = 0; nb < 4; ++nb) {
-        acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-        acc2[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int nb = 0; nb < 4; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int nb = 0; nb < 4; ++nb) acc[nb] = mfma16x16x4(wP[nb][e], b[e], acc[nb]);
+      };
+      const bool extra = wave == 5 || wave == 6;
+      const int64_t re = wave == 5 ? s0 - 1 : s0 + 16 * 7 + 1;  // the extra block's row 0
+      float4 mA[4], mB[4], xA, xB = make_float4(0.f, 0.f, 0.f, 0.f);
+      load_mask(a.g2, rb, R, lg4, l16, mA);
+      xA = ld_dpar(rb + l16);
+      if (extra) {
+        load_mask(a.g2, re, R, lg4, l16, mB);
+        xB = ld_dpar(re + l16);
       }
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-#pragma unroll
-        for (int nb = 0; nb < 4; ++nb) {
-          acc[nb] = mfma16x16x4(wP[nb][e], bA[e], acc[nb]);
-          acc2[nb] = mfma16x16x4(wP[nb][e], bB[e], acc2[nb]);
-        }
-      mask_epi(acc, mA, psc, rb - 1, R, T, lg4, l16, alo, ahi, a.dg2, slot, ST_LDW);
-      mask_epi(acc2, mB, psc, rb + 1, R, T, lg4, l16, bown ? 14 : 16, bown ? 15 : 16, a.dg2, slot + 2 * ST_LDW,
-               ST_LDW);
+      f32x4 acc[4];
+      front(rb, mA, xA, acc);
+      mask_epi(acc, mA, psc, rb, R, T, lg4, l16, slo, shi, a.dg2, slot + ST_LDW, ST_LDW, -1,
+               wave > 0 ? sh.slot[wave - 1] + 17 * ST_LDW : nullptr, wave < 7 ? sh.slot[wave + 1] : nullptr);
+      if (extra) {
+        f32x4 acc2[4];
+        front(re, mB, xB, acc2);
+        mask_epi(acc2, mB, psc, re, R, T, lg4, l16, 0, 0, a.dg2, wave == 5 ? sh.slot[0] : sh.slot[7] + 2 * ST_LDW,
+                 ST_LDW, wave == 5 ? 0 : 15);
+      }
     }
     float4 m1[4];
     load_mask(a.g1, rb, R, lg4, l16, m1);
-    if (it == 0) {  // the first strip: every wave's share of the image DMA has landed
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      lds_barrier();
-    } else {
-      __builtin_amdgcn_wave_barrier();
-    }
+    if (it == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the first strip: the image DMA
+    lds_barrier();  // every slot's rows (and, first strip, every wave's share of the images)
     // ---- dec_conv2 dgrad (mask g1) -> dg1 (registers, HBM)
     f32x4 d1[4];
     {
