@@ -35,7 +35,7 @@ struct CoopLds {
   static constexpr int LDL = 16 * KB + 4;        // lgS / dlgS row stride
   float W2S[16 * KB * LDW2];                     // rows ij >= KK zero
   float W1S[TH * 8];                             // W1' = [W1 | b1 | 0]  (TH x 8)
-  float uS[WR * 8];                              // u' = [u, 1 at column U, 0]
+  float uS[2][WR * 8];                           // u' = [u, 1 at column U, 0]; two windows' worth
   float lgS[WR * LDL];                           // transition logits of the window's rows
   float dlgS[WR * LDL];                          // their gradients (zero for ij >= KK, non-owned rows)
   float aS[WR * KP];                             // A_i = sum_j q[j] log_A[i][j] per row (next row's dq)
@@ -266,10 +266,12 @@ __global__ __launch_bounds__(256, 2) void elbo_head_coop_kernel(HeadArgs a) {
 #pragma unroll
     for (int k = 0; k < KP; ++k) qi = si == k ? qv[k] : qi;
 
-    lds_barrier();  // the previous window's phases B2 / C are done with uS, lgS, dlgS, aS, wS
-    // ---------------- L: u' rows to LDS (thread (row, i) writes columns i and i + KP of u')
+    // ---------------- L: u' rows to LDS (thread (row, i) writes columns i and i + KP of u').  uS is double
+    // buffered (the previous window's phase C may still read the other one), and every other array is
+    // first written behind a barrier this window passes, so no barrier is needed before this store
+    float* const uSb = sh.uS[nwn & 1];
 #pragma unroll
-    for (int c = si; c < 8; c += KP) sh.uS[prow * 8 + c] = c < U ? (valid ? cur.u : 0.f) : (c == U ? 1.f : 0.f);
+    for (int c = si; c < 8; c += KP) uSb[prow * 8 + c] = c < U ? (valid ? cur.u : 0.f) : (c == U ? 1.f : 0.f);
     lds_barrier();
     if (nwn == 0) stamp_if(a.dbg & 16, 9);
     // ---------------- A: tasks (ij block, 16-row block) over the waves; with 4 ij blocks (K > 6) wave w
@@ -284,7 +286,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_coop_kernel(HeadArgs a) {
           const int ij = 16 * wave + 4 * lg4 + v;
           lg[rb][v] = sh.b2S[ij];
         }
-        ub[rb] = sh.uS[(rb * 16 + l16) * 8 + lg4];
+        ub[rb] = uSb[(rb * 16 + l16) * 8 + lg4];
       }
 #pragma unroll 2
       for (int hb = 0; hb < HB; ++hb) {
@@ -309,7 +311,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_coop_kernel(HeadArgs a) {
         if (wave < NT) {
           const int ijb = wave % KB, rb = wave / KB;
           f32x4 lg = b2r;
-          const float ub = sh.uS[(rb * 16 + l16) * 8 + lg4];
+          const float ub = uSb[(rb * 16 + l16) * 8 + lg4];
 #pragma unroll
           for (int hb = 0; hb < HB; ++hb) {
             const f32x4 hc = mfma16x16x4(w1r[hb], ub, bbr[hb]);  // hid^T (h x rows), bias start
@@ -328,7 +330,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_coop_kernel(HeadArgs a) {
         const int ij = 16 * ijb + 4 * lg4 + v;
         lg[v] = sh.b2S[ij];
       }
-      const float ub = sh.uS[(rb * 16 + l16) * 8 + lg4];
+      const float ub = uSb[(rb * 16 + l16) * 8 + lg4];
 #pragma unroll 2
       for (int hb = 0; hb < HB; ++hb) {
         // u' columns c >= U are [1 (bias), 0, ..]: only c < U in the MFMA, the bias is the accumulator's start
@@ -435,7 +437,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_coop_kernel(HeadArgs a) {
     }
 #pragma unroll
     for (int rb = 0; rb < NRB; ++rb) {
-      const float ua = lg4 < U ? sh.uS[(rb * 16 + l16) * 8 + lg4] : 0.f;  // u'[row l16][c lg4], c < U
+      const float ua = lg4 < U ? uSb[(rb * 16 + l16) * 8 + lg4] : 0.f;  // u'[row l16][c lg4], c < U
       float dla[SD], dlt[4][KB], ubv[4];
 #pragma unroll
       for (int s = 0; s < SD; ++s) dla[s] = sh.dlgS[(rb * 16 + l16) * LDL + 4 * s + lg4];  // dlg[row l16][ij 4s+lg4]
@@ -444,7 +446,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_coop_kernel(HeadArgs a) {
         const int row = rb * 16 + 4 * lg4 + s;
 #pragma unroll
         for (int bb = 0; bb < KB; ++bb) dlt[s][bb] = sh.dlgS[row * LDL + bb * 16 + l16];  // dlg[row][ij 16bb+l16]
-        const float uv = sh.uS[row * 8 + (l16 & 7)];
+        const float uv = uSb[row * 8 + (l16 & 7)];
         ubv[s] = l16 < 8 ? uv : 0.f;  // u'[row][c' l16]
       }
 #pragma unroll
