@@ -272,7 +272,10 @@ __global__ __launch_bounds__(256, 2) void elbo_head_coop_kernel(HeadArgs a) {
     float* const uSb = sh.uS[nwn & 1];
 #pragma unroll
     for (int c = si; c < 8; c += KP) uSb[prow * 8 + c] = c < U ? (valid ? cur.u : 0.f) : (c == U ? 1.f : 0.f);
-    lds_barrier();
+    // K <= 4 (KP = 4, one ij block): wave w wrote rows 16w .. 16w + 15, exactly the row block its phase-A
+    // task reads, and phase C reads the others only behind the next two barriers: a wave barrier will do
+    if constexpr (KP == 4 && KB == 1) __builtin_amdgcn_wave_barrier();
+    else lds_barrier();
     if (nwn == 0) stamp_if(a.dbg & 16, 9);
     // ---------------- A: tasks (ij block, 16-row block) over the waves; with 4 ij blocks (K > 6) wave w
     // takes block w for every row block in one pass (the W2 operands read once for all of them)
