@@ -40,7 +40,8 @@ extern "C" {
 /* Bits of the training step's device status word (vqhmm_elbo_status_offset).  Kernels only
  * ever OR bits in; the caller zeroes the word when it allocates the workspace and reads it
  * after a synchronisation (TrainState.check_status raises RuntimeError on any bit). */
-#define VQHMM_STATUS_TAIL_TIMEOUT 1ull /* the backward tail's in-launch wait for the reduced dWc ran out */
+#define VQHMM_STATUS_TAIL_TIMEOUT 1ull /* reserved: raised by the round-3 tail's in-launch wait; the tail has
+                                          * had no cross-workgroup wait since, so no kernel sets it */
 
 /* Number of parameter tensors of a VAE_HMM, in nn.Module.parameters() order
  * (VQ_VAE_HMM_fixed.py:92-98 -> encoder :32-36, prior :44-57, decoder :74-79). */

@@ -73,3 +73,21 @@ def test_status_word_inside_workspace(dims, B, T):
     assert lib.vqhmm_elbo_status_offset(ctypes.byref(d), B, T, ctypes.byref(off)) == 0
     assert off.value % 8 == 0 and off.value + 8 <= nb.value
     assert lib.vqhmm_elbo_status_offset(ctypes.byref(d), 0, T, ctypes.byref(off)) == -1
+
+
+# the A/B switches the release library may read (common.h VQHMM_ENV): each selects between launch paths the
+# GPU tests prove bit-identical (VQHMM_STRIP_HEAD / VQHMM_HEAD: equal within their stated tolerance)
+RELEASE_SWITCHES = {"VQHMM_CONV_FUSE", "VQHMM_TAIL_FUSED", "VQHMM_STRIP", "VQHMM_STRIP_BWD", "VQHMM_STRIP_HEAD",
+                    "VQHMM_FB_RES", "VQHMM_HEAD"}
+
+
+def test_release_library_reads_no_profiling_knobs():
+    """result-changing timing / tuning knobs (VQHMM_WGRAD_JOBMASK, VQHMM_STRIP_DBG,
+    VQHMM_HEAD_DBG, VQHMM_PV_MODE, the chunk-count overrides, ...) exist only in the profiling build
+    (make prof): the release library's strings name no environment variable but the A/B switches."""
+    from vqhmm import _ext
+    data = open(_ext.LIB_PATH if "prof" not in _ext.LIB_PATH else _ext.LIB_PATH.replace("_prof", ""), "rb").read()
+    names = set(m.decode() for m in re.findall(rb"VQHMM_[A-Z0-9_]+", data))
+    names = {n for n in names if not n.startswith("VQHMM_STATUS")}
+    assert names <= RELEASE_SWITCHES, sorted(names - RELEASE_SWITCHES)
+    assert "VQHMM_WGRAD_JOBMASK" not in names and "VQHMM_STRIP_DBG" not in names

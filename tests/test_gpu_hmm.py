@@ -303,3 +303,26 @@ def test_hmm_k_over_256_rejected():
     log_pi, log_A, em = random_hmm(1, B, T, K)
     with pytest.raises(RuntimeError, match="unsupported"):
         vqhmm.viterbi(*gpu(log_pi, log_A, em))
+
+
+@pytest.mark.parametrize("kernel", FB_KERNELS)
+@pytest.mark.parametrize("K,T", [(4, 60), (8, 90), (16, 70), (48, 40)])
+def test_forward_backward_impossible_sequence(K, T, kernel, monkeypatch):
+    """A sequence with zero probability (every emission -inf at one step): logZ = -inf for it, as the
+    fp64 oracle gives, and the batch's other sequences are unaffected (the K > 32 kernel used to
+    turn -inf - -inf into a NaN logZ).  Its gamma (0 / 0: NaN in the oracle) is not a contract: the K <= 8
+    and K > 32 kernels give NaN, the 8 < K <= 32 one does not."""
+    import vqhmm
+    use_fb_kernel(monkeypatch, kernel)
+    B = 3
+    log_pi, log_A, em = random_hmm(K * 5 + T, B, T, K)
+    em[1, T // 3, :] = -np.inf
+    L = np.array([T, T, T - 7], np.int64)
+    gamma, logZ = vqhmm.forward_backward(*gpu(log_pi, log_A, em), torch.from_numpy(L))
+    with np.errstate(divide="ignore", invalid="ignore"):
+        rg, rz = hmm_ref.forward_backward_f64(log_pi, log_A, em, L)
+    g, z = gamma.cpu().numpy(), logZ.cpu().numpy()
+    assert z[1] == -np.inf and rz[1] == -np.inf
+    ok = [0, 2]
+    check_gamma(g[ok], rg[ok])
+    assert np.all(np.abs(z[ok] - rz[ok]) <= 1e-5 * np.maximum(1.0, np.abs(rz[ok])))

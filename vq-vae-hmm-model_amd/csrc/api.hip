@@ -39,7 +39,7 @@ struct Carver {
 // (head_mfma.hip) — A/B switches.
 int head_choice() {
   static const int v = [] {
-    const char* e = getenv("VQHMM_HEAD");
+    const char* e = VQHMM_ENV("VQHMM_HEAD");
     if (e && strcmp(e, "tile") == 0) return 2;
     if (e && strcmp(e, "wave") == 0) return 1;
     return 0;
@@ -51,14 +51,14 @@ int head_choice() {
 // VQHMM_WGRAD_MINROWS = the grouped launch's minimum rows per chunk (multiple of 64).
 bool wgroup_enabled() {
   static const bool v = [] {
-    const char* e = getenv("VQHMM_WGROUP");
+    const char* e = VQHMM_PROF_ENV("VQHMM_WGROUP");
     return !(e && e[0] == '0');
   }();
   return v;
 }
 int64_t wgroup_min_rows() {
   static const int64_t v = [] {
-    const char* e = getenv("VQHMM_WGRAD_MINROWS");
+    const char* e = VQHMM_PROF_ENV("VQHMM_WGRAD_MINROWS");
     // 3 stages: fewer, fuller slabs at small batches (B = 128: 64 / 128 / 192 / 256 rows 0.1463 / 0.1381 /
     // 0.1369 / 0.1377 ms; B = 256: 128 -> 192 rows 0.1953 -> 0.1921 ms)
     const long r = e ? atol(e) : 192;
@@ -74,14 +74,14 @@ int64_t wgroup_min_rows() {
 // step 0.1161 -> 0.1162 ms; cfg2 178 -> 199 us, 0.462 -> 0.488 ms; gpurun_out sq7)
 bool strip_fwd_env() {
   static const bool on = [] {
-    const char* e = getenv("VQHMM_STRIP");
+    const char* e = VQHMM_ENV("VQHMM_STRIP");
     return !e || atoi(e) != 0;
   }();
   return on;
 }
 bool strip_head_on() {
   static const bool on = [] {
-    const char* e = getenv("VQHMM_STRIP_HEAD");
+    const char* e = VQHMM_ENV("VQHMM_STRIP_HEAD");
     return e && atoi(e) != 0;
   }();
   return on && strip_fwd_env();
@@ -102,6 +102,7 @@ struct WLayer {
   int64_t rows, nchunks;
   float* slab;
   float* bslab;
+  float* cslab;  // the composed decoder conv1 (wl[2], grouped launch): per-chunk dE shares [nchunks][K][H]
 };
 
 struct ElboPlan {
@@ -117,8 +118,7 @@ struct ElboPlan {
   float *sW1, *sb1, *sW2, *sb2, *sq0;
   float *loss, *pieces;
   int64_t* cnt;  // valid count written by the prologue (loss finalized in the backward)
-  unsigned long long* sync;  // [0] / [1] the backward tail's arrival / departure counters (zeroed by the
-                             // prologue and re-armed by the tail itself), [2] the status word, [3] spare
+  unsigned long long* sync;  // [2] the status word (vqhmm_elbo_status_offset; reserved), [0], [1], [3] spare
   // staged head (shapes the fused heads do not cover): Prior MLP as 1x1 convs
   bool staged;
   bool wave_head;  // head_wave.hip (K <= 4, VQHMM_HEAD=wave)
@@ -127,7 +127,8 @@ struct ElboPlan {
   float *hid, *lgA, *dhid, *nx, *dqc, *trw, *logpi;
   // backward
   float *dg2, *dg1, *dqd, *dlog, *dh2, *dh1, *dWc;
-  float *Ecopy, *Wcopy;  // the prologue's copies of decoder.embeddings / decoder.conv1 weights (compose_adam)
+  float *Ecopy, *Wcopy;  // the prologue's copies of decoder.embeddings / decoder.conv1 weights, read by the
+                         // launch that also Adam-updates them (tail: E; compose_adam: both; Wcopy null when grouped)
   float* himg;           // the cooperative head's weight image (built by the prologue), or null
   bool wgroup;           // the six weight gradients run as one grouped launch (wgrad2_group)
   int nwl;
@@ -210,7 +211,6 @@ ElboPlan plan_elbo(const vqhmm_dims_t* d, int64_t B, int64_t T, void* ws) {
   p.dWc = c.take<float>((size_t)H * K * 3);
   p.himg = p.coop_head ? c.take<float>((size_t)head_coop_image_floats(K, p.TH)) : nullptr;
   p.Ecopy = c.take<float>((size_t)K * H);
-  p.Wcopy = c.take<float>((size_t)H * H * 3);
   const int shapes[8][3] = {{2 * D, H, 1}, {H, H, 3}, {H, K, 3}, {K, H2, 1}, {H2, H, 3}, {H, D, 3},
                             {p.TH, p.U, 1}, {K * K, p.TH, 1}};
   p.nwl = p.staged ? 8 : 6;
@@ -218,8 +218,12 @@ ElboPlan plan_elbo(const vqhmm_dims_t* d, int64_t B, int64_t T, void* ws) {
   for (int i = 0; i < 6; ++i) {
     WgradArgs t{};
     t.N = shapes[i][0]; t.C = shapes[i][1]; t.ks = shapes[i][2];
+    if (i == 2) t.cmpW = reinterpret_cast<const float*>(4096);  // the composed layer's dE epilogue (shape check only)
     p.wgroup = p.wgroup && wgrad2_group_supported(t);
   }
+  // the grouped path's tail forms the composed dW itself (a block reduces <= 256 dWc columns)
+  p.wgroup = p.wgroup && composed_block_cols(H, K) <= 256;
+  p.Wcopy = p.wgroup ? nullptr : c.take<float>((size_t)H * H * 3);
   for (int i = 0; i < p.nwl; ++i) {
     WLayer& w = p.wl[i];
     w.N = shapes[i][0]; w.C = shapes[i][1]; w.ks = shapes[i][2];
@@ -229,6 +233,7 @@ ElboPlan plan_elbo(const vqhmm_dims_t* d, int64_t B, int64_t T, void* ws) {
     w.nchunks = cdiv(R, w.rows);
     w.slab = c.take<float>((size_t)w.nchunks * w.N * w.C * w.ks);
     w.bslab = c.take<float>((size_t)w.nchunks * w.N);
+    w.cslab = (i == 2 && p.wgroup) ? c.take<float>((size_t)w.nchunks * K * H) : nullptr;
   }
   plan_images(p, c);
   p.bytes = c.off + 256;
@@ -470,8 +475,9 @@ bool logits_bwd_fused(const ElboPlan& p) { return p.K <= 8 && conv2_supported(co
 // ... and to_logits' dgrad too when the encoder conv2 width splits into float4s over the 4 lane groups.
 bool logits_dg_fused(const ElboPlan& p) { return logits_bwd_fused(p) && ld4(p.H2) % 16 == 0 && p.H2 <= 64; }
 
-// The six convolutions' weight-gradient problems, in S_W_PAR .. S_W_ENC1 order.
-void wgrad_jobs(const ElboPlan& p, WgradArgs* wa) {
+// The six convolutions' weight-gradient problems, in S_W_PAR .. S_W_ENC1 order (w: the parameters, for the
+// composed layer's dE epilogue in the grouped launch).
+void wgrad_jobs(const ElboPlan& p, const float* const* w, WgradArgs* wa) {
   const float* dys[6] = {p.dpar, p.dg2, p.dg1, p.dlog, p.dh2, p.dh1};
   const float* xs[6] = {p.g2, p.g1, p.q, p.h2e, p.h1e, p.xp};
   for (int i = 0; i < 6; ++i) {
@@ -480,12 +486,20 @@ void wgrad_jobs(const ElboPlan& p, WgradArgs* wa) {
     wa[i].dy = dys[i]; wa[i].x = xs[i]; wa[i].x_cf = 0; wa[i].R = p.R; wa[i].T = p.T;
     wa[i].N = L.N; wa[i].C = L.C; wa[i].ks = L.ks; wa[i].rows_per_chunk = L.rows; wa[i].slab = L.slab;
     wa[i].bias_slab = L.bslab;
+    static const bool no_cmp = VQHMM_PROF_ENV("VQHMM_WGRAD_NOCMP") != nullptr;  // timing only: dE left unwritten
+    if (L.cslab && !no_cmp) {
+      wa[i].cmpW = w[DEC1_W];
+      wa[i].cmp_slab = L.cslab;
+    }
   }
 }
 
-// The backward's slab segments (every weight gradient's per-chunk partials) for grad_tail /
-// tail_adam; returns the index of the composed decoder conv1's dWc segment.
-int make_tail(const ElboPlan& p, const StepCtx& c, TailArgs& ta) {
+// The backward's slab segments (every weight gradient's per-chunk partials) for the tail launch.  Grouped
+// weight gradients: the composed decoder conv1's dW is a composed segment over the dWc slab (its blocks
+// reduce their own dWc rows) and its dE a plain segment over the per-chunk dE shares, so every parameter's
+// gradient is complete after this one launch.  Otherwise the dWc segment reduces into p.dWc and the
+// composed gradients follow in a second launch (compose_adam / compose_bwd).
+void make_tail(const ElboPlan& p, const StepCtx& c, TailArgs& ta) {
   const float* const* w = c.w;
   int64_t off[VQHMM_NPARAMS + 1];
   vqhmm_dims_t d{p.D, p.H, p.K, p.H2, p.U, p.TH};
@@ -494,15 +508,19 @@ int make_tail(const ElboPlan& p, const StepCtx& c, TailArgs& ta) {
   const float* gs = c.gscale;
   int n = 0;
   auto seg = [&](const float* slab, int64_t nch, int64_t len, float* out, const float* scale) {
-    ta.s[n++] = SlabSeg{slab, out, scale, nch, len};
+    ta.s[n++] = SlabSeg{slab, out, scale, nch, len, nullptr, 0, 0};
   };
   const WLayer* wl = p.wl;
   seg(wl[0].slab, wl[0].nchunks, (int64_t)wl[0].N * wl[0].C, g + off[PAR_W], gs);  // dpar is unscaled
   seg(wl[0].bslab, wl[0].nchunks, wl[0].N, g + off[PAR_B], gs);
   seg(wl[1].slab, wl[1].nchunks, (int64_t)wl[1].N * wl[1].C * 3, g + off[DEC2_W], nullptr);
   seg(wl[1].bslab, wl[1].nchunks, wl[1].N, g + off[DEC2_B], nullptr);
-  const int dwc_seg = n;
-  seg(wl[2].slab, wl[2].nchunks, (int64_t)wl[2].N * wl[2].C * 3, p.dWc, nullptr);
+  if (p.wgroup) {
+    ta.s[n++] = SlabSeg{wl[2].slab, g + off[DEC1_W], nullptr, wl[2].nchunks, (int64_t)p.H * p.H * 3, p.Ecopy, p.H, p.K};
+    seg(wl[2].cslab, wl[2].nchunks, (int64_t)p.K * p.H, g + off[EMB], nullptr);
+  } else {
+    seg(wl[2].slab, wl[2].nchunks, (int64_t)wl[2].N * wl[2].C * 3, p.dWc, nullptr);
+  }
   seg(wl[2].bslab, wl[2].nchunks, wl[2].N, g + off[DEC1_B], nullptr);
   seg(wl[3].slab, wl[3].nchunks, (int64_t)wl[3].N * wl[3].C, g + off[LOGIT_W], nullptr);
   seg(wl[3].bslab, wl[3].nchunks, wl[3].N, g + off[LOGIT_B], nullptr);
@@ -529,7 +547,6 @@ int make_tail(const ElboPlan& p, const StepCtx& c, TailArgs& ta) {
     ta.fin_part = p.part; ta.fin_nblk = p.hgrid; ta.fin_cnt = p.cnt; ta.fin_B = p.B; ta.fin_T = p.T;
     ta.fin_D = p.D; ta.fin_loss = c.loss; ta.fin_accum = c.loss_accum; ta.fin_pieces = p.pieces;
   }
-  return dwc_seg;
 }
 
 // enc_conv1 -> enc_conv2, the composed dec_conv1 -> dec_conv2 and to_params_dgrad -> dec_conv2_dgrad
@@ -544,7 +561,7 @@ ConvArgs fused_pair(const ElboPlan& p, const float* const* w, int st) {
 }
 bool front_fused(const ElboPlan& p, const float* const* w, int st) {
   static const bool on = [] {
-    const char* e = getenv("VQHMM_CONV_FUSE");
+    const char* e = VQHMM_ENV("VQHMM_CONV_FUSE");
     return !e || atoi(e) != 0;
   }();
   return on && (st == S_ENC2 || st == S_DEC2 || st == S_DEC2_DG) && conv2_fused_supported(fused_pair(p, w, st));
@@ -575,14 +592,14 @@ ConvArgs dec1_dg_args(const ElboPlan& p, const float* const* w, const float* gsc
 // VQHMM_CONV_FUSE=0 switches it off too
 bool bwd_pair_fused(const ElboPlan& p, const float* const* w, const float* gscale) {
   static const bool on = [] {
-    const char* e = getenv("VQHMM_CONV_FUSE");
+    const char* e = VQHMM_ENV("VQHMM_CONV_FUSE");
     return !e || atoi(e) != 0;
   }();
   // measured: a launch fewer wins at small batches (B = 128: 22.3 -> 16.8 us), break-even at B = 512,
   // and at cfg2 (207k rows) the two launches are 3 us faster (168 VGPRs + spills at 3 waves / SIMD;
   // 2 waves without spills: slower still).  VQHMM_BWD_PAIR_ROWS moves the threshold (A/B)
   static const int64_t max_rows = [] {
-    const char* e = getenv("VQHMM_BWD_PAIR_ROWS");
+    const char* e = VQHMM_PROF_ENV("VQHMM_BWD_PAIR_ROWS");
     return e ? (int64_t)atoll(e) : (int64_t)1 << 17;
   }();
   if (!on || !logits_dg_fused(p) || p.R >= max_rows) return false;
@@ -595,13 +612,13 @@ bool bwd_pair_fused(const ElboPlan& p, const float* const* w, const float* gscal
 // VQHMM_STRIP_BWD=0 keeps the pair launches (A/B), read once
 bool strip_bwd_on(const ElboPlan& p) {
   static const bool on = [] {
-    const char* e = getenv("VQHMM_STRIP_BWD");
+    const char* e = VQHMM_ENV("VQHMM_STRIP_BWD");
     return !e || atoi(e) != 0;
   }();
   // measured (tools/gpu_stripab.sh): B = 128 0.124 -> 0.116 ms, 256 0.1765 -> 0.1715, 512 0.2784 -> 0.2761,
   // cfg2 (207k rows) 0.462 -> 0.467: below 2^17 rows only, as the backward pair
   static const int64_t max_rows = [] {  // A/B: VQHMM_STRIP_BWD_ROWS
-    const char* e = getenv("VQHMM_STRIP_BWD_ROWS");
+    const char* e = VQHMM_PROF_ENV("VQHMM_STRIP_BWD_ROWS");
     return e ? (int64_t)atoll(e) : (int64_t)1 << 17;
   }();
   return on && p.R < max_rows && logits_dg_fused(p) &&
@@ -609,10 +626,11 @@ bool strip_bwd_on(const ElboPlan& p) {
                              conv_of(p, nullptr, S_ENC2_DG));
 }
 
-// VQHMM_TAIL_FUSED=0: grad_tail and compose_bwd / compose_adam as two launches (A/B); read once
+// VQHMM_TAIL_FUSED=0 (grouped weight gradients): the tail without Adam, then the Adam launch (A/B; the
+// same bits); read once
 bool tail_fused_on() {
   static const bool v = [] {
-    const char* e = getenv("VQHMM_TAIL_FUSED");
+    const char* e = VQHMM_ENV("VQHMM_TAIL_FUSED");
     return !e || atoi(e) != 0;
   }();
   return v;
@@ -648,7 +666,6 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       a.Ecopy = p.Ecopy;
       a.Wcopy = p.Wcopy;
       if (c.need_grad == 2 && !c.norm) { a.lengths = c.lengths; a.cnt = p.cnt; }
-      a.sync = p.sync;
       if (p.himg) {
         a.hW1 = w[TN0_W]; a.hb1 = w[TN0_B]; a.hW2 = w[TN2_W]; a.hTH = p.TH; a.himg = p.himg;
       }
@@ -717,12 +734,12 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       return launch_logits_bwd(p.q, p.dqd, p.dqx, p.dlx, c.gscale, p.R, p.K, p.dlog, s);
     case S_W_PAR: case S_W_DEC2: case S_W_DEC1: case S_W_LOGIT: case S_W_ENC2: case S_W_ENC1: {
       WgradArgs wa[6];
-      wgrad_jobs(p, wa);
+      wgrad_jobs(p, w, wa);
       if (p.wgroup) {  // all six in S_W_ENC1's launch (every dY is ready by then, in any stage order)
         if (st != S_W_ENC1) return VQHMM_OK;
         // timing experiment only (gradients are then incomplete): VQHMM_WGRAD_JOBMASK bit i keeps job i
         static const int jmask = [] {
-          const char* e = getenv("VQHMM_WGRAD_JOBMASK");
+          const char* e = VQHMM_PROF_ENV("VQHMM_WGRAD_JOBMASK");
           return e ? atoi(e) : 63;
         }();
         if (jmask != 63) {
@@ -730,14 +747,15 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
           int n = 0;
           for (int i = 0; i < 6; ++i)
             if (jmask >> i & 1) sel[n++] = wa[i];
-          return n ? launch_wgrad2_group(sel, n, s) : VQHMM_OK;
+          return n ? launch_wgrad2_group(sel, n, s, c.adam && tail_fused_on() ? c.adam->step : nullptr) : VQHMM_OK;
         }
-        return launch_wgrad2_group(wa, 6, s);
+        // the fused tail applies Adam without a completion ticket: this launch advances the step counter
+        return launch_wgrad2_group(wa, 6, s, c.adam && tail_fused_on() ? c.adam->step : nullptr);
       }
       return launch_wgrad(wa[st - S_W_PAR], s);
     }
     case S_REDUCE: {
-      if (tail_fused_on()) return VQHMM_OK;  // in S_COMPOSE_BWD's launch (tail_kernel)
+      if (p.wgroup && tail_fused_on()) return VQHMM_OK;  // in S_COMPOSE_BWD's launch (tail_kernel)
       TailArgs ta{};
       make_tail(p, c, ta);
       return launch_grad_tail(ta, s);
@@ -746,21 +764,24 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       int64_t off[VQHMM_NPARAMS + 1];
       vqhmm_dims_t d{p.D, p.H, p.K, p.H2, p.U, p.TH};
       vqhmm_param_layout(&d, off);
+      if (p.wgroup) {  // every gradient is complete after the tail launch
+        if (tail_fused_on()) {  // slab reduction (+ Adam on each reduced column) in one launch
+          TailArgs ta{};
+          make_tail(p, c, ta);
+          return launch_tail(ta, c.adam, c.g, s);
+        }
+        if (!c.adam) return VQHMM_OK;
+        const AdamArgs& ad = *c.adam;
+        return launch_adam(ad.p, c.g, ad.m, ad.v, off[VQHMM_NPARAMS], ad.lr, ad.b1, ad.b2, ad.eps, ad.step, ad.gmul, s);
+      }
       ComposeAdamArgs ca{};
       ca.dWc = p.dWc; ca.H = p.H; ca.K = p.K;
       ca.g = c.g; ca.n = off[VQHMM_NPARAMS]; ca.off_w = off[DEC1_W]; ca.off_e = off[EMB];
       if (c.adam) {  // this launch updates the parameters: E / W from the prologue's copies
         ca.Ecopy = p.Ecopy; ca.Wcopy = p.Wcopy;
         ca.adam = *c.adam;
-      } else {
-        ca.Ecopy = w[EMB]; ca.Wcopy = w[DEC1_W];
+        return launch_compose_adam(ca, s);
       }
-      if (tail_fused_on()) {  // slab reduction + composed dW / dE (+ Adam) in one launch
-        TailArgs ta{};
-        const int dwc_seg = make_tail(p, c, ta);
-        return launch_tail(ta, ca, dwc_seg, p.sync, c.adam != nullptr, s);
-      }
-      if (c.adam) return launch_compose_adam(ca, s);
       const LogPriorGradArgs lp{nullptr, nullptr, p.K, c.beta, c.norm, p.B, c.gscale, nullptr};  // in S_REDUCE
       return launch_compose_bwd(p.dWc, w[DEC1_W], w[EMB], p.H, p.K, c.g + off[DEC1_W], c.g + off[EMB], lp, s);
     }
@@ -804,7 +825,8 @@ void stage_work(const ElboPlan& p, int st, double* flops, double* bytes, int* mf
     *flops = R * 8.0 * p.K;
   } else if (st == S_REDUCE) {
     double b = 0;
-    for (int i = 0; i < 6; ++i) b += (double)p.wl[i].nchunks * (p.wl[i].N * p.wl[i].C * p.wl[i].ks + p.wl[i].N);
+    for (int i = 0; i < 6; ++i)
+      b += (double)p.wl[i].nchunks * (p.wl[i].N * p.wl[i].C * p.wl[i].ks + p.wl[i].N + (p.wl[i].cslab ? p.K * p.H : 0));
     b += (double)p.hgrid * ((double)p.TH * p.U + p.TH + (double)p.K * p.K * p.TH + p.K * p.K + p.K);
     *bytes = 4.0 * b;
     *flops = b;
@@ -902,8 +924,10 @@ int vqhmm_elbo_stage_info(const vqhmm_dims_t* d, int64_t B, int64_t T, int stage
     else if (bwd_pair && stage == S_ENC2_DG) nm = "dec_conv1_dgrad+logits_bwd+to_logits_dgrad+enc_conv2_dgrad";
     else if (stage == S_LOGIT_BWD && logits_bwd_fused(p)) nm = "(logits_bwd: in dec_conv1_dgrad's epilogue)";
     else if (stage == S_LOGIT_DG && logits_dg_fused(p)) nm = "(to_logits_dgrad: in dec_conv1_dgrad's epilogue)";
-    else if (tail_fused_on() && stage == S_REDUCE) nm = "(grad_tail: in the tail launch)";
-    else if (tail_fused_on() && stage == S_COMPOSE_BWD) nm = "tail(grad_tail+compose_bwd[+adam])";
+    else if (p.wgroup && tail_fused_on() && stage == S_REDUCE) nm = "(grad_tail: in the tail launch)";
+    else if (p.wgroup && tail_fused_on() && stage == S_COMPOSE_BWD) nm = "tail(slab reduction+composed dW/dE[+adam])";
+    else if (p.wgroup && stage == S_REDUCE) nm = "grad_tail(slab reduction+composed dW/dE)";
+    else if (p.wgroup && stage == S_COMPOSE_BWD) nm = "[adam]";
     strncpy(name, nm, name_len - 1);
     name[name_len - 1] = 0;
   }
@@ -980,9 +1004,9 @@ int vqhmm_elbo_stage_info(const vqhmm_dims_t* d, int64_t B, int64_t T, int stage
     stage_work(p, S_LOGIT_DG, &f1, &b1, &m1);
     f += f1; b += b1;
   }
-  if (tail_fused_on() && stage == S_REDUCE) {
+  if (p.wgroup && tail_fused_on() && stage == S_REDUCE) {
     f = 0; b = 0;
-  } else if (tail_fused_on() && stage == S_COMPOSE_BWD) {
+  } else if (p.wgroup && tail_fused_on() && stage == S_COMPOSE_BWD) {
     double f1, b1;
     int m1;
     stage_work(p, S_REDUCE, &f1, &b1, &m1);

@@ -22,7 +22,20 @@
 #define VQHMM_ELAUNCH -2
 #define VQHMM_EWORKSPACE -3
 #define VQHMM_EUNSUPPORTED -4
-#define VQHMM_STATUS_TAIL_TIMEOUT 1ull
+#define VQHMM_STATUS_TAIL_TIMEOUT 1ull  // reserved (include/vqhmm.h): no kernel sets it
+
+// Environment knobs.  VQHMM_ENV: the A/B switches the release library honours, each choosing between
+// launch paths the tests prove bit-identical (or, VQHMM_STRIP_HEAD / VQHMM_HEAD, equal within the
+// stated tolerance).  VQHMM_PROF_ENV: tuning and timing experiments that change summation orders,
+// skip work or invalidate results; they exist only in the profiling build (`make PROFILING=1` ->
+// vqhmm/libvqhmm_prof.so, loaded with VQHMM_LIB_PATH).  In the release build the name never reaches
+// the binary and the knob reads as unset.
+#define VQHMM_ENV(name) getenv(name)
+#ifdef VQHMM_PROFILING
+#define VQHMM_PROF_ENV(name) getenv(name)
+#else
+#define VQHMM_PROF_ENV(name) ((const char*)nullptr)
+#endif
 
 namespace vqhmm {
 

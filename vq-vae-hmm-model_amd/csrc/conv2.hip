@@ -247,7 +247,7 @@ __global__ __launch_bounds__((64 * C2wOcc<NB, KCP>::MAXW)) void conv2w_kernel(Co
 // waves per workgroup cap for the wave-independent conv kernels (VQHMM_CONV_WMAX, A/B; read once)
 static int conv_wmax(int dflt) {
   static const int v = [] {
-    const char* e = getenv("VQHMM_CONV_WMAX");
+    const char* e = VQHMM_PROF_ENV("VQHMM_CONV_WMAX");
     return e ? atoi(e) : 0;
   }();
   return v >= 1 && v < dflt ? v : dflt;
@@ -591,20 +591,17 @@ int launch_conv2_bwd_pair(const ConvArgs& a, const ConvArgs& f, hipStream_t s) {
 // VQHMM_CONV_WAVE_ROWS rows (default: always; it measured equal or faster at B = 128 .. 1024)
 // and the workgroup-tile kernel above; VQHMM_CONV_PIPE=0
 // turns the operand pipelining off (A/B).  Read once.
-static int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
+static int env_int(const char* e, int dflt) { return e ? atoi(e) : dflt; }
 static bool conv2_wave_mode(int64_t R) {
   static const int force = [] {
-    const char* e = getenv("VQHMM_CONV");
+    const char* e = VQHMM_PROF_ENV("VQHMM_CONV");
     return !e ? 0 : (e[0] == 'w' && e[1] == 'g') ? 1 : (e[0] == 'w' && e[1] == 'a') ? 2 : 0;
   }();
-  static const int64_t rows = env_int("VQHMM_CONV_WAVE_ROWS", 1 << 30);
+  static const int64_t rows = env_int(VQHMM_PROF_ENV("VQHMM_CONV_WAVE_ROWS"), 1 << 30);
   return force == 2 || (force == 0 && R < rows);
 }
 static bool conv2_pipe() {
-  static const bool v = env_int("VQHMM_CONV_PIPE", 1) != 0;
+  static const bool v = env_int(VQHMM_PROF_ENV("VQHMM_CONV_PIPE"), 1) != 0;
   return v;
 }
 

@@ -274,7 +274,11 @@ __global__ __launch_bounds__(256, 2) void elbo_head_coop_kernel(HeadArgs a) {
     for (int c = si; c < 8; c += KP) uSb[prow * 8 + c] = c < U ? (valid ? cur.u : 0.f) : (c == U ? 1.f : 0.f);
     // K <= 4 (KP = 4, one ij block): wave w wrote rows 16w .. 16w + 15, exactly the row block its phase-A
     // task reads, and phase C reads the others only behind the next two barriers: a wave barrier will do
-    if constexpr (KP == 4 && KB == 1) __builtin_amdgcn_wave_barrier();
+    if constexpr (KP == 4 && KB == 1) {  // wave-scope release / acquire around it, as vq_rows_kernel
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    }
     else lds_barrier();
     if (nwn == 0) stamp_if(a.dbg & 16, 9);
     // ---------------- A: tasks (ij block, 16-row block) over the waves; with 4 ij blocks (K > 6) wave w
@@ -540,7 +544,7 @@ bool head_coop_supported(const HeadArgs& a) {
 // another cap (tuning A/B, read once)
 int head_coop_grid(int64_t R, int K) {
   static const int cap = [] {
-    const char* e = getenv("VQHMM_HEAD_GRID");
+    const char* e = VQHMM_PROF_ENV("VQHMM_HEAD_GRID");
     const int v = e ? atoi(e) : 0;
     return v >= 64 && v <= 1024 ? v : 512;
   }();

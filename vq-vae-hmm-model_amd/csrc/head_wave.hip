@@ -549,7 +549,7 @@ __global__ __launch_bounds__(256, 2) void elbo_head_wave_kernel(HeadArgs a) {
 // more waves finish sooner.  VQHMM_HEAD_NBW=1|4 overrides (A/B).
 static int head_wave_nbw(int64_t R) {
   static const int force = [] {
-    const char* e = getenv("VQHMM_HEAD_NBW");
+    const char* e = VQHMM_PROF_ENV("VQHMM_HEAD_NBW");
     return e ? atoi(e) : 0;
   }();
   if (force == 1 || force == 2 || force == 4) return force;
@@ -562,7 +562,7 @@ static int head_wave_nbw(int64_t R) {
 // lower (tuning A/B, read once)
 int head_wave_grid(int64_t R) {
   static const int cap = [] {
-    const char* e = getenv("VQHMM_HEAD_GRID");
+    const char* e = VQHMM_PROF_ENV("VQHMM_HEAD_GRID");
     const int v = e ? atoi(e) : 0;
     return v >= 64 && v <= 512 ? v : 512;
   }();
@@ -579,7 +579,7 @@ static size_t head_wave_lds(int HB) {
 
 int launch_head_wave(const HeadArgs& a0, int grid, hipStream_t s) {
   static const int dbg = [] {
-    const char* e = getenv("VQHMM_HEAD_DBG");
+    const char* e = VQHMM_PROF_ENV("VQHMM_HEAD_DBG");
     return e ? atoi(e) : 0;
   }();
   HeadArgs a = a0;

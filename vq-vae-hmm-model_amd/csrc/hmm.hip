@@ -1173,7 +1173,7 @@ __global__ __launch_bounds__(256) void fwdbwd_resident_kernel(const float* __res
 
 static int fb_lin_tier() {  // VQHMM_FB_LIN=0: log tier only (A/B switch)
   static const int lin = [] {
-    const char* e = getenv("VQHMM_FB_LIN");
+    const char* e = VQHMM_PROF_ENV("VQHMM_FB_LIN");
     return e && e[0] == '0' ? 0 : 1;
   }();
   return lin;
@@ -1205,7 +1205,7 @@ static DevShape dev_shape() {
 static bool fwdbwd_resident_ok(int64_t B, int64_t K, int64_t T) {
   // VQHMM_FB_RES=0 forces the streaming kernel: a test switch, read per call because the tests
   // run both kernels in one process
-  const char* env = getenv("VQHMM_FB_RES");
+  const char* env = VQHMM_ENV("VQHMM_FB_RES");
   if ((env && env[0] == '0') || K < 1 || K > 8 || T > 4096) return false;
   const int kp = K <= 2 ? 2 : K <= 4 ? 4 : 8;
   const size_t bytes = kp == 2 ? FbRes<2>::lds_bytes((int)T) : kp == 4 ? FbRes<4>::lds_bytes((int)T)
@@ -1223,7 +1223,7 @@ static void fwdbwd_res_go(const float* log_pi, const float* log_A, const float* 
                           int64_t T, float* gamma, float* logZ, void* ws, hipStream_t s) {
   const dim3 grid((unsigned)cdiv(B, FbRes<K>::SPW));
   static const bool prof = [] {
-    const char* e = getenv("VQHMM_FB_PROF");  // diagnostic: per-wave cycle counts into the workspace
+    const char* e = VQHMM_PROF_ENV("VQHMM_FB_PROF");  // diagnostic: per-wave cycle counts into the workspace
     return e && e[0] == '1';
   }();
   fwdbwd_resident_kernel<K><<<grid, 256, FbRes<K>::lds_bytes((int)T), s>>>(

@@ -140,7 +140,7 @@ __global__ __launch_bounds__(256) void fwdbwd_generic_kernel(const float* __rest
     const float mx = block_max(v, red);
     const float n = (mx == -__builtin_inff() ? mx : mx + __logf(block_sum(j < K ? __expf(v - mx) : 0.f, red)));
     lz += (double)n;
-    v -= n;
+    if (n != -__builtin_inff()) v -= n;  // an impossible prefix stays -inf (logZ = -inf, as the fp64 oracle)
     __syncthreads();  // the previous vector is no longer read
     if (j < K) {
       vS[j] = v;
@@ -169,7 +169,7 @@ __global__ __launch_bounds__(256) void fwdbwd_generic_kernel(const float* __rest
       const float bv = j < K ? (m == -__builtin_inff() ? m : m + __logf(s)) : -__builtin_inff();
       const float mx = block_max(bv, red);
       const float n = (mx == -__builtin_inff() ? mx : mx + __logf(block_sum(j < K ? __expf(bv - mx) : 0.f, red)));
-      bt = bv - n;
+      bt = n != -__builtin_inff() ? bv - n : bv;
     }
     const float g = j < K ? al[t * K + j] + bt : -__builtin_inff();
     const float gm = block_max(g, red);

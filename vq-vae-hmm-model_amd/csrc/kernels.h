@@ -122,6 +122,12 @@ struct WgradArgs {
   float* slab;       // [nchunks][N][C][ks]
   float* bias_slab;  // [nchunks][N] or null
   int pipe;          // wgrad2: software-pipelined operand reads (set by the launcher; VQHMM_WGRAD_PIPE=0 A/B)
+  // the composed decoder conv1 (grouped launch; N = H outputs o, C = K inputs k, k = 3, N*C*3 <= 1536):
+  // each chunk also writes its share of the embedding gradient,
+  //   cmp_slab[chunk][k][h] = sum_{o, tap} dWc_chunk[o][k][tap] * cmpW[o][h][tap],
+  // so the backward tail needs no reduced dWc before it can form dE (no cross-workgroup wait)
+  const float* cmpW;  // decoder.conv1.weight (H, H, 3), or null
+  float* cmp_slab;    // [nchunks][K][H]
 };
 
 struct HeadArgs {
@@ -179,11 +185,18 @@ struct LogPriorGradArgs {  // log_prior gradient (misc.hip log_prior_grad_body);
   float* out;
 };
 struct SlabSeg {
-  const float* slab;   // [nchunks][len]
+  const float* slab;   // [nchunks][len] ([nchunks][cmpH * cmpK * 3] for a composed segment)
   float* out;          // [len]
   const float* scale;  // device scalar or null
   int64_t nchunks, len;
+  // composed segment (cmpE set): out[j], j = (o * H + h) * 3 + tap, is the decoder conv1 weight gradient
+  // dW[o][h][tap] = sum_k dWc[o][k][tap] E[k][h] (VQ_VAE_HMM_fixed.py:83-85 folded), where each
+  // block reduces the dWc slab columns of its own o rows itself
+  const float* cmpE;   // (K, H): the embedding as this step's forward used it
+  int cmpH, cmpK;
 };
+// largest dWc column span one 64-column block of a composed segment reduces (block_reduce_cols' 256)
+__host__ __device__ inline int64_t composed_block_cols(int H, int K) { return (int64_t)(2 + 62 / (3 * H)) * 3 * K; }
 
 int launch_vq_argmin(const float* z, int64_t B, int64_t Dv, int64_t T, const float* cb, int64_t K, int32_t* idx,
                      float* dmin, hipStream_t s);
@@ -253,11 +266,12 @@ struct WgradGroup {
   int variant[MAX_WJOBS], wn[MAX_WJOBS], wc[MAX_WJOBS];
   int64_t blk0[MAX_WJOBS + 1];
   int njobs;
+  int64_t* step_inc;  // non-null: the Adam step counter this backward's tail applies; workgroup 0 advances it
 };
 bool wgrad2_group_supported(const WgradArgs& a);
 // a grouped job's rows per chunk (a multiple of its stage rows: 64, or 192 for the small outputs)
 int64_t wgrad2_group_rows(int64_t rows, int N, int C, int ks);
-int launch_wgrad2_group(const WgradArgs* jobs, int n, hipStream_t s);
+int launch_wgrad2_group(const WgradArgs* jobs, int n, hipStream_t s, int64_t* step_inc = nullptr);
 // Staged ELBO head (head_staged.hip): shapes the fused heads do not cover.
 struct StagedHeadArgs {
   int64_t B;
@@ -335,10 +349,10 @@ struct AdamArgs {
   double lr, b1, b2, eps;
   float gmul;
 };
-// The step's last launch when Adam is fused (single process): the composed decoder conv1's
+// The non-grouped path's composed decoder conv1 (a launch after grad_tail reduced dWc):
 // dW[o][h][tap] = sum_k dWc[o][k][tap] E[k][h] and dE[k][h] = sum_{o,tap} dWc[o][k][tap] W[o][h][tap]
-// written into g (E, W: the prologue's copies, since this launch updates the parameters), then
-// every element's Adam update.
+// written into g, then (compose_adam) every element's Adam update; E, W: the prologue's copies, since
+// that launch updates the parameters.
 struct ComposeAdamArgs {
   const float* dWc;      // (H, K, 3) reduced
   const float* Ecopy;    // (K, H)
@@ -350,10 +364,11 @@ struct ComposeAdamArgs {
   AdamArgs adam;
 };
 int launch_compose_adam(const ComposeAdamArgs& a, hipStream_t s);
-// grad_tail + compose_bwd (+ Adam: compose_adam) in one launch (misc.hip tail_kernel): ta.s[dwc_seg]
-// is the composed layer's dWc segment (ca.dWc == its out); *sync zeroed by the step's prologue
-int launch_tail(TailArgs& ta, const ComposeAdamArgs& ca, int dwc_seg, unsigned long long* sync, bool adam,
-                hipStream_t s);
+// The backward tail in ONE launch (misc.hip tail_kernel): grad_tail's blocks, each (adam != null) then
+// applying Adam to the columns it has just reduced; the composed segment's blocks form dW themselves,
+// so no block waits for another.  g = the flat gradient buffer the segments write into.  With adam, an
+// earlier launch of the same step must have advanced *adam->step (launch_wgrad2_group's step_inc).
+int launch_tail(TailArgs& ta, const AdamArgs* adam, const float* g, hipStream_t s);
 int launch_grad_tail(TailArgs& a, hipStream_t s);
 int launch_finalize_loss(const double* part, int nblk, const int64_t* lengths, const int64_t* norm, int64_t B, int T,
                          int D, float beta, float* loss, double* accum, float* pieces, hipStream_t s);
@@ -376,10 +391,9 @@ struct PrologueArgs {  // step prologue: x, u -> PCL, the composed decoder conv1
   float* wc_img_f;  // images of the composed decoder conv1 (forward / data gradient), or null
   float* wc_img_d;
   float* Ecopy;     // (K, H) / (H, H, 3) copies of the embedding and decoder.conv1's weight for the
-  float* Wcopy;     // fused compose + Adam launch, or null
+  float* Wcopy;     // launches that read them while Adam updates the parameters, or null
   const int64_t* lengths;  // with cnt: the last block writes the batch's valid count
   int64_t* cnt;            // (sum_b min(max(L_b, 0), T)) for a loss finalized in the backward, or null
-  unsigned long long* sync;  // zeroed: the backward tail's in-launch counter (launch_tail), or null
   // the cooperative head's Prior MLP weights in its LDS layout (head_coop_image_floats), or himg = null:
   // [W2 rows ij (16 * ceil(K^2 / 16) of them, zero past K^2) x (TH + 4) | W1' = [W1 | b1 | 0] (TH x 8)]
   const float *hW1, *hb1, *hW2;

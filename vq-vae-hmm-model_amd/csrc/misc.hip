@@ -95,11 +95,37 @@ __device__ void block_reduce_cols(const float* slab, int64_t nch, int64_t ld, in
 // Columns [64 (blockIdx.x - blk_start[si]), +64) of segment si summed over its chunks (fixed order)
 // and written to sg.out; returns the segment index (the caller's block is one of its blocks).
 // Threads < 64 hold their column's value in *val (valid when *col < len).
-__device__ int tail_segment_block(const TailArgs& ta, float (&part)[16][64], float* val, int64_t* colp) {
+// Composed segment (SlabSeg::cmpE): the block's 64 columns of dW lie in o rows o_lo .. o_hi; it reduces
+// those rows' dWc columns (3K each, contiguous in the slab) over the chunks itself, then forms
+// dW[o][h][tap] = sum_k dWc[o][k][tap] E[k][h] (fmaf chain over k, as compose_adam_block).
+__device__ void tail_composed_block(const SlabSeg& sg, int64_t col0, float* red, float* scratch, float* val,
+                                    int64_t* colp) {
+  const int H = sg.cmpH, K = sg.cmpK, L3 = 3 * K;
+  const int64_t o_lo = col0 / (3 * H), o_hi = min(col0 + 63, sg.len - 1) / (3 * H);
+  block_reduce_cols(sg.slab, sg.nchunks, (int64_t)H * L3, o_lo * L3, (int)((o_hi - o_lo + 1) * L3), red, scratch);
+  const int64_t col = col0 + threadIdx.x;
+  if (threadIdx.x < 64 && col < sg.len) {
+    const int o = (int)(col / (3 * H)), rem = (int)(col - (int64_t)o * 3 * H), h = rem / 3, tap = rem - 3 * h;
+    const float* dwc = red + (o - o_lo) * L3;
+    float v = 0.f;
+    for (int k = 0; k < K; ++k) v = fmaf(dwc[k * 3 + tap], sg.cmpE[(int64_t)k * H + h], v);
+    if (sg.scale) v *= *sg.scale;
+    sg.out[col] = v;
+    *val = v;
+  }
+  *colp = col;
+}
+
+__device__ int tail_segment_block(const TailArgs& ta, float (&part)[16][64], float* red, float* scratch, float* val,
+                                  int64_t* colp) {
   int si = 0;
   while (si + 1 < ta.nseg && (int64_t)blockIdx.x >= ta.blk_start[si + 1]) ++si;
   const SlabSeg& sg = ta.s[si];
   const int64_t col0 = ((int64_t)blockIdx.x - ta.blk_start[si]) * 64;
+  if (sg.cmpE) {
+    tail_composed_block(sg, col0, red, scratch, val, colp);
+    return si;
+  }
   const bool vec = (sg.len % 4 == 0) && ((reinterpret_cast<uintptr_t>(sg.slab) & 15) == 0);
   int nph;
   if (vec) {
@@ -185,47 +211,16 @@ __device__ void tail_logprior_block(const TailArgs& ta, float* red, float* scrat
   }
 }
 
-// One workgroup = 64 consecutive columns of one segment x all its chunks (where a segment's rows
-// are float4-aligned, 16 lanes x float4 cover the 64 columns and 16 chunk phases keep 16 x 8 wide
-// loads in flight per column group; otherwise 64 lanes x 4 phases of scalar loads), or (last
-// block, q0slab set) the log_prior gradient.  Phases combine in a fixed order.
-__global__ __launch_bounds__(256) void grad_tail_kernel(TailArgs ta) {
-  __shared__ float part[16][64];
-  __shared__ float red[256];
-  __shared__ float scratch[256];
-  const int64_t nblk = ta.blk_start[ta.nseg];
-  if (ta.fin_loss && (int64_t)blockIdx.x == nblk + (ta.q0slab ? 1 : 0)) {  // ---- the forward's loss
-    __shared__ double fred[5 * 256];
-    finalize_loss_block(ta.fin_part, ta.fin_nblk, nullptr, ta.lp.norm, ta.fin_B, ta.fin_T, ta.fin_D, ta.lp.beta,
-                        ta.fin_loss, ta.fin_accum, ta.fin_pieces, fred, ta.fin_cnt);
-    return;
-  }
-  if ((int64_t)blockIdx.x >= nblk) {  // ---- log_prior gradient
-    tail_logprior_block(ta, red, scratch);
-    return;
-  }
-  float v;
-  int64_t col;
-  tail_segment_block(ta, part, &v, &col);
-}
+// grad_tail (the tail without Adam) is tail_kernel<false>: one workgroup = 64 consecutive columns of one
+// segment x all its chunks (where a segment's rows are float4-aligned, 16 lanes x float4 cover the 64
+// columns and 16 chunk phases keep 16 x 8 wide loads in flight per column group; otherwise 64 lanes x 4
+// phases of scalar loads), or (q0slab set) the log_prior gradient, or the loss finalize.  Phases combine in
+// a fixed order.
 
-int launch_grad_tail(TailArgs& a, hipStream_t s) {
-  if (a.nseg > MAX_SEGS || (a.q0slab && a.lp.K > 256)) return VQHMM_EINVAL;
-  a.blk_start[0] = 0;
-  for (int i = 0; i < a.nseg; ++i) a.blk_start[i + 1] = a.blk_start[i] + cdiv(a.s[i].len, 64);
-  const int64_t nb = a.blk_start[a.nseg] + (a.q0slab ? 1 : 0) + (a.fin_loss ? 1 : 0);
-  if (nb == 0) return VQHMM_OK;
-  grad_tail_kernel<<<(unsigned)nb, 256, 0, s>>>(a);
-  VQHMM_LAUNCH_CHECK();
-  return VQHMM_OK;
-}
-
-// Blocks [0, nb): 256 consecutive elements each: gradient (decoder.conv1 weight from dWc and the
-// embedding copy; every other element as reduced) then Adam.  Blocks nb .. nb+K-1: one embedding
-// row k each, dE[k][h] with 4 thread groups splitting o (combined in a fixed order), then Adam.
-// composed decoder conv1: element block cb < cdiv(H*H*3, 256) of dW (256 elements), else row
-// k = cb - that of dE; gradient into g, then Adam (compose_adam_kernel / tail_adam_kernel)
-// pre: this thread's Adam element of a dW block, already loaded (or null)
+// The non-grouped path's composed decoder conv1 from the reduced dWc: element block cb < cdiv(H*H*3, 256)
+// of dW (256 elements), else row k = cb - that of dE (4 thread groups splitting o, combined in a fixed
+// order); gradient into g, then (ADAM) Adam.  pre: this thread's Adam element of a dW block, already
+// loaded (or null)
 template <bool ADAM>
 __device__ void compose_adam_block(const ComposeAdamArgs& a, int64_t cb, int64_t tn, float (&part)[4][256],
                                    const AdamElem* pre = nullptr) {
@@ -288,139 +283,67 @@ __global__ __launch_bounds__(256) void compose_adam_kernel(ComposeAdamArgs a) {
   adam_ticket(ad.step, tn);
 }
 
-// The whole backward tail in ONE launch: grad_tail's blocks (ADAM: each then applies Adam to the
-// columns it has just reduced), then the composed decoder conv1's dW / dE blocks
-// (compose_adam_block; ADAM: + their Adam).  Block order: [segment blocks][log_prior][loss
-// finalize][composed].  The composed blocks need the whole reduced dWc: every block of the dWc
-// segment drains its stores, releases them (agent fence) and adds 1 to sync[0]; a composed block
-// polls sync[0] (bounded, relaxed loads, one acquire fence after) until it reaches the segment's
-// block count.
-// Progress relies on IN-ORDER workgroup dispatch, not on co-residency: every dWc block has a lower
-// block index than every waiting block, so it is dispatched (and, never waiting itself, finishes)
-// before any waiting block can hold a CU slot it needs.  At cfg3 dims (H = 256) the grid is a few
-// thousand blocks, more than are resident at once; the H = 256 case of
-// tests/test_gpu_trainer.py::test_fused_tail_adam_bit_identical runs that shape.
-// sync[0] arrivals, sync[1] departures: the last composed block to depart zeroes both, so the next
-// launch (a re-run of the backward alone included) starts from 0 (the prologue zeroes them too).
-// sync[2] is the status word (VQHMM_STATUS_*): a wait that runs out of polls ORs in
-// VQHMM_STATUS_TAIL_TIMEOUT and its block skips the composed gradient; the host reads the word
-// (vqhmm_elbo_status_offset) and raises.  It is only ever set here, never cleared.
+// The whole backward tail in ONE launch: grad_tail's blocks, each (ADAM) then applying Adam to the columns
+// it has just reduced (their Adam operands are loaded before the reduction).  Block order: [segment
+// blocks][log_prior][loss finalize].  Every block works alone: the composed decoder conv1's dW blocks reduce
+// their own dWc rows (tail_composed_block) and its dE arrives as a per-chunk slab from the weight-gradient
+// launch (WgradArgs::cmp_slab), so no block waits for another and nothing depends on dispatch order.
+// ADAM: the step counter was already advanced by an earlier launch of the same backward (the grouped
+// weight-gradient launch, WgradGroup::step_inc), so every block reads this step's count as it is: no
+// completion ticket (560 same-address atomics cost ~5 us at B = 128).
 template <bool ADAM>
-__global__ __launch_bounds__(256) void tail_kernel(TailArgs ta, ComposeAdamArgs a, int dwc_seg, int dwc_blocks,
-                                                   unsigned long long* sync, int spin_limit, int ncomp) {
+__global__ __launch_bounds__(256) void tail_kernel(TailArgs ta, AdamArgs ad, const float* g) {
   __shared__ float part[16][64];
   __shared__ float red[256];
   __shared__ float scratch[256];
-  __shared__ float cpart[4][256];
-  const AdamArgs& ad = a.adam;
-  const int64_t tn = ADAM ? (*ad.step & 0xffffffffll) + 1 : 0;
+  const int64_t tn = ADAM ? (*ad.step & 0xffffffffll) : 0;
   const int64_t nblk = ta.blk_start[ta.nseg];
   const int64_t b = blockIdx.x;
-  const int64_t finb = nblk + (ta.q0slab ? 1 : 0), comp0 = finb + (ta.fin_loss ? 1 : 0);
+  const int64_t finb = nblk + (ta.q0slab ? 1 : 0);
   if (b < nblk) {
     AdamElem e{};
     if constexpr (ADAM) {  // this column's Adam operands in flight across the slab reduction
       int sj = 0;
       while (sj + 1 < ta.nseg && b >= ta.blk_start[sj + 1]) ++sj;
       const int64_t c = (b - ta.blk_start[sj]) * 64 + threadIdx.x;
-      if (sj != dwc_seg && threadIdx.x < 64 && c < ta.s[sj].len) e = adam_load(ad, (ta.s[sj].out - a.g) + c, tn);
+      if (threadIdx.x < 64 && c < ta.s[sj].len) e = adam_load(ad, (ta.s[sj].out - g) + c, tn);
     }
     float v = 0.f;
     int64_t col;
-    const int si = tail_segment_block(ta, part, &v, &col);
+    const int si = tail_segment_block(ta, part, red, scratch, &v, &col);
     const SlabSeg& sg = ta.s[si];
-    if (si == dwc_seg) {
-      // producer hand-off (MI355X_MICROARCH.md, inter-workgroup visibility): every storing wave
-      // drains, barrier, one release, drain again (the compiler may drop the fence's own wait),
-      // then the relaxed agent-scope arrival
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_fetch_add(sync, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    } else if (ADAM && threadIdx.x < 64 && col < sg.len) {
-      adam_apply(ad, (sg.out - a.g) + col, v, e);
-    }
+    if (ADAM && threadIdx.x < 64 && col < sg.len) adam_apply(ad, (sg.out - g) + col, v, e);
   } else if (ta.q0slab && b == nblk) {
     tail_logprior_block(ta, red, scratch);
     if (ADAM && threadIdx.x == 0)
       for (int k = 0; k < ta.lp.K; ++k) {
-        const int64_t i = (ta.lp.out - a.g) + k;
+        const int64_t i = (ta.lp.out - g) + k;
         adam_apply(ad, i, ta.lp.out[k], adam_load(ad, i, tn));
       }
   } else if (ta.fin_loss && b == finb) {
     __shared__ double fred[5 * 256];
     finalize_loss_block(ta.fin_part, ta.fin_nblk, nullptr, ta.lp.norm, ta.fin_B, ta.fin_T, ta.fin_D, ta.lp.beta,
                         ta.fin_loss, ta.fin_accum, ta.fin_pieces, fred, ta.fin_cnt);
-  } else {
-    const int64_t cb = b - comp0, jw = cb * 256 + threadIdx.x;
-    const bool dw = cb < cdiv((int64_t)a.H * a.H * 3, 256) && jw < (int64_t)a.H * a.H * 3;
-    AdamElem e{};
-    if (ADAM && dw) e = adam_load(ad, a.off_w + jw, tn);  // in flight across the wait
-    __shared__ int arrived;
-    if (threadIdx.x == 0) {
-      int got = 0;
-      for (int spin = 0; spin < spin_limit; ++spin) {
-        // relaxed: an acquire load would invalidate this XCD's L2 on every poll
-        if (__hip_atomic_load(sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned long long)dwc_blocks) {
-          got = 1;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      if (!got)
-        __hip_atomic_fetch_or(sync + 2, (unsigned long long)VQHMM_STATUS_TAIL_TIMEOUT, __ATOMIC_RELAXED,
-                              __HIP_MEMORY_SCOPE_AGENT);
-      arrived = got;
-    }
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    if (arrived) compose_adam_block<ADAM>(a, cb, tn, cpart, dw ? &e : nullptr);
-    __syncthreads();
-    if (threadIdx.x == 0) {  // departure; the last one re-arms the counters for the next launch
-      const unsigned long long d = __hip_atomic_fetch_add(sync + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (d == (unsigned long long)(ncomp - 1)) {
-        __hip_atomic_store(sync, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(sync + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
   }
-  if constexpr (ADAM) adam_ticket(ad.step, tn);
 }
 
-// Test hook, read once: VQHMM_TAIL_TEST_TIMEOUT=1 makes the composed blocks wait for a count that
-// never arrives, with a short poll budget, so a test can see the status word raised.
-static bool tail_test_timeout() {
-  static const bool v = [] {
-    const char* e = getenv("VQHMM_TAIL_TEST_TIMEOUT");
-    return e && e[0] == '1';
-  }();
-  return v;
-}
-
-int launch_tail(TailArgs& ta, const ComposeAdamArgs& ca, int dwc_seg, unsigned long long* sync, bool adam,
-                hipStream_t s) {
-  if (ta.nseg > MAX_SEGS || (ta.q0slab && ta.lp.K > 256) || dwc_seg < 0 || dwc_seg >= ta.nseg || !sync)
-    return VQHMM_EINVAL;
+int launch_tail(TailArgs& ta, const AdamArgs* adam, const float* g, hipStream_t s) {
+  if (ta.nseg > MAX_SEGS || (ta.q0slab && ta.lp.K > 256)) return VQHMM_EINVAL;
+  for (int i = 0; i < ta.nseg; ++i)
+    if (ta.s[i].cmpE && composed_block_cols(ta.s[i].cmpH, ta.s[i].cmpK) > 256) return VQHMM_EINVAL;
   ta.blk_start[0] = 0;
   for (int i = 0; i < ta.nseg; ++i) ta.blk_start[i + 1] = ta.blk_start[i] + cdiv(ta.s[i].len, 64);
-  const int64_t ncomp = cdiv((int64_t)ca.H * ca.H * 3, 256) + ca.K;
-  const int64_t nb = ta.blk_start[ta.nseg] + (ta.q0slab ? 1 : 0) + (ta.fin_loss ? 1 : 0) + ncomp;
-  int dwc_blocks = (int)cdiv(ta.s[dwc_seg].len, 64);
-  int spin_limit = 1 << 22;  // x ~s_sleep(1): about 0.2 s before the wait gives up
-  if (tail_test_timeout()) {
-    dwc_blocks += 1 << 30;
-    spin_limit = 1 << 10;
-  }
+  const int64_t nb = ta.blk_start[ta.nseg] + (ta.q0slab ? 1 : 0) + (ta.fin_loss ? 1 : 0);
+  if (nb == 0) return VQHMM_OK;
   if (adam)
-    tail_kernel<true><<<(unsigned)nb, 256, 0, s>>>(ta, ca, dwc_seg, dwc_blocks, sync, spin_limit, (int)ncomp);
+    tail_kernel<true><<<(unsigned)nb, 256, 0, s>>>(ta, *adam, g);
   else
-    tail_kernel<false><<<(unsigned)nb, 256, 0, s>>>(ta, ca, dwc_seg, dwc_blocks, sync, spin_limit, (int)ncomp);
+    tail_kernel<false><<<(unsigned)nb, 256, 0, s>>>(ta, AdamArgs{}, g);
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
 }
+
+int launch_grad_tail(TailArgs& a, hipStream_t s) { return launch_tail(a, nullptr, nullptr, s); }
 
 int launch_compose_adam(const ComposeAdamArgs& a, hipStream_t s) {
   const int64_t nb = cdiv(a.n, 256) + cdiv((int64_t)a.H * a.H * 3, 256) + a.K;
@@ -734,7 +657,6 @@ __device__ __forceinline__ void himg_slice(const PrologueArgs& a, int64_t i0) {
 __global__ __launch_bounds__(256) void prologue_kernel(PrologueArgs a) {
   extern __shared__ float cs[];
   const unsigned bx = blockIdx.x;
-  if (bx == 0 && threadIdx.x < 2 && a.sync) a.sync[threadIdx.x] = 0ull;  // the backward tail's counters
   if (bx < a.nbx) {
     to_pcl_slot(a.x, a.D, a.B, a.T, a.xsc, a.xst, a.xp, (int64_t)bx * 256 + threadIdx.x);
   } else if (bx < a.nbx + a.nbu) {

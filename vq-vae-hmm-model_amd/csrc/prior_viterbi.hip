@@ -301,7 +301,7 @@ bool prior_viterbi_supported(const PriorArgs& p) {
 // profiling switch (VQHMM_PV_MODE: 1 = no chain, 2 = no tables; results then invalid)
 static int pv_mode() {
   static const int m = [] {
-    const char* e = getenv("VQHMM_PV_MODE");
+    const char* e = VQHMM_PROF_ENV("VQHMM_PV_MODE");
     return e ? atoi(e) : 0;
   }();
   return m;

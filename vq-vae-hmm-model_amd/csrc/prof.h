@@ -21,11 +21,13 @@ __device__ __forceinline__ void stamp_if(bool on, int k) {
   if (on && threadIdx.x == 0 && blockIdx.x < 256) g_prof[blockIdx.x * 16 + k] = __builtin_amdgcn_s_memrealtime();
 }
 
-// the environment switch of one kernel family, read once
-inline int prof_env(const char* name) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : 0;
-}
+// the environment switch of one kernel family, read once; profiling build only (common.h VQHMM_PROF_ENV)
+inline int prof_env_value(const char* e) { return e ? atoi(e) : 0; }
+#ifdef VQHMM_PROFILING
+#define prof_env(name) prof_env_value(getenv(name))
+#else
+#define prof_env(name) prof_env_value(nullptr)
+#endif
 
 inline int prof_copy(uint64_t* out, int64_t n) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;

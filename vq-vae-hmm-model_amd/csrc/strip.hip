@@ -1026,7 +1026,7 @@ static StripFwdArgs strip_fwd_args(const ConvArgs& e1, const ConvArgs& e2, const
   a.h1e = e1.out; a.h2e = e2.out; a.logits = e2.t_out; a.q = e2.q_out; a.g1 = d1.out; a.g2 = d2.out; a.par = d2.t_out;
   a.nstrip = cdiv(e1.R, ST_OWN);
   static const int dbg = [] {
-    const char* e = getenv("VQHMM_STRIP_DBG");
+    const char* e = VQHMM_PROF_ENV("VQHMM_STRIP_DBG");
     return e ? atoi(e) : 0;
   }();
   a.dbg = dbg;

@@ -448,14 +448,13 @@ __global__ __launch_bounds__(256) void vq_sse_finalize_kernel(const double* __re
   if (threadIdx.x == 0) *sse = red[0];
 }
 
-static int env_int(const char* name, int dflt, int lo, int hi) {
-  const char* e = getenv(name);
+static int env_int(const char* e, int dflt, int lo, int hi) {
   const int v = e ? atoi(e) : dflt;
   return v >= lo && v <= hi ? v : dflt;
 }
 
 static int64_t persistent_waves(int64_t tiles, int dflt = 8) {
-  static const int wpc = env_int("VQHMM_VQ_WPC", 0, 1, 32);  // tuning knob: resident waves per CU
+  static const int wpc = env_int(VQHMM_PROF_ENV("VQHMM_VQ_WPC"), 0, 1, 32);  // tuning knob: resident waves per CU
   return std::min<int64_t>(tiles, 256 * (int64_t)(wpc ? wpc : dflt));
 }
 
@@ -473,7 +472,7 @@ static int64_t rows_waves(int64_t N) {  // one wave per SIMD measured best (cfg3
 template <int DG, int CB>
 static void launch_rows(const float* z, int64_t B, int Dv, int T, const float* cb, int K, int32_t* idx, float* dmin,
                         hipStream_t s, float* zq_st = nullptr, double* part = nullptr) {
-  static const int nbuf = env_int("VQHMM_VQ_NBUF", 2, 2, 3);  // tuning knob: register sets in flight
+  static const int nbuf = env_int(VQHMM_PROF_ENV("VQHMM_VQ_NBUF"), 2, 2, 3);  // tuning knob: register sets in flight
   const int64_t tiles = cdiv(B * (int64_t)T, 64);
   const int64_t waves = rows_waves(B * (int64_t)T);
   const unsigned grid = (unsigned)(waves / 4);
@@ -506,7 +505,7 @@ static bool dispatch_rows(const float* z, int64_t B, int Dv, int T, const float*
 }
 
 static bool rows_path(const float* z, int64_t B, int64_t Dv, int64_t T, int64_t K) {
-  static const int impl = env_int("VQHMM_VQ_IMPL", 0, 0, 2);  // 0 auto, 1 tile-32, 2 rows
+  static const int impl = env_int(VQHMM_PROF_ENV("VQHMM_VQ_IMPL"), 0, 0, 2);  // 0 auto, 1 tile-32, 2 rows
   const int64_t N = B * T;
   const bool rows_ok = T % 4 == 0 && (reinterpret_cast<uintptr_t>(z) & 15) == 0 && N * Dv < (int64_t(1) << 30);
   return K <= 32 && rows_ok && impl != 1 && (Dv == 4 || Dv == 8 || Dv == 16 || Dv == 32 || Dv == 64);
@@ -548,7 +547,7 @@ int launch_vq_argmin(const float* z, int64_t B, int64_t Dv, int64_t T, const flo
   const int64_t N = B * T;
   if (N == 0) return VQHMM_OK;
   if (K <= 0 || Dv <= 0 || Dv > 2048 || T <= 0 || T > INT32_MAX) return VQHMM_EINVAL;
-  static const int impl = env_int("VQHMM_VQ_IMPL", 0, 0, 2);  // 0 auto, 1 tile-32, 2 rows
+  static const int impl = env_int(VQHMM_PROF_ENV("VQHMM_VQ_IMPL"), 0, 0, 2);  // 0 auto, 1 tile-32, 2 rows
   const bool rows_ok = T % 4 == 0 && (reinterpret_cast<uintptr_t>(z) & 15) == 0 && N * Dv < (int64_t(1) << 30);
   if (K <= 32 && Dv <= 64 && rows_ok && impl != 1) {
     const bool done = K <= 16 ? dispatch_rows<1>(z, B, (int)Dv, (int)T, cb, (int)K, idx, dmin, s)

@@ -37,6 +37,46 @@ constexpr int w2_max(int a, int b) { return a > b ? a : b; }
 constexpr int W2_LDS_MAX = w2_max(w2_max(w2_lds_floats<64, 64>(), w2_lds_floats<16, 16, RT_S4>()),
                                   w2_max(w2_lds_floats<16, 64, RT_S>(), w2_lds_floats<64, 16, RT_S>()));
 
+// The composed decoder conv1's embedding-gradient share of one chunk (WgradArgs::cmpW; N = H <= 64 outputs o,
+// C = K <= 8 inputs k): cmp_slab[chunk][k][h] = sum_{o, tap} dWc[o][k][tap] W[o][h][tap] from the chunk's dWc
+// in LDS (cbuf, the slab layout); 4 thread groups split o (o = g, g + 4, ...), combined in a fixed order
+// through part (4 * 8 * 64 floats, the free stage buffer).  dE = sum over chunks (the backward tail).
+__device__ __forceinline__ void wgrad_compose_de(const WgradArgs& a, int64_t chunk, const float* cbuf, float* part) {
+  const int H = a.N, K = a.C, tid = threadIdx.x, h = tid & 63, g = tid >> 6;
+  // all 48 weight loads in flight at once (clamped addresses, no branch), across the barrier that publishes
+  // cbuf: one memory latency instead of a chain of them
+  float w[16][3];
+  const int hc = h < H ? h : H - 1;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int o = min(g + 4 * i, H - 1);
+#pragma unroll
+    for (int tap = 0; tap < 3; ++tap) w[i][tap] = a.cmpW[((int64_t)o * H + hc) * 3 + tap];
+  }
+  __syncthreads();  // cbuf (this chunk's dWc) complete
+  float acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int o = g + 4 * i;
+    if (o < H && h < H)
+#pragma unroll
+      for (int tap = 0; tap < 3; ++tap)
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (k < K) acc[k] = fmaf(cbuf[(o * K + k) * 3 + tap], w[i][tap], acc[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) part[(g * 8 + k) * 64 + h] = acc[k];
+  __syncthreads();
+  for (int i = tid; i < K * H; i += 256) {
+    const int k = i / H, hh = i - k * H;
+    const float v = ((part[k * 64 + hh] + part[(8 + k) * 64 + hh]) + part[(16 + k) * 64 + hh]) + part[(24 + k) * 64 + hh];
+    a.cmp_slab[chunk * K * H + i] = v;
+  }
+}
+
 // One chunk (workgroup) of the split-K weight gradient; smem = w2_lds_floats<NPAD, CPAD>() floats.
 // PK (k = 3, 3*C <= 16): the three taps share ONE 16-wide MFMA column block, column j = tap*C + c
 // (a per-lane gather from the X stage), so a narrow-input layer (enc_conv1 C = 5, the composed
@@ -239,12 +279,19 @@ __device__ __forceinline__ void wgrad2_body(const WgradArgs& a, int WN, int WC, 
             const int n = (wn + i * WN) * 16 + 4 * lg4 + v;
             const int c = (wc + j * WC) * 16 + l16;
             if constexpr (PK) {
-              if (n < a.N && pvalid) out[((int64_t)n * a.C + pcc) * KS + ptap] = acc[tp][i][j][v];
+              if (n < a.N && pvalid) {
+                out[((int64_t)n * a.C + pcc) * KS + ptap] = acc[tp][i][j][v];
+                if (a.cmpW) xbuf[(n * a.C + pcc) * KS + ptap] = acc[tp][i][j][v];
+              }
             } else {
-              if (n < a.N && c < a.C) out[((int64_t)n * a.C + c) * KS + tp] = acc[tp][i][j][v];
+              if (n < a.N && c < a.C) {
+                out[((int64_t)n * a.C + c) * KS + tp] = acc[tp][i][j][v];
+                if (a.cmpW) xbuf[(n * a.C + c) * KS + tp] = acc[tp][i][j][v];
+              }
             }
           }
   }
+  if (a.cmpW) wgrad_compose_de(a, chunk, xbuf, smem);  // the composed decoder conv1: this chunk's dE share
   if (a.bias_slab) {
     __syncthreads();
     bred[tid] = bacc;
@@ -281,6 +328,7 @@ __global__ __launch_bounds__(256) void wgrad2_kernel(WgradArgs a, int WN, int WC
 __global__ __launch_bounds__(256) void wgrad2_group_kernel(WgradGroup g) {
   extern __shared__ float4 smem4[];
   float* sm = reinterpret_cast<float*>(smem4);  // W2_LDS_MAX floats
+  if (g.step_inc && blockIdx.x == 0 && threadIdx.x == 0) *g.step_inc = (*g.step_inc & 0xffffffffll) + 1;
   int j = 0;
   while (j + 1 < g.njobs && (int64_t)blockIdx.x >= g.blk0[j + 1]) ++j;
   const WgradArgs& a = g.job[j];
@@ -298,7 +346,7 @@ __global__ __launch_bounds__(256) void wgrad2_group_kernel(WgradGroup g) {
 // A/B switch: VQHMM_WGRAD_PACK=0 keeps the tap-major form for narrow inputs (read once)
 static bool packed_taps() {
   static const bool v = [] {
-    const char* e = getenv("VQHMM_WGRAD_PACK");
+    const char* e = VQHMM_PROF_ENV("VQHMM_WGRAD_PACK");
     return !(e && e[0] == '0');
   }();
   return v;
@@ -339,14 +387,19 @@ int64_t wgrad2_group_rows(int64_t rows, int N, int C, int ks) {
 
 bool wgrad2_group_supported(const WgradArgs& a) {
   int wn, wc;
-  return !a.x_cf && a.N <= 64 && a.C <= 64 && (a.ks == 1 || a.ks == 3) && w2_variant(a.N, a.C, a.ks, &wn, &wc) >= 0;
+  const int v = w2_variant(a.N, a.C, a.ks, &wn, &wc);
+  if (a.x_cf || a.N > 64 || a.C > 64 || (a.ks != 1 && a.ks != 3) || v < 0) return false;
+  // the composed epilogue: dWc fits the row-wave buffer (1536 floats), one row-wave, K <= 8 accumulators
+  if (a.cmpW) return a.ks == 3 && a.C <= 8 && a.N * a.C * 3 <= 1536 && (v == 20 || (v % 10 != 5 && v % 10 != 6 && v % 10 != 8));
+  return true;
 }
 
-int launch_wgrad2_group(const WgradArgs* jobs, int n, hipStream_t s) {
+int launch_wgrad2_group(const WgradArgs* jobs, int n, hipStream_t s, int64_t* step_inc) {
   if (n < 1 || n > MAX_WJOBS) return VQHMM_EINVAL;
   WgradGroup g{};
+  g.step_inc = step_inc;
   static const bool pipe = [] {
-    const char* e = getenv("VQHMM_WGRAD_PIPE");
+    const char* e = VQHMM_PROF_ENV("VQHMM_WGRAD_PIPE");
     return !(e && e[0] == '0');
   }();
   // biggest outputs first (their chunks run longest)
@@ -381,7 +434,7 @@ bool wgrad2_supported(const WgradArgs& a) { return !a.x_cf && a.N <= 64 && a.C <
 // shorter tail (cfg2 step 128 / 192 / 256 / 512 chunks: 0.4735 / 0.4728 / 0.4817 / 0.485 ms)
 static int64_t big_chunks() {
   static const int64_t n = [] {
-    const char* e = getenv("VQHMM_WGRAD_BIG_CHUNKS");
+    const char* e = VQHMM_PROF_ENV("VQHMM_WGRAD_BIG_CHUNKS");
     const long v = e ? atol(e) : 0;
     return (int64_t)(v >= 64 && v <= 4096 ? v : 192);
   }();
@@ -391,7 +444,7 @@ static int64_t big_chunks() {
 // chunks for every output size (experiment override VQHMM_WGRAD_CHUNKS, read once; 0 = default)
 static int64_t all_chunks() {
   static const int64_t n = [] {
-    const char* e = getenv("VQHMM_WGRAD_CHUNKS");
+    const char* e = VQHMM_PROF_ENV("VQHMM_WGRAD_CHUNKS");
     const long v = e ? atol(e) : 0;
     return (int64_t)(v >= 64 && v <= 65536 ? v : 0);
   }();
@@ -401,7 +454,7 @@ static int64_t all_chunks() {
 // chunks for small outputs (N * C * ks < 4096; override VQHMM_WGRAD_SMALL_CHUNKS, read once)
 static int64_t small_chunks() {
   static const int64_t n = [] {
-    const char* e = getenv("VQHMM_WGRAD_SMALL_CHUNKS");
+    const char* e = VQHMM_PROF_ENV("VQHMM_WGRAD_SMALL_CHUNKS");
     const long v = e ? atol(e) : 0;
     return (int64_t)(v >= 64 && v <= 4096 ? v : 512);
   }();
@@ -421,7 +474,7 @@ static int launch_w2(const WgradArgs& a, int WN, int WC, hipStream_t s) {
   if (WR > 1 && (NBW * CBW != 1 || KS * 4 * 64 * (4 / WR) > 1536)) return VQHMM_EUNSUPPORTED;
   if (WN * WC * WR != 4) return VQHMM_EINVAL;
   static const bool pipe = [] {
-    const char* e = getenv("VQHMM_WGRAD_PIPE");
+    const char* e = VQHMM_PROF_ENV("VQHMM_WGRAD_PIPE");
     return !(e && e[0] == '0');
   }();
   WgradArgs ap = a;

@@ -302,8 +302,10 @@ class TrainState:
                 print(f"vqhmm: all-reduce could not be captured in the step graph ({e}); using split graphs",
                       file=sys.stderr)
             else:
-                self.step_graphs = 1
-                return g.replay
+                if self._verify_dp_graph(g, x, u, lengths, beta, norm):
+                    self.step_graphs = 1
+                    return g.replay
+                print("vqhmm: the one-graph DP step differs from the eager step; using split graphs", file=sys.stderr)
         self.step_graphs = 2
         g_fb, g_adam = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         with torch.cuda.graph(g_fb):
@@ -316,6 +318,33 @@ class TrainState:
             self.reduce_gradients()
             g_adam.replay()
         return replay
+
+
+    def _state_tensors(self):
+        return [self.flat, self.grad, self.exp_avg, self.exp_avg_sq, self.step_dev, self.loss, self.epoch_acc]
+
+    def _verify_dp_graph(self, g, x, u, lengths, beta, norm):
+        """The one-graph DP step (RCCL all-reduce captured) checked once, on first use, against the eager
+        DP step from the same state: parameters, moments, gradient and loss must agree bit for bit on every
+        rank (one MAX all-reduce of the verdict, so all ranks pick the same form).  The state is restored
+        afterwards, so the check costs two steps and changes nothing."""
+        snap = [t.clone() for t in self._state_tensors()]
+        g.replay()
+        torch.cuda.synchronize(self.device)
+        after_graph = [t.clone() for t in self._state_tensors()]
+        for t, v in zip(self._state_tensors(), snap):
+            t.copy_(v)
+        self.forward_backward(x, u, lengths, beta, norm)
+        self.reduce_gradients()
+        self.apply_adam(norm is not None)
+        torch.cuda.synchronize(self.device)
+        same = all(torch.equal(a, b) for a, b in zip(after_graph, self._state_tensors()))
+        for t, v in zip(self._state_tensors(), snap):
+            t.copy_(v)
+        bad = torch.tensor([0 if same else 1], dtype=torch.int32, device=self.device)
+        torch.distributed.all_reduce(bad, op=torch.distributed.ReduceOp.MAX, group=self.pg)
+        torch.cuda.synchronize(self.device)
+        return int(bad.item()) == 0
 
 
 def _dp_graph_default():
