@@ -60,7 +60,7 @@ void oracle_viterbi_f32(const float* log_pi, const float* log_A, const float* em
                         int32_t* path, float* score) {
     float* delta = (float*)malloc(sizeof(float) * (size_t)K);
     float* nd = (float*)malloc(sizeof(float) * (size_t)K);
-    unsigned char* bp = (unsigned char*)malloc((size_t)(T > 0 ? T : 1) * (size_t)K);
+    int32_t* bp = (int32_t*)malloc(sizeof(int32_t) * (size_t)(T > 0 ? T : 1) * (size_t)K);  /* any K */
     for (int64_t b = 0; b < B; ++b) {
         int64_t L = lengths[b] < T ? lengths[b] : T;
         for (int64_t t = 0; t < T; ++t) path[b * T + t] = -1;
@@ -78,7 +78,7 @@ void oracle_viterbi_f32(const float* log_pi, const float* log_A, const float* em
                     if (v > best) { best = v; arg = (int)i; }
                 }
                 nd[j] = best + e[t * K + j];
-                bp[t * K + j] = (unsigned char)arg;
+                bp[t * K + j] = arg;
             }
             memcpy(delta, nd, sizeof(float) * (size_t)K);
         }

@@ -53,7 +53,11 @@ def check_step_vs_oracle(dims, B, T, seed, full_frac=0.5, rtol_norm=2e-6, indepe
              1e-4 of 0 relative to the layer's largest |pre-activation| (a forward bug that
              flips or zeroes activations cannot hide behind the branch-conditioned oracle).
       independent=True: also every gradient against the fp32 CPU oracle's autograd on ITS
-             own branch, 1e-5 normwise (round 1's check, no device information used).
+             own branch (round 1's check, no device information used): 1e-5 normwise where the
+             fp32 oracle's ReLU decisions equal the device's, 5e-5 where a few differ (counted and
+             bounded like the fp64 masks: each flip sits at a pre-activation within fp32 rounding
+             of 0 and moves a gradient by ~1e-5; the cfg4 shard's encoder.conv1 grad measured
+             2.7e-5 with such flips).
     The autograd surface (compute_loss + backward) must give the same bits as TrainState."""
     import vqhmm
     D, H, K, H2, U, TH = dims
@@ -91,6 +95,16 @@ def check_step_vs_oracle(dims, B, T, seed, full_frac=0.5, rtol_norm=2e-6, indepe
         if nd:
             worst = pre[diff].abs().max().item() / max(pre.abs().max().item(), 1e-30)
             assert worst <= 1e-4, f"{name}: a flipped ReLU decision at |pre| = {worst:.2e} of the layer max"
+    rtol_ind = 1e-5
+    if independent:  # the fp32 oracle's own ReLU decisions against the device's
+        nflip = 0
+        for name, mk, pre in zip(("enc conv1", "enc conv2", "dec conv1", "dec conv2"), masks,
+                                 RM.preactivations({k: v.detach() for k, v in p32.items()}, x)):
+            diff = mk != (pre > 0)
+            nd = int(diff.sum())
+            nflip += nd
+            assert nd <= max(4, int(1e-6 * pre.numel())), f"{name}: {nd} ReLU decisions differ from the fp32 oracle's"
+        rtol_ind = 1e-5 if nflip == 0 else 5e-5
     RM.elbo(p64, x.double(), u.double(), L, 1.0, K, U, relu_masks=masks).backward()
     for i, name in enumerate(vqhmm.PARAM_ORDER):
         g = st.grad[st.off[i]:st.off[i + 1]].view_as(auto[name])
@@ -98,12 +112,12 @@ def check_step_vs_oracle(dims, B, T, seed, full_frac=0.5, rtol_norm=2e-6, indepe
         assert_grad_close(g.cpu().numpy(), p64[name].grad.numpy(), name, rtol_norm=rtol_norm, rtol_max=10 * rtol_norm)
         if independent:
             assert_grad_close(g.cpu().numpy(), p32[name].grad.numpy(), name + " (fp32 oracle, own branch)",
-                              rtol_norm=1e-5, rtol_max=1.0)
+                              rtol_norm=rtol_ind, rtol_max=1.0)
 
 
 def test_cfg4_shard_train_step_vs_oracle():
     """One rank's shard of cfg4 (4096 sequences over 8 GPUs = 512 x T=512, K=8, D=16)."""
-    check_step_vs_oracle((16, 64, 8, 32, 4, 128), 512, 512, seed=4096)
+    check_step_vs_oracle((16, 64, 8, 32, 4, 128), 512, 512, seed=4096, independent=True)
 
 
 def test_cfg4_shard_hmm_on_model_tables():
@@ -137,6 +151,12 @@ def test_cfg4_shard_hmm_on_model_tables():
 def test_cfg3_dims_train_step_vs_oracle():
     """cfg3 model dims (K=32, D=64, H=256, H2=128, TH=128) at a small B x T."""
     check_step_vs_oracle((64, 256, 32, 128, 4, 128), 6, 64, seed=2048, rtol_norm=1e-5)
+
+
+def test_cfg3_dims_train_step_b64_t200_vs_oracle():
+    """cfg3 model dims at B = 64, T = 200 (25.6k rows: every wide-conv and wide-wgrad launch runs many
+    row tiles and several row chunks, ragged lengths)."""
+    check_step_vs_oracle((64, 256, 32, 128, 4, 128), 64, 200, seed=2049, rtol_norm=1e-5)
 
 
 def test_cfg3_dims_adam_steps_vs_oracle():

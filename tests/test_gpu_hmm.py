@@ -297,9 +297,27 @@ def test_hmm_generic_left_to_right():
     assert np.all(np.abs(logZ.cpu().numpy() - rz) <= 1e-5 * np.abs(rz))
 
 
-def test_hmm_k_over_256_rejected():
+@pytest.mark.parametrize("K,B,T", [(257, 2, 9), (300, 3, 12), (600, 2, 7), (1100, 2, 4)])
+def test_hmm_generic_k_over_256(K, B, T):
+    """K > 256 (hmm_generic.hip with several states per thread, 16-bit backpointers): Viterbi bit-exact vs the
+    C oracle, gamma / logZ vs the fp64 oracle, ragged lengths (the API takes any (B, T, K))."""
     import vqhmm
-    K, B, T = 257, 1, 4
+    log_pi, log_A, em = random_hmm(K + B + T, B, T, K)
+    L = np.full(B, T, np.int64)
+    L[-1] = T - 2
+    path, score = vqhmm.viterbi(*gpu(log_pi, log_A, em), torch.from_numpy(L))
+    rp, rs = c_oracle.viterbi(log_pi, log_A, em, L)
+    assert np.array_equal(path.cpu().numpy(), rp)
+    assert np.array_equal(score.cpu().numpy().view(np.uint32), rs.view(np.uint32))
+    gamma, logZ = vqhmm.forward_backward(*gpu(log_pi, log_A, em), torch.from_numpy(L))
+    rg, rz = hmm_ref.forward_backward_f64(log_pi, log_A, em, L)
+    check_gamma(gamma.cpu().numpy(), rg)
+    assert np.all(np.abs(logZ.cpu().numpy() - rz) <= 1e-5 * np.maximum(1.0, np.abs(rz)))
+
+
+def test_hmm_k_over_4096_rejected():
+    import vqhmm
+    K, B, T = 4097, 1, 1
     log_pi, log_A, em = random_hmm(1, B, T, K)
     with pytest.raises(RuntimeError, match="unsupported"):
         vqhmm.viterbi(*gpu(log_pi, log_A, em))

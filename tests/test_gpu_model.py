@@ -170,15 +170,17 @@ def test_cfg2_full_size_vs_oracle():
     check_step_vs_oracle((5, 64, 3, 32, 4, 128), 1024, 200, seed=1234, independent=True)
 
 
-@pytest.mark.parametrize("B", [256, 128])
+@pytest.mark.parametrize("B", [512, 256, 128])
 def test_strong_scaling_shards_vs_oracle(B):
-    """The per-GPU shards of cfg2 under strong scaling at N = 4 and 8: B = 256 runs the head's 2-block
+    """The per-GPU shards of cfg2 under strong scaling at N = 4 and 8 (B = 512 at N = 2 too): B = 256 runs the head's 2-block
     windows and B = 128 the 1-block ones plus the fused backward pair (conv2g_kernel), each checked
     against the oracle, at the contract's 1e-5 normwise bound (at B = 256 this draw's
     transition_net.0 gradient sits at 5.3e-6 of the fp64 oracle whatever the window size, NBW 1, 2 or
     4, i.e. fp32 summation, above the full-size test's stricter 2e-6)."""
     from test_gpu_configs import check_step_vs_oracle
-    check_step_vs_oracle((5, 64, 3, 32, 4, 128), B, 200, seed=4321 + B, rtol_norm=1e-5)
+    # independent=True: also every gradient against the fp32 CPU oracle's autograd on its own ReLU branch
+    # (VERDICT r3 item 7: these are exactly the per-GPU workloads of the multi-GPU configs)
+    check_step_vs_oracle((5, 64, 3, 32, 4, 128), B, 200, seed=4321 + B, rtol_norm=1e-5, independent=True)
 
 
 def test_cpu_input_rejected():

@@ -228,7 +228,10 @@ ElboPlan plan_elbo(const vqhmm_dims_t* d, int64_t B, int64_t T, void* ws) {
     WLayer& w = p.wl[i];
     w.N = shapes[i][0]; w.C = shapes[i][1]; w.ks = shapes[i][2];
     const int64_t tiles = cdiv(w.N, 64) * cdiv(w.C, 64);
-    w.rows = (w.N <= 64 && w.C <= 64) ? wgrad2_rows(R, w.N, w.C, w.ks) : wgrad_chunks(R, tiles);
+    WgradArgs probe{};
+    probe.N = w.N; probe.C = w.C; probe.ks = w.ks; probe.rows_per_chunk = 64;
+    w.rows = (w.N <= 64 && w.C <= 64) ? wgrad2_rows(R, w.N, w.C, w.ks)
+             : wgradbig_supported(probe) ? wgradbig_rows(R, w.N, w.C) : wgrad_chunks(R, tiles);
     if (i < 6 && p.wgroup) w.rows = wgrad2_group_rows(std::max<int64_t>(w.rows, wgroup_min_rows()), w.N, w.C, w.ks);
     w.nchunks = cdiv(R, w.rows);
     w.slab = c.take<float>((size_t)w.nchunks * w.N * w.C * w.ks);
@@ -817,7 +820,8 @@ void stage_work(const ElboPlan& p, int st, double* flops, double* bytes, int* mf
     *bytes = 4.0 * R * (2 * p.D + p.D + p.U + 2 * p.K + 2 * p.D + 2 * p.K);
     HeadArgs h{};
     h.K = p.K; h.U = p.U; h.TH = p.TH; h.D = p.D; h.R = p.R;
-    *mfma = (head_mfma_supported(h) || head_coop_supported(h)) ? 1 : 0;
+    // the staged head (K > 8) is its Prior MLP's dense contractions on the wide conv / wgrad kernels (MFMA)
+    *mfma = (head_mfma_supported(h) || head_coop_supported(h) || p.staged) ? 1 : 0;
   } else if (st == S_TOPCL) {
     *bytes = 4.0 * (N * (p.D + p.U) + R * (ld4(p.D) + ld4(p.U)));
   } else if (st == S_LOGIT_BWD) {

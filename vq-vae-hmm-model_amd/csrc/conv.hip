@@ -240,10 +240,30 @@ static int launch_conv_cfg(const ConvArgs& a, hipStream_t s) {
   return VQHMM_OK;
 }
 
+// The wide-channel path (convbig.hip): the conv on convbig_kernel and a fused 1x1 tail (to_logits + softmax,
+// to_params) as a second convbig launch over the activation the first one stored.  Null when it does not apply.
+static bool convbig_split(const ConvArgs& a, ConvArgs& main, ConvArgs& tail) {
+  main = a;
+  main.tW = nullptr; main.tb = nullptr; main.C2 = 0; main.t_out = nullptr; main.q_out = nullptr;
+  if (!convbig_supported(main)) return false;
+  if (!a.tW) return !a.q_out;
+  if (!a.out || !a.t_out || a.t_cf0 || a.q_cf || a.reg_out) return false;
+  tail = ConvArgs{};
+  tail.R = a.R; tail.T = a.T;
+  tail.src = a.out; tail.Kc = a.N; tail.ks = 1; tail.W = a.tW; tail.bias = a.tb; tail.N = a.C2; tail.act = 0;
+  tail.out = a.t_out; tail.q_out = a.q_out;
+  return convbig_supported(tail);
+}
+
 int launch_conv(const ConvArgs& a, hipStream_t s) {
   if (a.R == 0) return VQHMM_OK;
   if (!a.src || !a.W || a.Kc <= 0 || a.N <= 0 || (a.ks != 1 && a.ks != 3)) return VQHMM_EINVAL;
   if (conv2_supported(a)) return launch_conv2(a, s);
+  ConvArgs cm, ct;
+  if (convbig_split(a, cm, ct)) {
+    if (int rc = launch_convbig(cm, s)) return rc;
+    return a.tW ? launch_convbig(ct, s) : VQHMM_OK;
+  }
   const bool wide = a.Kc > 16;
   if (a.N <= 16) return wide ? launch_conv_cfg<4, 1, 4, 1, 32>(a, s) : launch_conv_cfg<4, 1, 4, 1, 16>(a, s);
   if (a.N <= 32) return wide ? launch_conv_cfg<4, 1, 4, 2, 32>(a, s) : launch_conv_cfg<4, 1, 4, 2, 16>(a, s);
@@ -374,6 +394,7 @@ int launch_wgrad(const WgradArgs& a0, hipStream_t s) {
   if (a.R == 0) return VQHMM_OK;
   if (!a.dy || !a.x || !a.slab || (a.ks != 1 && a.ks != 3) || a.rows_per_chunk % 64) return VQHMM_EINVAL;
   if (wgrad2_supported(a)) return launch_wgrad2(a, s);
+  if (wgradbig_supported(a)) return launch_wgradbig(a, s);
   const int64_t nchunks = cdiv(a.R, a.rows_per_chunk);
   constexpr int TN = 64, TC = 64;
   const dim3 grid((unsigned)(cdiv(a.N, TN) * cdiv(a.C, TC)), (unsigned)nchunks);

@@ -1,0 +1,369 @@
+// Wide convolutions (k = 1 or 3, more than 64 channels on a side; Kc a multiple of 16) as an implicit GEMM on
+// the f32 MFMA: the cfg3-dims layers (H = 256, H2 = 128, K = 32, D = 64) of VQ_VAE_HMM_fixed.py:34-36,77-79 and
+// their data gradients, the 1x1 tails to_logits / to_params (:36, :79) as their own launches, and the staged
+// head's Prior MLP layers (:53-57) at K^2 = 1024 transition logits.
+//
+// GEMM view over PCL rows (common.h): Y[r][n] = sum_{tap, c} X[r + tap - 1][c] Weff[n][c][tap], Weff = W (forward)
+// or W[c][n][2 - tap] (data gradient).  A workgroup owns a BM = 128 row x BN column tile; its 4 waves split it
+// 2 x 2 (64 rows x BN / 2 columns each: 4 x BN / 32 accumulators of v_mfma_f32_16x16x4_f32).  The reduction
+// walks 16-channel slices: the slice's 130 input rows and its 3 x BN weight rows are staged in LDS (rows of 24
+// floats: the float4 operand reads of all four 16-lane groups are bank-conflict free), while the next slice's
+// operands are already in flight in registers.  Inside a slice lane group g holds channels 4g .. 4g + 3 of its
+// row as one float4 and MFMA e uses element e, for A and B alike, so every channel is summed exactly once
+// (the k order inside a slice is a fixed permutation; the result is a k-ordered fmaf chain as any f32 MFMA).
+//
+// Epilogue: scale, bias, ReLU or the ReLU-backward mask (act 2: aux > 0), pad rows zero, PCL store; SOFTMAX
+// (N <= BN / 2 <= 64, the tail to_logits): q = softmax over the row's N channels to q_out, through LDS.
+#include <algorithm>
+
+#include "kernels.h"
+
+namespace vqhmm {
+
+namespace {
+constexpr int CB_BM = 128;  // rows per tile
+constexpr int CB_KC = 16;   // channels per slice
+constexpr int CB_LD = 24;   // LDS row stride (floats) of the staged X rows and weight rows
+}  // namespace
+
+template <int BN>
+struct ConvBigCfg {
+  static constexpr int WN = BN / 32;                   // 16-col accumulator blocks per wave (2 waves across)
+  static constexpr int X4 = (CB_BM + 2) * 4;           // float4s of one slice's X rows
+  static constexpr int W4 = 3 * BN * 4;                // float4s of one slice's weight rows (3 taps)
+  static constexpr int PX = (X4 + 255) / 256, PW = (W4 + 255) / 256;
+  static constexpr int LDS_FLOATS = (CB_BM + 2) * CB_LD + 3 * BN * CB_LD;
+};
+
+// One float4 of the slice's weights: source address (or null: zeros) and the 4 LDS destinations (tap, n, c) it
+// scatters to.  Forward: per n the slice's (c, tap) pairs are 48 (k = 3) / 16 (k = 1) contiguous floats of W[n];
+// data gradient: per c the tile's (n, tap) pairs are 3 BN / BN contiguous floats of W[c].
+template <int BN>
+__device__ __forceinline__ const float* cb_wsrc(const ConvArgs& a, int n0, int c0, int q, int (&dst)[4]) {
+  const int ks = a.ks;
+  if (!a.w_dgrad) {
+    const int per_n = 4 * ks;  // float4s per n row of the slice
+    const int n = q / per_n, f = q - n * per_n;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int idx = 4 * f + e, c = ks == 3 ? idx / 3 : idx, tap = ks == 3 ? idx - 3 * (idx / 3) : 0;
+      dst[e] = (tap * BN + n) * CB_LD + c;
+    }
+    if (n >= BN || n0 + n >= a.N) return nullptr;
+    return a.W + ((int64_t)(n0 + n) * a.Kc + c0) * ks + 4 * f;
+  }
+  const int per_c = ks * BN / 4;
+  const int c = q / per_c, f = q - c * per_c;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int idx = 4 * f + e, n = ks == 3 ? idx / 3 : idx, t = ks == 3 ? idx - 3 * (idx / 3) : 0;
+    dst[e] = ((ks - 1 - t) * BN + n) * CB_LD + c;
+  }
+  if (c >= CB_KC || n0 + (ks == 3 ? (4 * f) / 3 : 4 * f) >= a.N) return nullptr;  // N % 4 == 0: whole float4s
+  return a.W + ((int64_t)(c0 + c) * a.N + n0) * ks + 4 * f;
+}
+
+template <int BN, bool SOFTMAX>
+__global__ __launch_bounds__(256) void convbig_kernel(ConvArgs a) {
+  using C = ConvBigCfg<BN>;
+  constexpr int WN = C::WN;
+  extern __shared__ float4 smem4[];
+  float* Xs = reinterpret_cast<float*>(smem4);  // [(BM + 2)][LD]
+  float* Ws = Xs + (CB_BM + 2) * CB_LD;         // [3][BN][LD]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lg = lane >> 4, l16 = lane & 15;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int64_t m0 = (int64_t)blockIdx.x * CB_BM;
+  const int n0 = blockIdx.y * BN;
+  const int ldx = a.Kc, ks = a.ks, nslice = a.Kc / CB_KC;
+  const int wrows = ks * BN * 4;  // valid weight float4s per slice
+
+  float4 px[C::PX], pw[C::PW];
+  auto load = [&](int c0) {
+#pragma unroll
+    for (int k = 0; k < C::PX; ++k) {
+      const int i = tid + 256 * k, row = i >> 2, c4 = (i & 3) * 4;
+      const int64_t r = m0 - 1 + row;
+      const bool ok = i < C::X4 && r >= 0 && r < a.R;
+      px[k] = ok ? *reinterpret_cast<const float4*>(a.src + r * ldx + c0 + c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < C::PW; ++k) {
+      const int q = tid + 256 * k;
+      int dst[4];
+      const float* src = q < wrows ? cb_wsrc<BN>(a, n0, c0, q, dst) : nullptr;
+      pw[k] = src ? *reinterpret_cast<const float4*>(src) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto store = [&](int c0) {
+#pragma unroll
+    for (int k = 0; k < C::PX; ++k) {
+      const int i = tid + 256 * k;
+      if (i < C::X4) *reinterpret_cast<float4*>(Xs + (i >> 2) * CB_LD + (i & 3) * 4) = px[k];
+    }
+#pragma unroll
+    for (int k = 0; k < C::PW; ++k) {
+      int q = tid + 256 * k;
+      if (q < wrows) {
+        // q made opaque: the 4 LDS destinations are recomputed here, not hoisted out of the slice loop (kept live
+        // they cost 4 VGPRs per prefetched float4, a second wave per SIMD)
+        asm volatile("" : "+v"(q));
+        int dst[4];
+        (void)cb_wsrc<BN>(a, n0, c0, q, dst);
+        Ws[dst[0]] = pw[k].x;
+        Ws[dst[1]] = pw[k].y;
+        Ws[dst[2]] = pw[k].z;
+        Ws[dst[3]] = pw[k].w;
+      }
+    }
+  };
+
+  f32x4 acc[4][WN];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  load(0);
+  for (int s = 0; s < nslice; ++s) {
+    __syncthreads();  // every wave is done reading the previous slice
+    store(s * CB_KC);
+    __syncthreads();
+    if (s + 1 < nslice) load((s + 1) * CB_KC);  // in flight across this slice's MFMAs
+    for (int tap = 0; tap < ks; ++tap) {
+      const int roff = ks == 3 ? tap : 1;
+      float4 av[4], bv[WN];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        av[i] = *reinterpret_cast<const float4*>(Xs + (wm * 64 + i * 16 + l16 + roff) * CB_LD + 4 * lg);
+#pragma unroll
+      for (int j = 0; j < WN; ++j)
+        bv[j] = *reinterpret_cast<const float4*>(Ws + (tap * BN + wn * (BN / 2) + j * 16 + l16) * CB_LD + 4 * lg);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < WN; ++j) {
+            const float ae = e == 0 ? av[i].x : e == 1 ? av[i].y : e == 2 ? av[i].z : av[i].w;
+            const float be = e == 0 ? bv[j].x : e == 1 ? bv[j].y : e == 2 ? bv[j].z : bv[j].w;
+            acc[i][j] = mfma16x16x4(ae, be, acc[i][j]);
+          }
+    }
+  }
+
+  // ---- epilogue: lane (lg, l16), register v -> row wm*64 + i*16 + 4 lg + v, column wn*BN/2 + j*16 + l16
+  const float sc = a.scale ? *a.scale : 1.f;
+  const int ldn = a.N;  // N % 4 == 0: no pad channels
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int row = wm * 64 + i * 16 + 4 * lg + v;
+      const int64_t r = m0 + row;
+      int64_t b;
+      int t;
+      const bool valid = row_bt(r, a.R, a.T, b, t);
+#pragma unroll
+      for (int j = 0; j < WN; ++j) {
+        const int n = n0 + wn * (BN / 2) + j * 16 + l16;
+        float y = acc[i][j][v] * sc;
+        if (a.bias && n < a.N) y += a.bias[n];
+        if (a.act == 1) y = relu_f(y);
+        else if (a.act == 2 && r < a.R && n < a.N) y = a.aux[r * ldn + n] > 0.f ? y : 0.f;
+        y = valid ? y : 0.f;
+        acc[i][j][v] = y;
+        if (a.out && r < a.R && n < a.N) a.out[r * ldn + n] = y;
+      }
+    }
+  }
+  if constexpr (SOFTMAX) {  // q = softmax over the row's N <= BN / 2 channels (all in the wn = 0 waves)
+    __syncthreads();
+    float* Ys = Xs;  // [BM][BN / 2 + 1]
+    constexpr int LY = BN / 2 + 1;
+    if (wn == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+#pragma unroll
+          for (int j = 0; j < WN; ++j) Ys[(wm * 64 + i * 16 + 4 * lg + v) * LY + j * 16 + l16] = acc[i][j][v];
+    }
+    __syncthreads();
+    if (tid < CB_BM) {
+      const int64_t r = m0 + tid;
+      int64_t b;
+      int t;
+      const bool valid = row_bt(r, a.R, a.T, b, t);
+      const float* y = Ys + tid * LY;
+      float mx = -__builtin_inff();
+      for (int n = 0; n < a.N; ++n) mx = fmaxf(mx, y[n]);
+      float se = 0.f;
+      for (int n = 0; n < a.N; ++n) se += __expf(y[n] - mx);
+      if (r < a.R)
+        for (int n = 0; n < a.N; ++n) a.q_out[r * ldn + n] = valid ? __expf(y[n] - mx) / se : 0.f;
+    }
+  }
+}
+
+// shapes the wide kernel takes: PCL in and out, Kc a multiple of 16 (whole slices), N a multiple of 4 (no pad
+// channels, whole weight float4s), no CF outputs / fused tails / softmax wider than half a tile
+bool convbig_supported(const ConvArgs& a) {
+  return !a.src_cf && a.Kc % CB_KC == 0 && a.Kc > 0 && a.N % 4 == 0 && a.N > 0 && (a.ks == 1 || a.ks == 3) &&
+         !a.out_cf && !a.tW && !a.t_cf0 && !a.q_cf && !a.reg_out && a.act <= 2 && (a.act != 2 || a.aux) &&
+         (!a.q_out || a.N <= 64) && (a.out || a.q_out) && a.R < (1ll << 40);
+}
+
+template <int BN, bool SM>
+static int launch_cb(const ConvArgs& a, hipStream_t s) {
+  const size_t lds = (size_t)ConvBigCfg<BN>::LDS_FLOATS * sizeof(float);
+  const dim3 grid((unsigned)cdiv(a.R, CB_BM), (unsigned)cdiv(a.N, BN));
+  convbig_kernel<BN, SM><<<grid, 256, lds, s>>>(a);
+  VQHMM_LAUNCH_CHECK();
+  return VQHMM_OK;
+}
+
+int launch_convbig(const ConvArgs& a, hipStream_t s) {
+  if (!convbig_supported(a)) return VQHMM_EUNSUPPORTED;
+  if (a.R == 0) return VQHMM_OK;
+  if (a.q_out) return launch_cb<128, true>(a, s);
+  return a.N <= 64 ? launch_cb<64, false>(a, s) : launch_cb<128, false>(a, s);
+}
+
+
+// ------------------------------------------------------------------ wide weight gradients
+// dW[n][c][tap] = sum_r dY[r][n] X[r + tap - 1][c] over a chunk of PCL rows (split-K; the per-chunk partials go
+// to a slab the backward tail sums in a fixed order), and the bias gradient sum_r dY[r][n] (c-tile 0).  A
+// workgroup owns TN = 128 outputs n x TC = 64 inputs c x every tap; its 4 waves split that 2 x 2 (64 n x 32 c x
+// ks taps: 4 x 2 x ks accumulators).  64-row stages of dY and X (one halo row each side) in LDS, the next stage
+// in flight in registers; operands are b32 reads with row strides = 16 (mod 64) floats (the four 16-lane groups
+// read rows 4 apart in disjoint banks).
+namespace {
+constexpr int WB_TN = 128, WB_TC = 64, WB_RT = 64;
+constexpr int WB_LDA = WB_TN + 16, WB_LDB = WB_TC + 16;
+constexpr int WB_DY4 = WB_RT * WB_TN / 4, WB_X4 = (WB_RT + 2) * WB_TC / 4;
+constexpr int WB_PD = WB_DY4 / 256, WB_PX = (WB_X4 + 255) / 256;
+}  // namespace
+
+template <int KS>
+__global__ __launch_bounds__(256) void wgradbig_kernel(WgradArgs a) {
+  __shared__ float dys[WB_RT * WB_LDA];
+  __shared__ float xs[(WB_RT + 2) * WB_LDB];
+  __shared__ float bred[256];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lg = lane >> 4, l16 = lane & 15;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int ntc = (int)cdiv(a.C, WB_TC);
+  const int n0 = (blockIdx.x / ntc) * WB_TN, c0 = (blockIdx.x % ntc) * WB_TC;
+  const int64_t chunk = blockIdx.y;
+  const int64_t rbeg = chunk * a.rows_per_chunk, rend = min(a.R, rbeg + a.rows_per_chunk);
+  const int ldn = ld4(a.N), ldc = ld4(a.C);
+  const bool do_bias = a.bias_slab && c0 == 0;
+
+  float4 pd[WB_PD], px[WB_PX];
+  auto load = [&](int64_t r0) {
+#pragma unroll
+    for (int k = 0; k < WB_PD; ++k) {
+      const int i = tid + 256 * k, row = i / (WB_TN / 4), n = n0 + (i - row * (WB_TN / 4)) * 4;
+      const int64_t r = r0 + row;
+      pd[k] = (r < rend && n < ldn) ? *reinterpret_cast<const float4*>(a.dy + r * ldn + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < WB_PX; ++k) {
+      const int i = tid + 256 * k, row = i / (WB_TC / 4), c = c0 + (i - row * (WB_TC / 4)) * 4;
+      const int64_t r = r0 - 1 + row;
+      px[k] = (i < WB_X4 && r >= 0 && r < a.R && c < ldc) ? *reinterpret_cast<const float4*>(a.x + r * ldc + c)
+                                                           : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  f32x4 acc[KS][4][2];
+#pragma unroll
+  for (int tp = 0; tp < KS; ++tp)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[tp][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bacc = 0.f;
+
+  load(rbeg);
+  for (int64_t r0 = rbeg; r0 < rend; r0 += WB_RT) {
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < WB_PD; ++k) {
+      const int i = tid + 256 * k, row = i / (WB_TN / 4), n = (i - row * (WB_TN / 4)) * 4;
+      *reinterpret_cast<float4*>(dys + row * WB_LDA + n) = pd[k];
+    }
+#pragma unroll
+    for (int k = 0; k < WB_PX; ++k) {
+      const int i = tid + 256 * k, row = i / (WB_TC / 4), c = (i - row * (WB_TC / 4)) * 4;
+      if (i < WB_X4) *reinterpret_cast<float4*>(xs + row * WB_LDB + c) = px[k];
+    }
+    __syncthreads();
+    if (r0 + WB_RT < rend) load(r0 + WB_RT);
+    if (do_bias && tid < WB_TN) {
+      float bp[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) bp[k] = 0.f;
+#pragma unroll
+      for (int row = 0; row < WB_RT; ++row) bp[row & 7] += dys[row * WB_LDA + tid];
+      bacc += ((bp[0] + bp[1]) + (bp[2] + bp[3])) + ((bp[4] + bp[5]) + (bp[6] + bp[7]));
+    }
+#pragma unroll 4
+    for (int st = 0; st < WB_RT / 4; ++st) {
+      const int rr = 4 * st + lg;  // this lane group's row of the k-step
+      float av[4], bv[KS][2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) av[i] = dys[rr * WB_LDA + wm * 64 + i * 16 + l16];
+#pragma unroll
+      for (int tp = 0; tp < KS; ++tp)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bv[tp][j] = xs[(rr + (KS == 3 ? tp : 1)) * WB_LDB + wn * 32 + j * 16 + l16];
+#pragma unroll
+      for (int tp = 0; tp < KS; ++tp)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[tp][i][j] = mfma16x16x4(av[i], bv[tp][j], acc[tp][i][j]);
+    }
+  }
+  // ---- this chunk's partial: slab[chunk][n][c][tap]; lane (lg, l16), reg v -> n row 4 lg + v, c column l16
+  float* out = a.slab + chunk * (int64_t)a.N * a.C * KS;
+#pragma unroll
+  for (int tp = 0; tp < KS; ++tp)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int n = n0 + wm * 64 + i * 16 + 4 * lg + v, c = c0 + wn * 32 + j * 16 + l16;
+          if (n < a.N && c < a.C) out[((int64_t)n * a.C + c) * KS + tp] = acc[tp][i][j][v];
+        }
+  if (do_bias && tid < WB_TN && n0 + tid < a.N) a.bias_slab[chunk * a.N + n0 + tid] = bacc;
+  (void)bred;
+}
+
+// the wide weight gradients: PCL operands, N and C multiples of 4
+bool wgradbig_supported(const WgradArgs& a) {
+  return !a.x_cf && a.N % 4 == 0 && a.C % 4 == 0 && a.N > 0 && a.C > 0 && (a.ks == 1 || a.ks == 3) &&
+         !a.cmpW && a.rows_per_chunk % WB_RT == 0;
+}
+
+// rows per chunk: about 768 workgroups over the output tiles, whole 64-row stages
+int64_t wgradbig_rows(int64_t R, int N, int C) {
+  const int64_t tiles = cdiv(N, WB_TN) * cdiv(C, WB_TC);
+  const int64_t want = std::max<int64_t>(1, 768 / tiles);
+  return std::max<int64_t>(WB_RT, cdiv(cdiv(R, want), WB_RT) * WB_RT);
+}
+
+int launch_wgradbig(const WgradArgs& a, hipStream_t s) {
+  if (!wgradbig_supported(a)) return VQHMM_EUNSUPPORTED;
+  if (a.R == 0) return VQHMM_OK;
+  const dim3 grid((unsigned)(cdiv(a.N, WB_TN) * cdiv(a.C, WB_TC)), (unsigned)cdiv(a.R, a.rows_per_chunk));
+  if (a.ks == 3) wgradbig_kernel<3><<<grid, 256, 0, s>>>(a);
+  else wgradbig_kernel<1><<<grid, 256, 0, s>>>(a);
+  VQHMM_LAUNCH_CHECK();
+  return VQHMM_OK;
+}
+
+}  // namespace vqhmm

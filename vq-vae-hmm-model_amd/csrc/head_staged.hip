@@ -97,10 +97,131 @@ __global__ __launch_bounds__(256) void head_l1_kernel(StagedHeadArgs a) {
   }
 }
 
+// One wave per row, lane = channel (D <= 64 recon channels, K <= 64 states): every load and store is a whole
+// contiguous row (the thread-per-row form read each row's channels 16 B apart per lane: 3.2 ms at cfg3); the
+// row's log-sum-exp and <q, log q> are wave reductions (DPP + permlane, a fixed order).
+// head_l1 for 8 < K <= 32, one wave per row with every load and store a whole contiguous row: lane (i, h) =
+// (l >> 1, l & 1) holds log_A_t[i][16 h .. 16 h + 15] (the old lane-per-i form walked each i row with a
+// K-float stride per lane: 2.6 ms at cfg3).  Row reductions pair lanes (xor 1); the column sums dqc_j =
+// sum_i q_{t-1,i} log_A[i][j] run over the 32 lanes of a half (xor 2 .. 32, a fixed tree).  V4: K % 4 == 0
+// (float4 rows).
+template <bool V4>
+__global__ __launch_bounds__(256) void head_l1_wide_kernel(StagedHeadArgs a) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int K = a.K, KK = K * K, LDA = ld4(KK), LQ = ld4(K);
+  const int i = lane >> 1, h = lane & 1, j0 = 16 * h;
+  const bool irow = i < K;
+  const float cpri = -a.beta / loss_norm_batch(a.norm, a.B);
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + wave; r < a.R; r += nw) {
+    int64_t b;
+    int t;
+    const bool valid = row_bt(r, a.R, a.T, b, t);
+    float* row = a.lgA + r * LDA;
+    if (!valid) {  // pad rows: zero gradient rows (the wgrad / dgrad sums run over all rows)
+      for (int e = lane; e < LDA; e += 64) row[e] = 0.f;
+      if (lane < LQ) { a.nx[r * LQ + lane] = 0.f; a.dqc[r * LQ + lane] = 0.f; }
+      if (lane == 0) a.trw[r] = 0.f;
+      continue;
+    }
+    const int64_t L = a.lengths[b];
+    const float w = (t >= 1 && t < L) ? 1.f : 0.f;
+    float la[16], qc[16];
+    if constexpr (V4) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const bool in = irow && j0 + 4 * g < K;
+        const float4 v = in ? *reinterpret_cast<const float4*>(row + i * K + j0 + 4 * g) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 c = j0 + 4 * g < K ? *reinterpret_cast<const float4*>(a.q + r * LQ + j0 + 4 * g)
+                                        : make_float4(0.f, 0.f, 0.f, 0.f);
+        la[4 * g] = v.x; la[4 * g + 1] = v.y; la[4 * g + 2] = v.z; la[4 * g + 3] = v.w;
+        qc[4 * g] = c.x; qc[4 * g + 1] = c.y; qc[4 * g + 2] = c.z; qc[4 * g + 3] = c.w;
+      }
+    } else {
+#pragma unroll
+      for (int jj = 0; jj < 16; ++jj) {
+        const int j = j0 + jj;
+        la[jj] = (irow && j < K) ? row[i * K + j] : 0.f;
+        qc[jj] = j < K ? a.q[r * LQ + j] : 0.f;
+      }
+    }
+    // log_softmax of row i (lanes 2i, 2i + 1)
+    float m = -__builtin_inff();
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj)
+      if (j0 + jj < K) m = fmaxf(m, la[jj]);
+    m = fmaxf(m, __shfl_xor(m, 1));
+    float se = 0.f;
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj)
+      if (j0 + jj < K) se += __expf(la[jj] - m);
+    se += __shfl_xor(se, 1);
+    const float ls = m + __logf(se);
+    const float qp = irow ? a.q[(r - 1) * LQ + i] : 0.f;  // row r - 1 is a zero pad row at t = 0
+    float nxi = 0.f, sq = 0.f;
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) {
+      la[jj] -= ls;
+      if (j0 + jj < K) {
+        nxi = fmaf(la[jj], qc[jj], nxi);
+        sq += qc[jj];
+      }
+    }
+    nxi += __shfl_xor(nxi, 1);
+    sq += __shfl_xor(sq, 1);
+    // transition term sum_i q_{t-1,i} nx_i (each i counted once: h = 0 lanes)
+    float tri = (irow && h == 0) ? qp * nxi : 0.f;
+#pragma unroll
+    for (int o = 2; o < 64; o <<= 1) tri += __shfl_xor(tri, o);
+    if (h == 0 && i < LQ) a.nx[r * LQ + i] = irow ? nxi : 0.f;
+    if (lane == 0) a.trw[r] = w * tri;  // lane 0 (h = 0) holds the sum over every i
+    // dqc_j = w sum_i q_{t-1,i} log_A[i][j]: over the 32 lanes of this half
+    float d[16];
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) d[jj] = irow ? qp * la[jj] : 0.f;
+#pragma unroll
+    for (int o = 2; o < 64; o <<= 1)
+#pragma unroll
+      for (int jj = 0; jj < 16; ++jj) d[jj] += __shfl_xor(d[jj], o);
+    if (i == 0) {
+#pragma unroll
+      for (int jj = 0; jj < 16; ++jj)
+        if (j0 + jj < LQ) a.dqc[r * LQ + j0 + jj] = j0 + jj < K ? w * d[jj] : 0.f;
+    }
+    // log_softmax backward of d tr / d log_A = cpri w q_{t-1,i} q_{t,j}, in place over the row
+    const float ci = cpri * w * qp, rs = ci * sq;
+    float g[16];
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) g[jj] = ci * qc[jj] - __expf(la[jj]) * rs;
+    if constexpr (V4) {
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4)
+        if (irow && j0 + 4 * q4 < K)
+          *reinterpret_cast<float4*>(row + i * K + j0 + 4 * q4) = make_float4(g[4 * q4], g[4 * q4 + 1], g[4 * q4 + 2], g[4 * q4 + 3]);
+    } else {
+#pragma unroll
+      for (int jj = 0; jj < 16; ++jj)
+        if (irow && j0 + jj < K) row[i * K + j0 + jj] = g[jj];
+    }
+    for (int e = KK + lane; e < LDA; e += 64) row[e] = 0.f;
+  }
+}
+
+__device__ __forceinline__ float wave_max_dpp(float v) {
+  v = fmaxf(v, __builtin_bit_cast(float, dpp_u32<0xB1>(__builtin_bit_cast(uint32_t, v))));
+  v = fmaxf(v, __builtin_bit_cast(float, dpp_u32<0x4E>(__builtin_bit_cast(uint32_t, v))));
+  v = fmaxf(v, __builtin_bit_cast(float, dpp_u32<0x141>(__builtin_bit_cast(uint32_t, v))));
+  v = fmaxf(v, __builtin_bit_cast(float, dpp_u32<0x128>(__builtin_bit_cast(uint32_t, v))));
+  float2 r = pair16(v);
+  v = fmaxf(r.x, r.y);
+  r = pair32(v);
+  return fmaxf(r.x, r.y);
+}
+
 __global__ __launch_bounds__(256) void head_l2_kernel(StagedHeadArgs a) {
   __shared__ double red[4][256];
   __shared__ unsigned long long cnt;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int K = a.K, D = a.D, LQ = ld4(K), LP = ld4(2 * D), LX = ld4(D);
   if (tid == 0) cnt = a.norm ? (unsigned long long)a.norm[0] : 0ull;
   __syncthreads();
@@ -116,54 +237,57 @@ __global__ __launch_bounds__(256) void head_l2_kernel(StagedHeadArgs a) {
   __syncthreads();
   const float inv_n = 1.0f / fmaxf((float)(cnt * (unsigned long long)D), 1.0f);
   const float cpri = -a.beta / loss_norm_batch(a.norm, a.B), cent = a.beta / loss_norm_batch(a.norm, a.B);
+  const float lpk = lane < K ? a.log_pi[lane] : 0.f;
   float s_rec = 0.f, s_init = 0.f, s_tr = 0.f, s_ent = 0.f;
-  for (int64_t r = (int64_t)blockIdx.x * 256 + tid; r < a.R; r += (int64_t)gridDim.x * 256) {
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + wave; r < a.R; r += nw) {
     int64_t b;
     int t;
     const bool valid = row_bt(r, a.R, a.T, b, t);
     const int64_t L = valid ? a.lengths[b] : 0;
     const bool m = valid && t < L;
-    if (a.need_grad) {
-      for (int c = 0; c < LP; ++c) a.dpar[r * LP + c] = 0.f;
-    }
-    for (int c = 0; c < D; ++c) {
-      if (!m) break;
-      const float mu = a.par[r * LP + c], lv = a.par[r * LP + D + c], xv = a.x[r * LX + c];
-      const float ev = __expf(lv);
-      const float var = (ev < 1e-8f ? 1e-8f : ev)  /* clamp(min=1e-8), NaN stays NaN */;
-      const float df = mu - xv;
-      const float r2 = df * df / var;
-      s_rec += 0.5f * (__logf(6.2831855f * var) + r2);
+    // recon NLL, lane c = channel (c, c + 64, ...)
+    for (int c = lane; c < D; c += 64) {
+      float dmu = 0.f, dlv = 0.f;
+      if (m) {
+        const float mu = a.par[r * LP + c], lv = a.par[r * LP + D + c], xv = a.x[r * LX + c];
+        const float ev = __expf(lv);
+        const float var = (ev < 1e-8f ? 1e-8f : ev)  /* clamp(min=1e-8), NaN stays NaN */;
+        const float df = mu - xv;
+        const float r2 = df * df / var;
+        s_rec += 0.5f * (__logf(6.2831855f * var) + r2);
+        dmu = df / var * inv_n;
+        dlv = (ev >= 1e-8f) ? 0.5f * (1.f - r2) * inv_n : 0.f;
+      }
       if (a.need_grad) {
-        a.dpar[r * LP + c] = df / var * inv_n;
-        a.dpar[r * LP + D + c] = (ev >= 1e-8f) ? 0.5f * (1.f - r2) * inv_n : 0.f;
+        a.dpar[r * LP + c] = dmu;
+        a.dpar[r * LP + D + c] = dlv;
       }
     }
-    // entropy of q = softmax(logits) and its logits gradient
-    float mx = -__builtin_inff();
-    for (int k = 0; k < K; ++k) mx = fmaxf(mx, a.logits[r * LQ + k]);
-    float se = 0.f;
-    for (int k = 0; k < K; ++k) se += __expf(a.logits[r * LQ + k] - mx);
-    const float lse = mx + __logf(se);
-    float f = 0.f;
-    for (int k = 0; k < K; ++k) f = fmaf(a.q[r * LQ + k], a.logits[r * LQ + k] - lse, f);
-    if (m) s_ent -= f;
-    if (valid) s_tr += a.trw[r];
+    if (a.need_grad)
+      for (int c = 2 * D + lane; c < LP; c += 64) a.dpar[r * LP + c] = 0.f;  // pad channels
+    // entropy of q = softmax(logits) and its logits gradient, lane k = state
+    const float lg = lane < K ? a.logits[r * LQ + lane] : -__builtin_inff();
+    const float qk = lane < K ? a.q[r * LQ + lane] : 0.f;
+    const float mx = wave_max_dpp(lg);
+    const float lse = mx + __logf(wave_sum_dpp(lane < K ? __expf(lg - mx) : 0.f));
+    const float f = wave_sum_dpp(lane < K ? qk * (lg - lse) : 0.f);
+    if (m && lane == 0) s_ent -= f;
+    if (valid && lane == 0) s_tr += a.trw[r];
     const float wn = (valid && t + 1 < L) ? 1.f : 0.f;  // weight of the t -> t+1 transition
-    for (int k = 0; k < LQ; ++k) {
+    if (lane < LQ) {
       float dl = 0.f, dq = 0.f;
-      if (valid && k < K) {
-        const float qk = a.q[r * LQ + k];
-        if (m) dl = cent * qk * ((a.logits[r * LQ + k] - lse) - f);
-        dq = cpri * (a.dqc[r * LQ + k] + wn * a.nx[(r + 1) * LQ + k]);  // dqc already carries w_t
+      if (valid && lane < K) {
+        if (m) dl = cent * qk * ((lg - lse) - f);
+        dq = cpri * (a.dqc[r * LQ + lane] + wn * a.nx[(r + 1) * LQ + lane]);  // dqc already carries w_t
         if (t == 0) {
-          dq = fmaf(cpri, a.log_pi[k], dq);
-          s_init = fmaf(qk, a.log_pi[k], s_init);
+          dq = fmaf(cpri, lpk, dq);
+          s_init = fmaf(qk, lpk, s_init);
         }
       }
       if (a.need_grad) {
-        a.dlx[r * LQ + k] = dl;
-        a.dqx[r * LQ + k] = dq;
+        a.dlx[r * LQ + lane] = dl;
+        a.dqx[r * LQ + lane] = dq;
       }
     }
   }
@@ -180,13 +304,24 @@ __global__ __launch_bounds__(256) void head_l2_kernel(StagedHeadArgs a) {
   if (tid < 4) a.part[blockIdx.x * 4 + tid] = red[tid][0];
 }
 
-// q summed over the t = 0 rows (init term gradient of log_prior), one chunk
-__global__ void head_q0_kernel(const float* q, int64_t B, int T, int K, float* q0) {
-  const int k = threadIdx.x;
-  if (k >= K) return;
+// q summed over the t = 0 rows (init term gradient of log_prior), one chunk: thread (part, k) sums sequences
+// b = part, part + P, ... (P = 256 / ld4(K) parts, loads independent), the parts combined in a fixed order
+// (was one thread per k over all B: 2048 dependent loads, 0.64 ms at cfg3)
+__global__ __launch_bounds__(256) void head_q0_kernel(const float* q, int64_t B, int T, int K, float* q0) {
+  __shared__ float part[256];
+  const int L = ld4(K), P = 256 / L, k = threadIdx.x % L, ph = threadIdx.x / L;
   float s = 0.f;
-  for (int64_t b = 0; b < B; ++b) s += q[(b * (T + 2) + 1) * ld4(K) + k];
-  q0[k] = s;
+  if (ph < P) {
+#pragma unroll 8
+    for (int64_t b = ph; b < B; b += P) s += q[(b * (T + 2) + 1) * L + k];
+  }
+  part[threadIdx.x] = s;
+  __syncthreads();
+  if ((int)threadIdx.x < K) {
+    float v = 0.f;
+    for (int h = 0; h < P; ++h) v += part[h * L + threadIdx.x];
+    q0[threadIdx.x] = v;
+  }
 }
 
 __global__ void log_softmax_small_kernel(const float* v, int K, float* out) {
@@ -199,21 +334,22 @@ __global__ void log_softmax_small_kernel(const float* v, int K, float* out) {
   for (int k = 0; k < K; ++k) out[k] = v[k] - l;
 }
 
-bool staged_head_supported(int K) { return K >= 1 && K <= 64; }
+bool staged_head_supported(int K) { return K >= 1 && K <= 64; }  // lane = state (head_l1 / head_l2)
 
 int launch_staged_head(const StagedHeadArgs& a, int l2grid, hipStream_t s) {
   if (!staged_head_supported(a.K)) return VQHMM_EUNSUPPORTED;
   log_softmax_small_kernel<<<1, 64, 0, s>>>(a.log_prior, a.K, a.log_pi);
   VQHMM_LAUNCH_CHECK();
   const unsigned g1 = (unsigned)std::min<int64_t>(cdiv(a.R, 4), 2048);
-  if (a.K <= 16) head_l1_kernel<16><<<g1, 256, 0, s>>>(a);
-  else if (a.K <= 32) head_l1_kernel<32><<<g1, 256, 0, s>>>(a);
+  if (a.K <= 8) head_l1_kernel<16><<<g1, 256, 0, s>>>(a);
+  else if (a.K <= 32 && a.K % 4 == 0) head_l1_wide_kernel<true><<<g1, 256, 0, s>>>(a);
+  else if (a.K <= 32) head_l1_wide_kernel<false><<<g1, 256, 0, s>>>(a);
   else head_l1_kernel<64><<<g1, 256, 0, s>>>(a);
   VQHMM_LAUNCH_CHECK();
   head_l2_kernel<<<l2grid, 256, 0, s>>>(a);
   VQHMM_LAUNCH_CHECK();
   if (a.need_grad) {
-    head_q0_kernel<<<1, 64, 0, s>>>(a.q, a.B, a.T, a.K, a.q0);
+    head_q0_kernel<<<1, 256, 0, s>>>(a.q, a.B, a.T, a.K, a.q0);
     VQHMM_LAUNCH_CHECK();
   }
   return VQHMM_OK;

@@ -202,7 +202,7 @@ __global__ __launch_bounds__(64) void viterbi_kernel(const float* __restrict__ l
 
 size_t viterbi_ws_bytes(int64_t B, int64_t T, int64_t K) {
   if (K > 8 && K <= 32) return viterbi_wide_ws_bytes(B, T);
-  if (K > 32 && K <= 256) return hmm_generic_viterbi_ws_bytes(B, T, K);
+  if (K > 32) return hmm_generic_supported(K) ? hmm_generic_viterbi_ws_bytes(B, T, K) : 0;
   if (K < 1 || K > 8) return 0;
   const int KP = K <= 2 ? 2 : K <= 4 ? 4 : 8;
   const int64_t spw = 64 / (KP * KP);
@@ -221,7 +221,7 @@ static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 int launch_viterbi(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths, int64_t B,
                    int64_t T, int64_t K, int32_t* path, float* score, void* ws, size_t ws_bytes, hipStream_t s) {
   if (B == 0) return VQHMM_OK;
-  if (K < 1 || K > 256 || T < 1 || T > (1 << 28)) return VQHMM_EUNSUPPORTED;
+  if (K < 1 || !hmm_generic_supported(K) || T < 1 || T > (1 << 28)) return VQHMM_EUNSUPPORTED;
   if (!ws || ws_bytes < viterbi_ws_bytes(B, T, K)) return VQHMM_EWORKSPACE;
   if (K > 32) return launch_viterbi_generic(log_pi, log_A, em, lengths, B, T, K, path, score, ws, s);
   if (K > 8) return launch_viterbi_wide(log_pi, log_A, em, lengths, B, T, K, path, score, ws, s);
@@ -1235,7 +1235,7 @@ size_t fwdbwd_ws_bytes(int64_t B, int64_t T, int64_t K) { return 2 * (size_t)B *
 int launch_fwdbwd(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths, int64_t B,
                   int64_t T, int64_t K, float* gamma, float* logZ, void* ws, size_t ws_bytes, hipStream_t s) {
   if (B == 0) return VQHMM_OK;
-  if (K < 1 || K > 256 || T < 1 || T > (1 << 28)) return VQHMM_EUNSUPPORTED;
+  if (K < 1 || !hmm_generic_supported(K) || T < 1 || T > (1 << 28)) return VQHMM_EUNSUPPORTED;
   if (!ws || ws_bytes < fwdbwd_ws_bytes(B, T, K)) return VQHMM_EWORKSPACE;
   if (K > 32) return launch_fwdbwd_generic(log_pi, log_A, em, lengths, B, T, K, gamma, logZ, ws, s);
   const bool w16 = aligned16(log_A) && aligned16(em);

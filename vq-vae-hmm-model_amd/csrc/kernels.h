@@ -205,6 +205,9 @@ size_t vq_quantize_ws_bytes(int64_t B, int64_t Dv, int64_t T, int64_t K);
 int launch_vq_quantize(const float* z, int64_t B, int64_t Dv, int64_t T, const float* cb, int64_t K, int32_t* idx,
                        float* zq_st, double* sse, void* ws, size_t ws_bytes, hipStream_t s);
 int launch_conv(const ConvArgs& a, hipStream_t s);
+// wide convolutions and weight gradients on the f32 MFMA (convbig.hip): Kc % 16 == 0, N % 4 == 0, PCL in / out
+bool convbig_supported(const ConvArgs& a);
+int launch_convbig(const ConvArgs& a, hipStream_t s);
 bool conv2_supported(const ConvArgs& a);
 // front conv + this conv in one launch (conv2.hip conv2f_kernel; ConvArgs::f_*)
 bool conv2_fused_supported(const ConvArgs& a);
@@ -254,6 +257,9 @@ int strip_prof_copy(uint64_t* out, int64_t n);
 int conv2_prof_copy(uint64_t* out, int64_t n);
 int head_prof_copy(uint64_t* out, int64_t n);  // head_coop.hip (VQHMM_HEAD_PROF)
 int launch_wgrad(const WgradArgs& a, hipStream_t s);
+bool wgradbig_supported(const WgradArgs& a);
+int64_t wgradbig_rows(int64_t R, int N, int C);
+int launch_wgradbig(const WgradArgs& a, hipStream_t s);
 int64_t wgrad_chunks(int64_t R, int64_t tiles);
 bool wgrad2_supported(const WgradArgs& a);
 int64_t wgrad2_rows(int64_t R, int N, int C, int ks);
@@ -409,7 +415,8 @@ int launch_gather_chunks(const float* src, const int64_t* meta, int64_t B, int64
 int launch_log_softmax_vec(const float* x, int K, float* out, hipStream_t s);
 int launch_argmax_cf(const float* q, int64_t B, int64_t K, int64_t T, int32_t* idx, hipStream_t s);
 size_t viterbi_ws_bytes(int64_t B, int64_t T, int64_t K);
-// 32 < K <= 256: one workgroup per sequence, thread = state (hmm_generic.hip)
+// K > 32 (<= 4096): one workgroup per sequence, thread = states j, j + 256, .. (hmm_generic.hip)
+bool hmm_generic_supported(int64_t K);
 size_t hmm_generic_viterbi_ws_bytes(int64_t B, int64_t T, int64_t K);
 size_t hmm_generic_fwdbwd_ws_bytes(int64_t B, int64_t T, int64_t K);
 int launch_viterbi_generic(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths,

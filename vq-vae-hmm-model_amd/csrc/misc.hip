@@ -387,13 +387,19 @@ __device__ __forceinline__ void compose_fwd_block(const float* W, const float* E
     if (Ecopy && o == 0) Ecopy[i] = es[i];
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < K * 3; i += 256) {
+  // output i = (k, tap) per wave (i = wave, wave + 4, ...): lane l sums h = l, l + 64, ... in order, then a
+  // fixed-order wave tree (was one thread per output with an H-long dependent chain: the prologue's longest path)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int i = wave; i < K * 3; i += 4) {
     const int k = i / 3, tap = i % 3;
     float s = 0.f;
-    for (int h = 0; h < H; ++h) s = fmaf(wo[h * 3 + tap], es[k * H + h], s);
-    Wc[(int64_t)o * K * 3 + i] = s;
-    if (img_f) img_f[((int64_t)tap * 16 * c2_nb(H) + o) * c2_ldx(K) + k] = s;
-    if (img_d) img_d[((int64_t)(2 - tap) * 16 * c2_nb(K) + k) * c2_ldx(H) + o] = s;
+    for (int h = lane; h < H; h += 64) s = fmaf(wo[h * 3 + tap], es[k * H + h], s);
+    s = wave_sum_dpp(s);
+    if (lane == 0) {
+      Wc[(int64_t)o * K * 3 + i] = s;
+      if (img_f) img_f[((int64_t)tap * 16 * c2_nb(H) + o) * c2_ldx(K) + k] = s;
+      if (img_d) img_d[((int64_t)(2 - tap) * 16 * c2_nb(K) + k) * c2_ldx(H) + o] = s;
+    }
   }
 }
 __global__ __launch_bounds__(256) void compose_fwd_kernel(const float* W, const float* E, int H, int K, float* Wc) {
@@ -481,9 +487,44 @@ __global__ void logits_bwd_kernel(const float* q, const float* dq_dec, const flo
   }
 }
 
+// The same, lane per channel (K <= 64): P = ld4(K) rounded up to a power of two lanes per row, 64 / P rows per
+// wave, <q, dq> by xor shuffles inside the row's lanes (a fixed tree).  Loads and stores are whole rows, where
+// the thread-per-row form above reads a row's channels with a 16 B-per-lane stride (cfg3 K = 32: 1.77 ms).
+template <int P>
+__global__ __launch_bounds__(256) void logits_bwd_lanes_kernel(const float* q, const float* dq_dec, const float* dqx,
+                                                               const float* dlx, const float* scale, int64_t R, int L,
+                                                               float* dlog) {
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t r = g / P;
+  const int k = (int)(g - r * P);
+  const bool on = r < R && k < L;
+  const float sc = scale ? *scale : 1.f;
+  const int64_t i = r * L + k;
+  const float qk = on ? q[i] : 0.f;
+  const float dq = on ? dq_dec[i] + sc * dqx[i] : 0.f;
+  float s = qk * dq;
+#pragma unroll
+  for (int o = 1; o < P; o <<= 1) s += __shfl_xor(s, o);
+  if (on) dlog[i] = qk * (dq - s) + sc * dlx[i];
+}
+
 int launch_logits_bwd(const float* q, const float* dq_dec, const float* dqx, const float* dlx, const float* scale,
                       int64_t R, int K, float* dlog, hipStream_t s) {
   if (R == 0) return VQHMM_OK;
+  const int L = ld4(K);
+  if (L <= 64) {
+    const int P = L <= 4 ? 4 : L <= 8 ? 8 : L <= 16 ? 16 : L <= 32 ? 32 : 64;
+    const unsigned nb = (unsigned)cdiv(R * P, 256);
+    switch (P) {
+      case 4: logits_bwd_lanes_kernel<4><<<nb, 256, 0, s>>>(q, dq_dec, dqx, dlx, scale, R, L, dlog); break;
+      case 8: logits_bwd_lanes_kernel<8><<<nb, 256, 0, s>>>(q, dq_dec, dqx, dlx, scale, R, L, dlog); break;
+      case 16: logits_bwd_lanes_kernel<16><<<nb, 256, 0, s>>>(q, dq_dec, dqx, dlx, scale, R, L, dlog); break;
+      case 32: logits_bwd_lanes_kernel<32><<<nb, 256, 0, s>>>(q, dq_dec, dqx, dlx, scale, R, L, dlog); break;
+      default: logits_bwd_lanes_kernel<64><<<nb, 256, 0, s>>>(q, dq_dec, dqx, dlx, scale, R, L, dlog); break;
+    }
+    VQHMM_LAUNCH_CHECK();
+    return VQHMM_OK;
+  }
   logits_bwd_kernel<<<(unsigned)cdiv(R, 256), 256, 0, s>>>(q, dq_dec, dqx, dlx, scale, R, K, dlog);
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;

@@ -39,14 +39,15 @@ constexpr int W2_LDS_MAX = w2_max(w2_max(w2_lds_floats<64, 64>(), w2_lds_floats<
 
 // The composed decoder conv1's embedding-gradient share of one chunk (WgradArgs::cmpW; N = H <= 64 outputs o,
 // C = K <= 8 inputs k): cmp_slab[chunk][k][h] = sum_{o, tap} dWc[o][k][tap] W[o][h][tap] from the chunk's dWc
-// in LDS (cbuf, the slab layout); 4 thread groups split o (o = g, g + 4, ...), combined in a fixed order
-// through part (4 * 8 * 64 floats, the free stage buffer).  dE = sum over chunks (the backward tail).
+// in LDS (cbuf[(o * 3 + tap) * 8 + k], zero for k >= K and o >= H, so the loop below has no branch: the group
+// kernel's code is large, and a branchy epilogue executed once per workgroup measured 13 us of instruction
+// fetch); 4 thread groups split o (o = g, g + 4, ...), combined in a fixed order through part (4 * 8 * 64
+// floats, the free stage buffer).  dE = sum over chunks (the backward tail).
 __device__ __forceinline__ void wgrad_compose_de(const WgradArgs& a, int64_t chunk, const float* cbuf, float* part) {
   const int H = a.N, K = a.C, tid = threadIdx.x, h = tid & 63, g = tid >> 6;
-  // all 48 weight loads in flight at once (clamped addresses, no branch), across the barrier that publishes
-  // cbuf: one memory latency instead of a chain of them
+  // all 48 weight loads in flight at once (clamped addresses), across the barrier that publishes cbuf
   float w[16][3];
-  const int hc = h < H ? h : H - 1;
+  const int hc = min(h, H - 1);
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int o = min(g + 4 * i, H - 1);
@@ -58,15 +59,15 @@ __device__ __forceinline__ void wgrad_compose_de(const WgradArgs& a, int64_t chu
 #pragma unroll
   for (int k = 0; k < 8; ++k) acc[k] = 0.f;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int o = g + 4 * i;
-    if (o < H && h < H)
+  for (int i = 0; i < 16; ++i)
 #pragma unroll
-      for (int tap = 0; tap < 3; ++tap)
+    for (int tap = 0; tap < 3; ++tap) {
+      const float4* c4 = reinterpret_cast<const float4*>(cbuf + ((g + 4 * i) * 3 + tap) * 8);
+      const float4 lo = c4[0], hi = c4[1];
+      const float cv[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if (k < K) acc[k] = fmaf(cbuf[(o * K + k) * 3 + tap], w[i][tap], acc[k]);
-  }
+      for (int k = 0; k < 8; ++k) acc[k] = fmaf(cv[k], w[i][tap], acc[k]);
+    }
 #pragma unroll
   for (int k = 0; k < 8; ++k) part[(g * 8 + k) * 64 + h] = acc[k];
   __syncthreads();
@@ -155,6 +156,8 @@ __device__ __forceinline__ void wgrad2_body(const WgradArgs& a, int WN, int WC, 
   float4 pdy[PD], px[PX];
   load_dy(rbeg, pdy);
   load_x(rbeg, px);
+  if (a.cmpW)  // the composed epilogue's dWc buffer: entries no MFMA lane writes (k >= K, o >= H) stay zero
+    for (int i = tid; i < 1536; i += 256) xbuf[i] = 0.f;
   for (int64_t r0 = rbeg; r0 < rend; r0 += RT) {
     __syncthreads();
 #pragma unroll
@@ -281,12 +284,12 @@ __device__ __forceinline__ void wgrad2_body(const WgradArgs& a, int WN, int WC, 
             if constexpr (PK) {
               if (n < a.N && pvalid) {
                 out[((int64_t)n * a.C + pcc) * KS + ptap] = acc[tp][i][j][v];
-                if (a.cmpW) xbuf[(n * a.C + pcc) * KS + ptap] = acc[tp][i][j][v];
+                if (a.cmpW) xbuf[(n * 3 + ptap) * 8 + pcc] = acc[tp][i][j][v];
               }
             } else {
               if (n < a.N && c < a.C) {
                 out[((int64_t)n * a.C + c) * KS + tp] = acc[tp][i][j][v];
-                if (a.cmpW) xbuf[(n * a.C + c) * KS + tp] = acc[tp][i][j][v];
+                if (a.cmpW) xbuf[(n * 3 + tp) * 8 + c] = acc[tp][i][j][v];
               }
             }
           }
