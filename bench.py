@@ -367,6 +367,9 @@ def main():
         sys.exit(f"bench.py: --gpus {a.gpus} but the launcher's WORLD_SIZE is {world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # RCCL's init banner ("RCCL version : ...", NCCL_DEBUG=VERSION) goes to stdout, where rank 0's one JSON line
+    # must stand alone: warnings only (VQHMM_NCCL_DEBUG picks another level)
+    os.environ["NCCL_DEBUG"] = os.environ.get("VQHMM_NCCL_DEBUG", "WARN")
     if world > 1:
         # VQHMM_BENCH_BACKEND=gloo rehearses the N-rank path on a box with fewer GPUs (ranks share
         # devices round-robin; the all-reduce then goes through host memory): never a measurement

@@ -23,6 +23,6 @@ import json
 d = json.load(open("$OUT/bench.json"))
 print(json.dumps({k: d[k] for k in ("value", "ms_per_step", "roofline", "cpu_baseline", "speedup_vs_cpu")})[:1500])
 for f in ("bench_b512", "bench_b256", "bench_b128", "bench_b128_dpform"):
-    e = json.load(open("$OUT/%s.json" % f))
+    e = json.loads([l for l in open("$OUT/%s.json" % f) if l.startswith("{")][-1])
     print(f, e["ms_per_step"], e["value"], e["config"]["step_form"])
 PY

@@ -16,13 +16,12 @@ MAP = {
     ("cfg2", "elbo_head"): "elbo_head_coop_kernel<3, 2, 8, 4>",
     ("cfg2", "strip_fwd(enc_conv1+enc_conv2+to_logits+dec_conv1+dec_conv2+to_params)"): "strip_fwd_kernel<2, 0, 0>",
     ("cfg2", "to_params_dgrad+dec_conv2_dgrad"): "conv2f_kernel<4, 0, 1, 2, false, 1>",
-    ("cfg2", "tail(grad_tail+compose_bwd[+adam])"): "tail_kernel<true>",
+    ("cfg2", "tail(slab reduction+composed dW/dE[+adam])"): "tail_kernel<true>",
     ("cfg2", "inputs_to_pcl+compose_fwd"): "prologue_kernel",
-    ("cfg2", "grad_tail(reduce_slabs+log_prior_grad)"): "grad_tail_kernel",
     ("cfg2", "wgrad_group(all 6 weight gradients)"): "wgrad2_group_kernel",
     ("cfg2", "dec_conv1_dgrad(+logits_bwd, to_logits_dgrad if K<=4)"): "conv2w_kernel<1, 4, 3, 3",
     ("cfg2", "enc_conv2_dgrad"): "conv2w_kernel<4, 2, 3, 2",
-    ("vq_cfg3", "vq_argmin"): "vq_rows_kernel<16, 2, false",
+    ("vq_cfg3", "vq_argmin"): "vq_rows_kernel<16, 2, false, 2, false>",
     ("viterbi_cfg5", "viterbi_cfg5"): "viterbi_kernel<8, true>",
     ("fwdbwd_cfg4", "fwdbwd_cfg4"): "fwdbwd_kernel<8, true>",
 }

@@ -29,13 +29,17 @@ constexpr int RT_S = 96;   // rows per stage of the small jobs (< 4096 outputs: 
 constexpr int RT_S4 = 128;  // ... for the 4-row-wave body (its 16-row slices must split evenly over 4 waves)
 }
 
-// LDS floats of one wgrad2 body: dY stage, X stage, bias partials, row-wave exchange
-template <int NPAD, int CPAD, int RTV = RT>
-constexpr int w2_lds_floats() { return RTV * (NPAD + 4) + (RTV + 2) * (CPAD + 4) + 256 + 1536; }
+// LDS floats of one wgrad2 body: dY stage, X stage (two of each double-buffered), bias partials, row-wave
+// exchange
+template <int NPAD, int CPAD, int RTV = RT, bool DB = false>
+constexpr int w2_lds_floats() { return (DB ? 2 : 1) * (RTV * (NPAD + 4) + (RTV + 2) * (CPAD + 4)) + 256 + 1536; }
 constexpr int w2_max(int a, int b) { return a > b ? a : b; }
 // the group launch's dynamic LDS: the largest body (64x64 at RT, 16x64 / 64x16 small jobs at RT_S)
-constexpr int W2_LDS_MAX = w2_max(w2_max(w2_lds_floats<64, 64>(), w2_lds_floats<16, 16, RT_S4>()),
-                                  w2_max(w2_lds_floats<16, 64, RT_S>(), w2_lds_floats<64, 16, RT_S>()));
+template <bool DB>
+constexpr int w2_lds_max() {
+  return w2_max(w2_max(w2_lds_floats<64, 64, RT, DB>(), w2_lds_floats<16, 16, RT_S4, DB>()),
+                w2_max(w2_lds_floats<16, 64, RT_S, DB>(), w2_lds_floats<64, 16, RT_S, DB>()));
+}
 
 // The composed decoder conv1's embedding-gradient share of one chunk (WgradArgs::cmpW; N = H <= 64 outputs o,
 // C = K <= 8 inputs k): cmp_slab[chunk][k][h] = sum_{o, tap} dWc[o][k][tap] W[o][h][tap] from the chunk's dWc
@@ -82,7 +86,10 @@ __device__ __forceinline__ void wgrad_compose_de(const WgradArgs& a, int64_t chu
 // PK (k = 3, 3*C <= 16): the three taps share ONE 16-wide MFMA column block, column j = tap*C + c
 // (a per-lane gather from the X stage), so a narrow-input layer (enc_conv1 C = 5, the composed
 // decoder conv1 C = K = 3) issues a third of the MFMAs of the tap-major form.
-template <int NBW, int CBW, int KS, int NPAD, int CPAD, int WR, bool PK = false, int RT = vqhmm::RT>
+// DB: the dY / X stages double-buffered in LDS: stage s + 1 is stored from its prefetch registers into the
+// other buffer while stage s's MFMAs run, one barrier per stage (single-buffered: store, barrier, MFMAs,
+// barrier)
+template <int NBW, int CBW, int KS, int NPAD, int CPAD, int WR, bool PK = false, int RT = vqhmm::RT, bool DB = false>
 __device__ __forceinline__ void wgrad2_body(const WgradArgs& a, int WN, int WC, int64_t chunk, float* smem) {
   static_assert(!PK || (KS == 3 && CBW == 1), "packed taps: k = 3, one column block");
   constexpr int KA = PK ? 1 : KS;  // accumulator tap blocks
@@ -90,10 +97,11 @@ __device__ __forceinline__ void wgrad2_body(const WgradArgs& a, int WN, int WC, 
   constexpr int DY4 = RT * NPAD / 4;             // float4 slots of the dY stage
   constexpr int X4 = (RT + 2) * CPAD / 4;        // float4 slots of the X stage
   constexpr int PD = (DY4 + 255) / 256, PX = (X4 + 255) / 256;
-  float* dys = smem;                  // [RT][LDA]
-  float* xs = dys + RT * LDA;         // [RT + 2][LDB]
-  float* bred = xs + (RT + 2) * LDB;  // [256]
-  float* xbuf = bred + 256;           // [1536] row-wave exchange (WR > 1 only with NBW = CBW = 1)
+  constexpr int STG = RT * LDA + (RT + 2) * LDB;  // one dY + X stage
+  float* dys = smem;                             // [RT][LDA] (buffer 0)
+  float* xs = dys + RT * LDA;                    // [RT + 2][LDB]
+  float* bred = smem + (DB ? 2 : 1) * STG;       // [256]
+  float* xbuf = bred + 256;                      // [1536] row-wave exchange (WR > 1 only with NBW = CBW = 1)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lg4 = lane >> 4, l16 = lane & 15;
@@ -106,7 +114,7 @@ __device__ __forceinline__ void wgrad2_body(const WgradArgs& a, int WN, int WC, 
   // stays in flight across the MFMAs; rows outside the chunk / channels past
   // the row are zeroed when the registers are written to LDS.
   const int ldn = ld4(a.N), ldc = ld4(a.C);
-  auto load_dy = [&](int64_t r0, float4* p) {
+  auto load_dy = [&](int64_t r0, float4* p) __attribute__((always_inline)) {
 #pragma unroll
     for (int k = 0; k < PD; ++k) {
       const int s = tid + k * 256;
@@ -116,12 +124,12 @@ __device__ __forceinline__ void wgrad2_body(const WgradArgs& a, int WN, int WC, 
       p[k] = *reinterpret_cast<const float4*>(a.dy + r * ldn + min(c, ldn - 4));
     }
   };
-  auto mask_dy = [&](int64_t r0, int k, float4 v) {
+  auto mask_dy = [&](int64_t r0, int k, float4 v) __attribute__((always_inline)) {
     const int s = tid + k * 256;
     const int row = s / (NPAD / 4), c = (s - row * (NPAD / 4)) * 4;
     return (r0 + row < rend && c < ldn) ? v : make_float4(0.f, 0.f, 0.f, 0.f);
   };
-  auto load_x = [&](int64_t r0, float4* p) {
+  auto load_x = [&](int64_t r0, float4* p) __attribute__((always_inline)) {
 #pragma unroll
     for (int k = 0; k < PX; ++k) {
       const int s = tid + k * 256;
@@ -131,7 +139,7 @@ __device__ __forceinline__ void wgrad2_body(const WgradArgs& a, int WN, int WC, 
       p[k] = *reinterpret_cast<const float4*>(a.x + r * ldc + min(c, ldc - 4));
     }
   };
-  auto mask_x = [&](int64_t r0, int k, float4 v) {
+  auto mask_x = [&](int64_t r0, int k, float4 v) __attribute__((always_inline)) {
     const int s = tid + k * 256;
     const int row = s / (CPAD / 4), c = (s - row * (CPAD / 4)) * 4;
     const int64_t r = r0 - 1 + row;
@@ -158,14 +166,14 @@ __device__ __forceinline__ void wgrad2_body(const WgradArgs& a, int WN, int WC, 
   load_x(rbeg, px);
   if (a.cmpW)  // the composed epilogue's dWc buffer: entries no MFMA lane writes (k >= K, o >= H) stay zero
     for (int i = tid; i < 1536; i += 256) xbuf[i] = 0.f;
-  for (int64_t r0 = rbeg; r0 < rend; r0 += RT) {
-    __syncthreads();
+  // a stage's dY / X rows from the prefetch registers into LDS buffer (db, xb)
+  auto store_stage = [&](int64_t r0, float* db, float* xb) __attribute__((always_inline)) {
 #pragma unroll
     for (int k = 0; k < PD; ++k) {
       const int s = tid + k * 256;
       if (s < DY4) {
         const int row = s / (NPAD / 4), c = (s - row * (NPAD / 4)) * 4;
-        *reinterpret_cast<float4*>(dys + row * LDA + c) = mask_dy(r0, k, pdy[k]);
+        *reinterpret_cast<float4*>(db + row * LDA + c) = mask_dy(r0, k, pdy[k]);
       }
     }
 #pragma unroll
@@ -173,70 +181,116 @@ __device__ __forceinline__ void wgrad2_body(const WgradArgs& a, int WN, int WC, 
       const int s = tid + k * 256;
       if (s < X4) {
         const int row = s / (CPAD / 4), c = (s - row * (CPAD / 4)) * 4;
-        *reinterpret_cast<float4*>(xs + row * LDB + c) = mask_x(r0, k, px[k]);
+        *reinterpret_cast<float4*>(xb + row * LDB + c) = mask_x(r0, k, px[k]);
       }
     }
-    __syncthreads();
-    if (r0 + RT < rend) {
-      load_dy(r0 + RT, pdy);
-      load_x(r0 + RT, px);
-    }
-    if (a.bias_slab) {  // RT / bstep rows per thread for every thread (RT % bstep == 0): all reads in flight
-      float bp[RT / bstep];
+  };
+  // bias partials and this wave's MFMAs over a stored stage
+  auto compute = [&](const float* dys, const float* xs) __attribute__((always_inline)) {
+      if (a.bias_slab) {  // RT / bstep rows per thread for every thread (RT % bstep == 0): all reads in flight
+        float bp[RT / bstep];
 #pragma unroll
-      for (int k = 0; k < RT / bstep; ++k) bp[k] = dys[(brow0 + k * bstep) * LDA + bcol];
+        for (int k = 0; k < RT / bstep; ++k) bp[k] = dys[(brow0 + k * bstep) * LDA + bcol];
 #pragma unroll
-      for (int k = 0; k < RT / bstep; ++k) bacc += bp[k];
-    }
-    // this wave's 16-row slices of the stage, as 4 * (4 / WR) MFMA steps (one row per lane group
-    // each): the operands of step s + 1 are read from LDS while the MFMAs of step s run (two
-    // register sets, sched_barrier keeps the reads ahead); each accumulator's chain is unchanged
-    static_assert((RT / 16) % WR == 0 && RT % 16 == 0, "a stage's 16-row slices split evenly over the row-waves");
-    constexpr int NST = 4 * ((RT / 16) / WR);
-    float av[2][NBW], bv[2][KA][CBW];
-    auto load = [&](int st, float (&a_)[NBW], float (&b_)[KA][CBW]) {
-      const int sl = wr + (st >> 2) * WR, e = st & 3;
-      const int rr = sl * 16 + 4 * lg4 + e;
+        for (int k = 0; k < RT / bstep; ++k) bacc += bp[k];
+      }
+      // this wave's 16-row slices of the stage, as 4 * (4 / WR) MFMA steps (one row per lane group
+      // each): the operands of step s + 1 are read from LDS while the MFMAs of step s run (two
+      // register sets, sched_barrier keeps the reads ahead); each accumulator's chain is unchanged
+      static_assert((RT / 16) % WR == 0 && RT % 16 == 0, "a stage's 16-row slices split evenly over the row-waves");
+      constexpr int NST = 4 * ((RT / 16) / WR);
+      float av[2][NBW], bv[2][KA][CBW];
+      auto load = [&](int st, float (&a_)[NBW], float (&b_)[KA][CBW]) __attribute__((always_inline)) {
+        const int sl = wr + (st >> 2) * WR, e = st & 3;
+        const int rr = sl * 16 + 4 * lg4 + e;
 #pragma unroll
-      for (int i = 0; i < NBW; ++i) a_[i] = dys[rr * LDA + (wn + i * WN) * 16 + l16];
-      if constexpr (PK) {
-        const float xv = xs[(rr + ptap) * LDB + pcc];
-        b_[0][0] = pvalid ? xv : 0.f;
-      } else {
+        for (int i = 0; i < NBW; ++i) a_[i] = dys[rr * LDA + (wn + i * WN) * 16 + l16];
+        if constexpr (PK) {
+          const float xv = xs[(rr + ptap) * LDB + pcc];
+          b_[0][0] = pvalid ? xv : 0.f;
+        } else {
 #pragma unroll
-        for (int tp = 0; tp < KS; ++tp) {
-          const int xrow = rr + (KS == 3 ? tp : 1);
+          for (int tp = 0; tp < KS; ++tp) {
+            const int xrow = rr + (KS == 3 ? tp : 1);
 #pragma unroll
-          for (int j = 0; j < CBW; ++j) b_[tp][j] = xs[xrow * LDB + (wc + j * WC) * 16 + l16];
+            for (int j = 0; j < CBW; ++j) b_[tp][j] = xs[xrow * LDB + (wc + j * WC) * 16 + l16];
+          }
+        }
+      };
+      if (a.pipe) {
+        load(0, av[0], bv[0]);
+#pragma unroll
+        for (int st = 0; st < NST; ++st) {
+          const int cb = st & 1;
+          if (st + 1 < NST) load(st + 1, av[cb ^ 1], bv[cb ^ 1]);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int tp = 0; tp < KA; ++tp)
+#pragma unroll
+            for (int j = 0; j < CBW; ++j)
+#pragma unroll
+              for (int i = 0; i < NBW; ++i) acc[tp][i][j] = mfma16x16x4(av[cb][i], bv[cb][tp][j], acc[tp][i][j]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else {  // A/B reference: the compiler's own schedule
+#pragma unroll
+        for (int st = 0; st < NST; ++st) {
+          load(st, av[0], bv[0]);
+#pragma unroll
+          for (int tp = 0; tp < KA; ++tp)
+#pragma unroll
+            for (int j = 0; j < CBW; ++j)
+#pragma unroll
+              for (int i = 0; i < NBW; ++i) acc[tp][i][j] = mfma16x16x4(av[0][i], bv[0][tp][j], acc[tp][i][j]);
         }
       }
-    };
-    if (a.pipe) {
-      load(0, av[0], bv[0]);
+  };
+  if constexpr (!DB) {
+    for (int64_t r0 = rbeg; r0 < rend; r0 += RT) {
+      __syncthreads();
 #pragma unroll
-      for (int st = 0; st < NST; ++st) {
-        const int cb = st & 1;
-        if (st + 1 < NST) load(st + 1, av[cb ^ 1], bv[cb ^ 1]);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int tp = 0; tp < KA; ++tp)
-#pragma unroll
-          for (int j = 0; j < CBW; ++j)
-#pragma unroll
-            for (int i = 0; i < NBW; ++i) acc[tp][i][j] = mfma16x16x4(av[cb][i], bv[cb][tp][j], acc[tp][i][j]);
-        __builtin_amdgcn_sched_barrier(0);
+      for (int k = 0; k < PD; ++k) {
+        const int s = tid + k * 256;
+        if (s < DY4) {
+          const int row = s / (NPAD / 4), c = (s - row * (NPAD / 4)) * 4;
+          *reinterpret_cast<float4*>(dys + row * LDA + c) = mask_dy(r0, k, pdy[k]);
+        }
       }
-    } else {  // A/B reference: the compiler's own schedule
 #pragma unroll
-      for (int st = 0; st < NST; ++st) {
-        load(st, av[0], bv[0]);
-#pragma unroll
-        for (int tp = 0; tp < KA; ++tp)
-#pragma unroll
-          for (int j = 0; j < CBW; ++j)
-#pragma unroll
-            for (int i = 0; i < NBW; ++i) acc[tp][i][j] = mfma16x16x4(av[0][i], bv[0][tp][j], acc[tp][i][j]);
+      for (int k = 0; k < PX; ++k) {
+        const int s = tid + k * 256;
+        if (s < X4) {
+          const int row = s / (CPAD / 4), c = (s - row * (CPAD / 4)) * 4;
+          *reinterpret_cast<float4*>(xs + row * LDB + c) = mask_x(r0, k, px[k]);
+        }
       }
+      __syncthreads();
+      if (r0 + RT < rend) {
+        load_dy(r0 + RT, pdy);
+        load_x(r0 + RT, px);
+      }
+      compute(dys, xs);
+    }
+  } else {
+    store_stage(rbeg, dys, xs);
+    if (rbeg + RT < rend) {
+      load_dy(rbeg + RT, pdy);
+      load_x(rbeg + RT, px);
+    }
+    __syncthreads();
+    int sb = 0;
+    for (int64_t r0 = rbeg; r0 < rend; r0 += RT, sb ^= 1) {
+      float* const cd = smem + sb * STG;   // this stage
+      float* const nd = smem + (sb ^ 1) * STG;  // the next one, stored while this one's MFMAs run
+      compute(cd, cd + RT * LDA);
+      if (r0 + RT < rend) {
+        store_stage(r0 + RT, nd, nd + RT * LDA);
+        if (r0 + 2 * RT < rend) {
+          load_dy(r0 + 2 * RT, pdy);
+          load_x(r0 + 2 * RT, px);
+        }
+      }
+      __syncthreads();  // the next stage stored; this stage's buffer free for the one after
     }
   }
   // ---- combine the WR row-waves (fixed order), then write the partial
@@ -317,20 +371,21 @@ __global__ __launch_bounds__(256) void wgrad2_kernel(WgradArgs a, int WN, int WC
 // b - blk0[j] of job j.  Each job is one of the launch shapes below (variant id = its row in
 // w2_variant, +10 for k = 3), so every body keeps its own register/LDS layout; big jobs come
 // first so their workgroups start first and the small ones fill the tail.
-#define VQHMM_W2_VARIANTS(KSV, O)                                                   \
-  case O + 0: wgrad2_body<4, 1, KSV, 64, 64, 1>(a, WN, WC, ch, sm); break;               \
-  case O + 1: wgrad2_body<2, 1, KSV, 32, 64, 1>(a, WN, WC, ch, sm); break;               \
-  case O + 2: wgrad2_body<1, 2, KSV, 64, 32, 1>(a, WN, WC, ch, sm); break;               \
-  case O + 3: wgrad2_body<1, 1, KSV, 16, 64, 1, false, RT_S>(a, WN, WC, ch, sm); break;  \
-  case O + 4: wgrad2_body<1, 1, KSV, 64, 16, 1, false, RT_S>(a, WN, WC, ch, sm); break;  \
-  case O + 5: wgrad2_body<1, 1, KSV, 16, 32, 2, false, RT_S>(a, WN, WC, ch, sm); break;  \
-  case O + 6: wgrad2_body<1, 1, KSV, 32, 16, 2, false, RT_S>(a, WN, WC, ch, sm); break;  \
-  case O + 7: wgrad2_body<1, 1, KSV, 32, 32, 1, false, RT_S>(a, WN, WC, ch, sm); break;  \
-  case O + 8: wgrad2_body<1, 1, KSV, 16, 16, 4, false, RT_S4>(a, WN, WC, ch, sm); break;
+#define VQHMM_W2_VARIANTS(KSV, O)                                                       \
+  case O + 0: wgrad2_body<4, 1, KSV, 64, 64, 1, false, RT, DB>(a, WN, WC, ch, sm); break;    \
+  case O + 1: wgrad2_body<2, 1, KSV, 32, 64, 1, false, RT, DB>(a, WN, WC, ch, sm); break;    \
+  case O + 2: wgrad2_body<1, 2, KSV, 64, 32, 1, false, RT, DB>(a, WN, WC, ch, sm); break;    \
+  case O + 3: wgrad2_body<1, 1, KSV, 16, 64, 1, false, RT_S, DB>(a, WN, WC, ch, sm); break;  \
+  case O + 4: wgrad2_body<1, 1, KSV, 64, 16, 1, false, RT_S, DB>(a, WN, WC, ch, sm); break;  \
+  case O + 5: wgrad2_body<1, 1, KSV, 16, 32, 2, false, RT_S, DB>(a, WN, WC, ch, sm); break;  \
+  case O + 6: wgrad2_body<1, 1, KSV, 32, 16, 2, false, RT_S, DB>(a, WN, WC, ch, sm); break;  \
+  case O + 7: wgrad2_body<1, 1, KSV, 32, 32, 1, false, RT_S, DB>(a, WN, WC, ch, sm); break;  \
+  case O + 8: wgrad2_body<1, 1, KSV, 16, 16, 4, false, RT_S4, DB>(a, WN, WC, ch, sm); break;
 
+template <bool DB>
 __global__ __launch_bounds__(256) void wgrad2_group_kernel(WgradGroup g) {
   extern __shared__ float4 smem4[];
-  float* sm = reinterpret_cast<float*>(smem4);  // W2_LDS_MAX floats
+  float* sm = reinterpret_cast<float*>(smem4);  // w2_lds_max<DB>() floats
   if (g.step_inc && blockIdx.x == 0 && threadIdx.x == 0) *g.step_inc = (*g.step_inc & 0xffffffffll) + 1;
   int j = 0;
   while (j + 1 < g.njobs && (int64_t)blockIdx.x >= g.blk0[j + 1]) ++j;
@@ -340,7 +395,7 @@ __global__ __launch_bounds__(256) void wgrad2_group_kernel(WgradGroup g) {
   switch (g.variant[j]) {
     VQHMM_W2_VARIANTS(1, 0)
     VQHMM_W2_VARIANTS(3, 10)
-    case 20: wgrad2_body<1, 1, 3, 64, 16, 1, true, RT_S>(a, WN, WC, ch, sm); break;
+    case 20: wgrad2_body<1, 1, 3, 64, 16, 1, true, RT_S, DB>(a, WN, WC, ch, sm); break;
     default: break;
   }
 }
@@ -425,7 +480,13 @@ int launch_wgrad2_group(const WgradArgs* jobs, int n, hipStream_t s, int64_t* st
     g.blk0[i + 1] = g.blk0[i] + cdiv(a.R, a.rows_per_chunk);
   }
   if (g.blk0[n] == 0) return VQHMM_OK;
-  wgrad2_group_kernel<<<(unsigned)g.blk0[n], 256, W2_LDS_MAX * sizeof(float), s>>>(g);
+  // A/B (profiling build): VQHMM_WGRAD_DB=1 double-buffers the dY / X stages (one barrier per stage)
+  static const bool db = [] {
+    const char* e = VQHMM_PROF_ENV("VQHMM_WGRAD_DB");
+    return e && e[0] == '1';
+  }();
+  if (db) wgrad2_group_kernel<true><<<(unsigned)g.blk0[n], 256, w2_lds_max<true>() * sizeof(float), s>>>(g);
+  else wgrad2_group_kernel<false><<<(unsigned)g.blk0[n], 256, w2_lds_max<false>() * sizeof(float), s>>>(g);
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
 }
