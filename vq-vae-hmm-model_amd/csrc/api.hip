@@ -511,7 +511,7 @@ void make_tail(const ElboPlan& p, const StepCtx& c, TailArgs& ta) {
   const float* gs = c.gscale;
   int n = 0;
   auto seg = [&](const float* slab, int64_t nch, int64_t len, float* out, const float* scale) {
-    ta.s[n++] = SlabSeg{slab, out, scale, nch, len, nullptr, 0, 0, 64};
+    ta.s[n++] = SlabSeg{slab, out, scale, nch, len, nullptr, 0, 0};
   };
   const WLayer* wl = p.wl;
   seg(wl[0].slab, wl[0].nchunks, (int64_t)wl[0].N * wl[0].C, g + off[PAR_W], gs);  // dpar is unscaled
@@ -519,7 +519,7 @@ void make_tail(const ElboPlan& p, const StepCtx& c, TailArgs& ta) {
   seg(wl[1].slab, wl[1].nchunks, (int64_t)wl[1].N * wl[1].C * 3, g + off[DEC2_W], nullptr);
   seg(wl[1].bslab, wl[1].nchunks, wl[1].N, g + off[DEC2_B], nullptr);
   if (p.wgroup) {
-    ta.s[n++] = SlabSeg{wl[2].slab, g + off[DEC1_W], nullptr, wl[2].nchunks, (int64_t)p.H * p.H * 3, p.Ecopy, p.H, p.K, 64};
+    ta.s[n++] = SlabSeg{wl[2].slab, g + off[DEC1_W], nullptr, wl[2].nchunks, (int64_t)p.H * p.H * 3, p.Ecopy, p.H, p.K};
     seg(wl[2].cslab, wl[2].nchunks, (int64_t)p.K * p.H, g + off[EMB], nullptr);
   } else {
     seg(wl[2].slab, wl[2].nchunks, (int64_t)wl[2].N * wl[2].C * 3, p.dWc, nullptr);

@@ -194,20 +194,7 @@ struct SlabSeg {
   // block reduces the dWc slab columns of its own o rows itself
   const float* cmpE;   // (K, H): the embedding as this step's forward used it
   int cmpH, cmpK;
-  int cpb;             // columns per tail block (set by launch_tail: tail_cols_per_block)
 };
-// float4 rows of a plain segment (len % 4 == 0, 16 B aligned slab)
-__host__ __device__ inline bool tail_seg_vec(const SlabSeg& s) {
-  return s.len % 4 == 0 && (reinterpret_cast<uintptr_t>(s.slab) & 15) == 0;
-}
-// Columns per tail block: deep slabs (many chunks, e.g. the head's one slab row per workgroup) get fewer
-// columns and more chunk phases, so a block's loads stay about one round of 8 per thread deep (411 head
-// slab rows at B = 128 took 4 rounds of float4 loads, the 9-column b2 slab 13 rounds of scalar ones).
-__host__ __device__ inline int tail_cols_per_block(const SlabSeg& s) {
-  if (s.cmpE) return 64;
-  if (tail_seg_vec(s)) return s.nchunks <= 128 ? 64 : 16;        // 16 / 64 phases
-  return s.nchunks <= 32 ? 64 : s.nchunks <= 128 ? 16 : 4;         // 4 / 16 / 64 phases
-}
 // largest dWc column span one 64-column block of a composed segment reduces (block_reduce_cols' 256)
 __host__ __device__ inline int64_t composed_block_cols(int H, int K) { return (int64_t)(2 + 62 / (3 * H)) * 3 * K; }
 

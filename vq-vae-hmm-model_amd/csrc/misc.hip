@@ -121,18 +121,16 @@ __device__ int tail_segment_block(const TailArgs& ta, float (&part)[16][64], flo
   int si = 0;
   while (si + 1 < ta.nseg && (int64_t)blockIdx.x >= ta.blk_start[si + 1]) ++si;
   const SlabSeg& sg = ta.s[si];
-  const int cpb = sg.cpb;  // columns per block (tail_cols_per_block)
-  const int64_t col0 = ((int64_t)blockIdx.x - ta.blk_start[si]) * cpb;
+  const int64_t col0 = ((int64_t)blockIdx.x - ta.blk_start[si]) * 64;
   if (sg.cmpE) {
     tail_composed_block(sg, col0, red, scratch, val, colp);
     return si;
   }
-  float* pf = &part[0][0];  // [nph][cpb], nph * cpb <= 1024
-  const bool vec = tail_seg_vec(sg);
-  // nph chunk phases over the block's columns; 8 rows per phase in flight per round
-  const int nph = vec ? 256 / (cpb / 4) : 256 / cpb;
+  const bool vec = (sg.len % 4 == 0) && ((reinterpret_cast<uintptr_t>(sg.slab) & 15) == 0);
+  int nph;
   if (vec) {
-    const int cl = cpb / 4, ph = threadIdx.x / cl, cg = (threadIdx.x - ph * cl) * 4;
+    nph = 16;
+    const int ph = threadIdx.x >> 4, cg = (threadIdx.x & 15) * 4;
     const int64_t c4 = col0 + cg;
     float4 p8[8];
 #pragma unroll
@@ -141,49 +139,52 @@ __device__ int tail_segment_block(const TailArgs& ta, float (&part)[16][64], flo
       const float4* sl = reinterpret_cast<const float4*>(sg.slab + c4);
       const int64_t ld = sg.len / 4;
       int64_t c = ph;
-      for (; c + 7 * nph < sg.nchunks; c += 8 * nph) {
+      for (; c + 112 < sg.nchunks; c += 128) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          const float4 v = sl[(c + nph * k) * ld];
+          const float4 v = sl[(c + 16 * k) * ld];
           p8[k].x += v.x; p8[k].y += v.y; p8[k].z += v.z; p8[k].w += v.w;
         }
       }
 #pragma unroll
       for (int k = 0; k < 8; ++k) {  // < 8 rows left per phase
-        if (c + nph * k < sg.nchunks) {
-          const float4 v = sl[(c + nph * k) * ld];
+        if (c + 16 * k < sg.nchunks) {
+          const float4 v = sl[(c + 16 * k) * ld];
           p8[k].x += v.x; p8[k].y += v.y; p8[k].z += v.z; p8[k].w += v.w;
         }
       }
     }
+    float acc[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       auto g = [&](int k) { return e == 0 ? p8[k].x : e == 1 ? p8[k].y : e == 2 ? p8[k].z : p8[k].w; };
-      pf[ph * cpb + cg + e] = ((g(0) + g(1)) + (g(2) + g(3))) + ((g(4) + g(5)) + (g(6) + g(7)));
+      acc[e] = ((g(0) + g(1)) + (g(2) + g(3))) + ((g(4) + g(5)) + (g(6) + g(7)));
     }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) part[ph][cg + e] = acc[e];
   } else {
-    const int ph = threadIdx.x / cpb, cc = threadIdx.x - ph * cpb;
-    const int64_t cs = col0 + cc;
+    nph = 4;
+    const int64_t cs = col0 + (threadIdx.x & 63);
+    const int ph = threadIdx.x >> 6;
     float p8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (cs < sg.len) {
       int64_t c = ph;
-      for (; c + 7 * nph < sg.nchunks; c += 8 * nph) {
+      for (; c + 28 < sg.nchunks; c += 32) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) p8[k] += sg.slab[(c + nph * k) * sg.len + cs];
+        for (int k = 0; k < 8; ++k) p8[k] += sg.slab[(c + 4 * k) * sg.len + cs];
       }
 #pragma unroll
       for (int k = 0; k < 8; ++k)  // < 8 rows left per phase
-        if (c + nph * k < sg.nchunks) p8[k] += sg.slab[(c + nph * k) * sg.len + cs];
+        if (c + 4 * k < sg.nchunks) p8[k] += sg.slab[(c + 4 * k) * sg.len + cs];
     }
-    pf[ph * cpb + cc] = ((p8[0] + p8[1]) + (p8[2] + p8[3])) + ((p8[4] + p8[5]) + (p8[6] + p8[7]));
+    part[ph][threadIdx.x & 63] = ((p8[0] + p8[1]) + (p8[2] + p8[3])) + ((p8[4] + p8[5]) + (p8[6] + p8[7]));
   }
   __syncthreads();
   const int64_t col = col0 + threadIdx.x;
-  if ((int)threadIdx.x < cpb && col < sg.len) {
+  if (threadIdx.x < 64 && col < sg.len) {
     float v = 0.f;
     for (int h = 0; h < nph; h += 4)
-      v += ((pf[h * cpb + threadIdx.x] + pf[(h + 1) * cpb + threadIdx.x]) + pf[(h + 2) * cpb + threadIdx.x]) +
-           pf[(h + 3) * cpb + threadIdx.x];
+      v += ((part[h][threadIdx.x] + part[h + 1][threadIdx.x]) + part[h + 2][threadIdx.x]) + part[h + 3][threadIdx.x];
     if (sg.scale) v *= *sg.scale;
     sg.out[col] = v;
     *val = v;
@@ -304,14 +305,14 @@ __global__ __launch_bounds__(256) void tail_kernel(TailArgs ta, AdamArgs ad, con
     if constexpr (ADAM) {  // this column's Adam operands in flight across the slab reduction
       int sj = 0;
       while (sj + 1 < ta.nseg && b >= ta.blk_start[sj + 1]) ++sj;
-      const int64_t c = (b - ta.blk_start[sj]) * ta.s[sj].cpb + threadIdx.x;
-      if ((int)threadIdx.x < ta.s[sj].cpb && c < ta.s[sj].len) e = adam_load(ad, (ta.s[sj].out - g) + c, tn);
+      const int64_t c = (b - ta.blk_start[sj]) * 64 + threadIdx.x;
+      if (threadIdx.x < 64 && c < ta.s[sj].len) e = adam_load(ad, (ta.s[sj].out - g) + c, tn);
     }
     float v = 0.f;
     int64_t col;
     const int si = tail_segment_block(ta, part, red, scratch, &v, &col);
     const SlabSeg& sg = ta.s[si];
-    if (ADAM && (int)threadIdx.x < sg.cpb && col < sg.len) adam_apply(ad, (sg.out - g) + col, v, e);
+    if (ADAM && threadIdx.x < 64 && col < sg.len) adam_apply(ad, (sg.out - g) + col, v, e);
   } else if (ta.q0slab && b == nblk) {
     tail_logprior_block(ta, red, scratch);
     if (ADAM && threadIdx.x == 0)
@@ -331,10 +332,7 @@ int launch_tail(TailArgs& ta, const AdamArgs* adam, const float* g, hipStream_t 
   for (int i = 0; i < ta.nseg; ++i)
     if (ta.s[i].cmpE && composed_block_cols(ta.s[i].cmpH, ta.s[i].cmpK) > 256) return VQHMM_EINVAL;
   ta.blk_start[0] = 0;
-  for (int i = 0; i < ta.nseg; ++i) {
-    ta.s[i].cpb = tail_cols_per_block(ta.s[i]);
-    ta.blk_start[i + 1] = ta.blk_start[i] + cdiv(ta.s[i].len, ta.s[i].cpb);
-  }
+  for (int i = 0; i < ta.nseg; ++i) ta.blk_start[i + 1] = ta.blk_start[i] + cdiv(ta.s[i].len, 64);
   const int64_t nb = ta.blk_start[ta.nseg] + (ta.q0slab ? 1 : 0) + (ta.fin_loss ? 1 : 0);
   if (nb == 0) return VQHMM_OK;
   if (adam)
