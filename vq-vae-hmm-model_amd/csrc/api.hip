@@ -35,13 +35,15 @@ struct Carver {
 };
 
 // Head choice (VQHMM_HEAD, read once): default the workgroup-cooperative head (head_coop.hip) wherever it
-// applies; "wave" = the wave-window head for K <= 4 (head_wave.hip), "tile" = the tile-barrier MFMA head
-// (head_mfma.hip) — A/B switches.
+// applies, pipelined (one 8-wave workgroup per CU, elbo_head_pipe_kernel) for K <= 4; "coop" = the
+// two-workgroups-per-CU form for K <= 4 too, "wave" = the wave-window head for K <= 4 (head_wave.hip),
+// "tile" = the tile-barrier MFMA head (head_mfma.hip) — A/B switches.
 int head_choice() {
   static const int v = [] {
     const char* e = VQHMM_ENV("VQHMM_HEAD");
     if (e && strcmp(e, "tile") == 0) return 2;
     if (e && strcmp(e, "wave") == 0) return 1;
+    if (e && strcmp(e, "coop") == 0) return 3;
     return 0;
   }();
   return v;
@@ -123,6 +125,7 @@ struct ElboPlan {
   bool staged;
   bool wave_head;  // head_wave.hip (K <= 4, VQHMM_HEAD=wave)
   bool coop_head;  // head_coop.hip (K <= 8, the default); else head_mfma / head.hip
+  bool pipe_head;  // ... its pipelined kernel (K <= 4)
   bool strip_head;  // the head runs inside the forward strip launch (strip.hip; slabs = its workgroups)
   float *hid, *lgA, *dhid, *nx, *dqc, *trw, *logpi;
   // backward
@@ -163,7 +166,8 @@ ElboPlan plan_elbo(const vqhmm_dims_t* d, int64_t B, int64_t T, void* ws) {
     HeadArgs hc{};
     hc.K = K; hc.U = p.U; hc.TH = p.TH; hc.D = D;
     hc.R = R;
-    p.coop_head = head_coop_supported(hc) && head_choice() == 0;
+    p.coop_head = head_coop_supported(hc) && (head_choice() == 0 || head_choice() == 3);
+    p.pipe_head = p.coop_head && head_pipe_supported(hc) && head_choice() == 0;
     p.wave_head = !p.coop_head && head_mfma_supported(hc) && p.U <= 4 && head_choice() == 1;
   }
   {
@@ -172,7 +176,7 @@ ElboPlan plan_elbo(const vqhmm_dims_t* d, int64_t B, int64_t T, void* ws) {
     p.strip_head = p.coop_head && strip_head_on() && strip_fwd_shapes_ok(D, H, H2, K, R) && strip_head_supported(hc);
   }
   p.hgrid = p.strip_head ? strip_fwd_grid(R)
-            : p.coop_head ? head_coop_grid(R, K) : p.wave_head ? head_wave_grid(R) : head_grid(R);
+            : p.pipe_head ? head_pipe_grid(R) : p.coop_head ? head_coop_grid(R, K) : p.wave_head ? head_wave_grid(R) : head_grid(R);
   p.dpar = c.take<float>(R * ld4(2 * D));
   p.dqx = c.take<float>(R * ld4(K));
   p.dlx = c.take<float>(R * ld4(K));
@@ -724,6 +728,7 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       if (p.staged) return run_staged_head(p, c, w, s);
       if (p.strip_head) return VQHMM_OK;  // in S_ENC2's strip launch
       const HeadArgs h = head_args(p, c);
+      if (p.pipe_head) return launch_head_pipe(h, p.hgrid, s);
       if (p.coop_head) return launch_head_coop(h, p.hgrid, s);
       if (p.wave_head) return launch_head_wave(h, p.hgrid, s);
       return launch_head(h, p.hgrid, s);

@@ -18,6 +18,8 @@
 // Summation order differs from the reference's autograd; the tests hold it to 1e-5 relative.
 #include <stddef.h>
 
+#include <type_traits>
+
 #include "kernels.h"
 #include "prof.h"
 
@@ -531,6 +533,592 @@ __global__ __launch_bounds__(256, 2) void elbo_head_coop_kernel(HeadArgs a) {
     stamp_if(true, 7);
     if (threadIdx.x == 0 && blockIdx.x < 256) g_prof[blockIdx.x * 16 + 8] = (unsigned long long)nwn;
   }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Pipelined head (K <= 4: one 16-wide ij block, KP = 4; TH = 128): ONE 12-wave workgroup per CU runs
+// its windows as a software pipeline instead of two workgroups per CU taking turns.  Waves 0-7 ("MFMA
+// waves", two per SIMD) run the MLP on the matrix cores, waves 8-11 ("row waves", thread = (row, state) as
+// phase B above) the per-row VALU work and the loads; ONE workgroup barrier per window:
+//   step j:  MFMA waves  C(j-1) (MLP backward), then A(j+1) (transition logits)
+//            row waves   u' of window j+2, phase B of j (log_softmax rows, A_i, d logits), the dq / recon
+//                        NLL / entropy / init terms of j-1, then the loads of window j+2
+//   barrier
+// so every SIMD holds two independent MFMA instruction streams and one VALU stream.  Phase A: MFMA wave w
+// takes row block w % 4 over half the hidden blocks (w / 4), its partial logits to lgS[.][w / 4] (phase B
+// adds the halves); phase C: wave w owns hidden blocks [w HBW / 2, (w + 1) HBW / 2).  lgS, dlgS, aS, wS are
+// double-buffered, u' four-deep (C(j-1), A(j+1) and the store of j+2 touch three windows); the row waves
+// pass a window's rows through LDS (three slots), loading them at the start of the step before.  Every per-row expression is phase B's above; the
+// MLP sums run in another order, and the windows' assignment to workgroups (so the slab rows, one per
+// workgroup) differs: the tests hold both heads to the oracle at 1e-5.
+namespace {
+template <int K, int HBW>
+struct PipeLds {
+  static constexpr int TH = 64 * HBW;
+  static constexpr int WR = 64;          // rows per window (63 owned + the halo row)
+  static constexpr int LDW2 = TH + 4;
+  static constexpr int LDL = 20;         // 16 ij + 4
+  float W2S[16 * LDW2];                  // rows ij >= K*K zero (the prologue's image: W2S | W1S contiguous)
+  float W1S[TH * 8];
+  float uS[4][WR * 8];
+  float lgS[2][2][WR * LDL];             // [window parity][hidden half]: partial transition logits
+  float dlgS[2][WR * LDL];
+  float aS[2][WR * 4];
+  float wS[2][WR];
+  float b2S[16];
+  double red[4][4];
+  float q0w[4][4];
+  unsigned long long cnt;
+};
+// the row waves' inputs of one window in LDS: thread vt's CoopRow as RC float4s at [slot][c][vt]
+template <int DM>
+struct PipeRowLds {
+  static constexpr int RF = 4 + 1 + 1 + 3 * (DM / 4) + 1 + 2;  // q, qprev, lg, mu / lv / x, u, L
+  static constexpr int RC = (RF + 3) / 4;
+  float4 v[3][RC][256];
+};
+
+// the row waves' state of one window, from phase B to the terms of the next step
+template <int KP>
+struct PipeRowState {
+  int64_t r;
+  int t;
+  bool valid, own, m;
+  float wgt, qi, rsj;
+  float qv[KP];
+};
+template <int V>
+using ic = std::integral_constant<int, V>;
+}  // namespace
+
+template <int K, int HBW, int DM>
+__global__ __launch_bounds__(768, 1) void elbo_head_pipe_kernel(HeadArgs a) {
+  using S = PipeLds<K, HBW>;
+  constexpr int KP = 4, KK = K * K, HB = 4 * HBW, HB2 = HB / 2, HBW2 = HBW / 2, TH = S::TH, LDL = S::LDL;
+  constexpr int WR = S::WR, WOWN = WR - 1, NRB = WR / 16, SD = (KK + 3) / 4, NC = DM / KP;
+  static_assert(K <= 4 && HBW >= 2, "one 16-wide ij block; a hidden block per MFMA wave");
+  static_assert(offsetof(S, W1S) == offsetof(S, W2S) + sizeof(float) * 16 * S::LDW2, "W2S | W1S contiguous");
+  extern __shared__ float4 smem4[];
+  S& sh = *reinterpret_cast<S*>(smem4);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool mw = wave < 8;  // MFMA waves 0..7; row waves 8..11
+  const int lg4 = lane >> 4, l16 = lane & 15;
+  const int vt = tid & 255, prow = vt / KP, si = vt % KP;  // row waves: (row, state)
+  stamp_if(a.dbg & 16, 0);
+  const int U = a.U, D = a.D;
+  const int ldp = ld4(2 * D), ldx = ld4(D), ldu = ld4(U);
+  const float Bn = loss_norm_batch(a.norm, a.B);
+  const float cpri = -a.beta / Bn;
+  const float cent = a.beta / Bn;
+  const bool grad = a.need_grad != 0;
+  const unsigned Tp = (unsigned)a.T + 2u;
+  const int64_t nwin = cdiv(a.R, WOWN);
+  const int64_t G = gridDim.x;
+  const int nloc = (int64_t)blockIdx.x < nwin ? (int)((nwin - 1 - blockIdx.x) / G + 1) : 0;  // this workgroup's windows
+  auto wr0 = [&](int j) { return ((int64_t)blockIdx.x + (int64_t)j * G) * WOWN; };
+
+  auto load_row = [&](int64_t r0, CoopRow<DM, KP>& v) {
+    const int64_t r = r0 + prow;
+    const unsigned rcl = (unsigned)(r < a.R ? r : a.R - 1);
+    const int b = (int)(rcl / Tp);
+    v.L = a.lengths[b];
+    const float4 q4 = *reinterpret_cast<const float4*>(a.q + (int64_t)rcl * KP);
+    v.q[0] = q4.x; v.q[1] = q4.y; v.q[2] = q4.z; v.q[3] = q4.w;
+    v.qprev = a.q[(int64_t)(rcl > 0 ? rcl - 1 : 0) * KP + si];
+    v.lg = a.logits[(int64_t)rcl * KP + si];
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      const int c = min(si + KP * k, D - 1);
+      v.mu[k] = a.par[(int64_t)rcl * ldp + c];
+      v.lv[k] = a.par[(int64_t)rcl * ldp + D + c];
+      v.x[k] = a.x[(int64_t)rcl * ldx + c];
+    }
+    v.u = a.u[(int64_t)rcl * ldu + min(si, ldu - 1)];
+  };
+  auto load_u = [&](int j) {
+    const int64_t r = wr0(j) + prow;
+    const unsigned rcl = (unsigned)(r < a.R ? r : a.R - 1);
+    return a.u[(int64_t)rcl * ldu + min(si, ldu - 1)];
+  };
+  // u' rows of window j (thread (row, i) writes columns i and i + 4)
+  auto write_u = [&](int j, float uv) {
+    const int64_t r = wr0(j) + prow;
+    const unsigned rcl = (unsigned)(r < a.R ? r : a.R - 1);
+    const int b = (int)(rcl / Tp);
+    const int t = (int)(rcl - (unsigned)b * Tp) - 1;
+    const bool valid = r < a.R && t >= 0 && t < a.T;
+    float* const uSb = sh.uS[j & 3];
+#pragma unroll
+    for (int c = si; c < 8; c += KP) uSb[prow * 8 + c] = c < U ? (valid ? uv : 0.f) : (c == U ? 1.f : 0.f);
+  };
+
+  // ---- staging (as elbo_head_coop_kernel's, over 12 waves); the row waves' first rows in flight across it
+  using RL = PipeRowLds<DM>;
+  RL& rl = *reinterpret_cast<RL*>(reinterpret_cast<char*>(smem4) + ((sizeof(S) + 15) / 16) * 16);
+  float u0 = 0.f;
+  if (!mw && nloc > 0) u0 = load_u(0);
+  if (a.himg) {
+    constexpr int N4 = (16 * S::LDW2 + TH * 8) / 4;
+    for (int c = wave; c * 64 < N4; c += 12) {
+      const int i = c * 64 + lane;
+      if (i < N4)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint32_t*>(a.himg) + 4 * i,
+                                         (__attribute__((address_space(3))) void*)(sh.W2S + c * 256), 16, 0, 0);
+    }
+  } else {
+    for (int i = tid; i < 16 * S::LDW2; i += 768) {
+      const int ij = i / S::LDW2, h = i - ij * S::LDW2;
+      sh.W2S[i] = (ij < KK && h < TH) ? a.W2[ij * TH + h] : 0.f;
+    }
+    for (int i = tid; i < TH * 8; i += 768) {
+      const int h = i >> 3, c = i & 7;
+      sh.W1S[i] = c < U ? a.W1[h * U + c] : (c == U ? a.b1[h] : 0.f);
+    }
+  }
+  for (int i = tid; i < 2 * WR * LDL; i += 768) (&sh.dlgS[0][0])[i] = 0.f;
+  if (tid < 16) sh.b2S[tid] = tid < KK ? a.b2[tid] : 0.f;
+  if (tid == 0) sh.cnt = a.norm ? (unsigned long long)a.norm[0] : a.cnt_in ? (unsigned long long)*a.cnt_in : 0ull;
+  float lp_i = 0.f;
+  {
+    float m = -__builtin_inff();
+    for (int k = 0; k < K; ++k) m = fmaxf(m, a.log_prior[k]);
+    float s = 0.f;
+    for (int k = 0; k < K; ++k) s += __expf(a.log_prior[k] - m);
+    if (si < K) lp_i = a.log_prior[si] - (m + __logf(s));
+  }
+  if (!mw && nloc > 0) write_u(0, u0);
+  __syncthreads();
+  if (!a.norm && !a.cnt_in) {
+    unsigned c = 0;
+    for (int64_t b = tid; b < a.B; b += 768) {
+      const int64_t L = a.lengths[b];
+      c += (unsigned)(L <= 0 ? 0 : (L < a.T ? L : a.T));
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o);
+    if (lane == 0) atomicAdd(&sh.cnt, (unsigned long long)c);
+  }
+  __syncthreads();
+  const float inv_n = 1.0f / fmaxf((float)(sh.cnt * (unsigned long long)D), 1.0f);
+  stamp_if(a.dbg & 16, 1);
+
+  float s_rec = 0.f, s_ent = 0.f, s_tr = 0.f, s_init = 0.f, q0acc = 0.f, db2acc = 0.f;
+  f32x4 gW2[HBW2], gW1[HBW2];
+#pragma unroll
+  for (int hb = 0; hb < HBW2; ++hb) gW2[hb] = gW1[hb] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // The two roles run their own copies of the window loop (one barrier per step in both, so every barrier
+  // meets all 12 waves): each role's registers are then live only in its own loop.
+  if (mw) {
+    const int rbA = wave & 3, hh = wave >> 2;  // phase A: row block, hidden half
+    // window-invariant operands (phase A: its row block's half of the hidden blocks; phase C: its hidden
+    // blocks) in registers where they fit
+    constexpr bool AREG = HB2 <= 8;
+    constexpr int NAR = AREG ? HB2 : 1;
+    float w1r[NAR];
+    f32x4 bbr[NAR], w2r[NAR], b2r;
+    const bool areg = AREG && nloc >= 2;
+    if constexpr (AREG) {
+      if (areg) {
+#pragma unroll
+        for (int e = 0; e < HB2; ++e) {
+          const int hb = hh * HB2 + e;
+          w1r[e] = lg4 < U ? sh.W1S[(hb * 16 + l16) * 8 + lg4] : 0.f;
+#pragma unroll
+          for (int v = 0; v < 4; ++v) bbr[e][v] = sh.W1S[(hb * 16 + 4 * lg4 + v) * 8 + U];
+          w2r[e] = *reinterpret_cast<const f32x4*>(&sh.W2S[l16 * S::LDW2 + hb * 16 + 4 * lg4]);
+        }
+#pragma unroll
+        for (int v = 0; v < 4; ++v) b2r[v] = hh == 0 ? sh.b2S[4 * lg4 + v] : 0.f;
+      }
+    }
+    constexpr bool CREG = HBW2 * SD <= 8;
+    float w1c[HBW2], bb1c[HBW2], w2c[HBW2][CREG ? SD : 1];
+    if constexpr (CREG)
+#pragma unroll
+      for (int hl = 0; hl < HBW2; ++hl) {
+        const int hb = wave * HBW2 + hl;
+        w1c[hl] = sh.W1S[(hb * 16 + l16) * 8 + lg4];
+        bb1c[hl] = sh.W1S[(hb * 16 + l16) * 8 + U];
+#pragma unroll
+        for (int s = 0; s < SD; ++s) w2c[hl][s] = sh.W2S[(4 * s + lg4) * S::LDW2 + hb * 16 + l16];
+      }
+
+    // phase A of window j: row block rbA over hidden blocks [hh HB2, (hh + 1) HB2) -> lgS[j & 1][hh]
+    auto phase_a = [&](int j) {
+      const float ub = sh.uS[j & 3][(rbA * 16 + l16) * 8 + lg4];
+      f32x4 lg0, lg1 = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (areg) {
+        if constexpr (AREG) {
+          f32x4 hc[HB2];
+#pragma unroll
+          for (int e = 0; e < HB2; ++e) hc[e] = mfma16x16x4(w1r[e], ub, bbr[e]);  // hid^T, bias start
+          lg0 = b2r;
+#pragma unroll
+          for (int e = 0; e < HB2; e += 2)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+              lg0 = mfma16x16x4(w2r[e][v], relu_f(hc[e][v]), lg0);
+              lg1 = mfma16x16x4(w2r[e + 1][v], relu_f(hc[e + 1][v]), lg1);
+            }
+        }
+      } else {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) lg0[v] = hh == 0 ? sh.b2S[4 * lg4 + v] : 0.f;
+#pragma unroll 2
+        for (int e = 0; e < HB2; e += 2) {
+          f32x4 hc[2], w2v[2];
+#pragma unroll
+          for (int f = 0; f < 2; ++f) {
+            const int hb = hh * HB2 + e + f;
+            const float w1a = lg4 < U ? sh.W1S[(hb * 16 + l16) * 8 + lg4] : 0.f;
+            f32x4 bb;
+#pragma unroll
+            for (int v = 0; v < 4; ++v) bb[v] = sh.W1S[(hb * 16 + 4 * lg4 + v) * 8 + U];
+            w2v[f] = *reinterpret_cast<const f32x4*>(&sh.W2S[l16 * S::LDW2 + hb * 16 + 4 * lg4]);
+            hc[f] = mfma16x16x4(w1a, ub, bb);
+          }
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            lg0 = mfma16x16x4(w2v[0][v], relu_f(hc[0][v]), lg0);
+            lg1 = mfma16x16x4(w2v[1][v], relu_f(hc[1][v]), lg1);
+          }
+        }
+      }
+      f32x4 lg;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) lg[v] = lg0[v] + lg1[v];
+      *reinterpret_cast<f32x4*>(&sh.lgS[j & 1][hh][(rbA * 16 + l16) * LDL + 4 * lg4]) = lg;
+    };
+
+    // phase C of window j (hidden blocks wave HBW2 ..): row block rb's operands, its hidden / d-hidden
+    // blocks (issued between the previous row block's weight-gradient MFMAs), then its weight-gradient MFMAs
+    struct COps {
+      float ua, dla[SD], dlt[4], ubv[4];
+    };
+    auto phase_c = [&](int j) {
+      const float* uSb = sh.uS[j & 3];
+      const float* dlb = sh.dlgS[j & 1];
+      if (wave == 0) {  // db2: column sums of dlg, ij = l16, rows lg4 * 16 ..
+#pragma unroll
+        for (int k = 0; k < WR / 4; ++k) db2acc += dlb[(lg4 * (WR / 4) + k) * LDL + l16];
+      }
+      auto ops = [&](int rb, COps& o) {
+        o.ua = lg4 < U ? uSb[(rb * 16 + l16) * 8 + lg4] : 0.f;
+#pragma unroll
+        for (int s = 0; s < SD; ++s) o.dla[s] = dlb[(rb * 16 + l16) * LDL + 4 * s + lg4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int row = rb * 16 + 4 * lg4 + s;
+          o.dlt[s] = dlb[row * LDL + l16];
+          const float uvv = uSb[row * 8 + (l16 & 7)];
+          o.ubv[s] = l16 < 8 ? uvv : 0.f;
+        }
+      };
+      auto hid = [&](const COps& o, f32x4 (&h)[HBW2], f32x4 (&dh)[HBW2]) {
+#pragma unroll
+        for (int hl = 0; hl < HBW2; ++hl) {
+          const int hb = wave * HBW2 + hl;
+          const float w1 = CREG ? w1c[hl] : sh.W1S[(hb * 16 + l16) * 8 + lg4];
+          const float bb1 = CREG ? bb1c[hl] : sh.W1S[(hb * 16 + l16) * 8 + U];
+          h[hl] = mfma16x16x4(o.ua, w1, f32x4{bb1, bb1, bb1, bb1});
+          dh[hl] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int s = 0; s < SD; ++s)
+#pragma unroll
+          for (int hl = 0; hl < HBW2; ++hl) {
+            const int hb = wave * HBW2 + hl;
+            const float w2 = CREG ? w2c[hl][CREG ? s : 0] : sh.W2S[(4 * s + lg4) * S::LDW2 + hb * 16 + l16];
+            dh[hl] = mfma16x16x4(o.dla[s], w2, dh[hl]);  // dlg @ W2
+          }
+      };
+      COps oc, on;
+      f32x4 h[HBW2], dh[HBW2];
+      ops(0, oc);
+      hid(oc, h, dh);
+#pragma unroll
+      for (int rb = 0; rb < NRB; ++rb) {
+        if (rb + 1 < NRB) ops(rb + 1, on);
+        f32x4 hr[HBW2], dm[HBW2];
+#pragma unroll
+        for (int hl = 0; hl < HBW2; ++hl)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            hr[hl][v] = relu_f(h[hl][v]);
+            dm[hl][v] = h[hl][v] > 0.f ? dh[hl][v] : 0.f;
+          }
+        if (rb + 1 < NRB) hid(on, h, dh);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int hl = 0; hl < HBW2; ++hl) {
+            gW2[hl] = mfma16x16x4(oc.dlt[s], hr[hl][s], gW2[hl]);  // dlg^T hid
+            gW1[hl] = mfma16x16x4(dm[hl][s], oc.ubv[s], gW1[hl]);  // dhid^T u'
+          }
+        oc = on;
+      }
+    };
+
+    for (int j = -1; j <= nloc; ++j) {
+      if (j >= 1 && grad) phase_c(j - 1);
+      if (j == 1) stamp_if(a.dbg & 16, 11);
+      if (j + 1 < nloc) phase_a(j + 1);
+      if (j == 1) stamp_if(a.dbg & 16, 12);
+      lds_barrier();
+      if (j == -1) stamp_if(a.dbg & 16, 9);
+      if (j == 0) stamp_if(a.dbg & 16, 10);
+      if (j == 1) stamp_if(a.dbg & 16, 2);
+    }
+  } else {
+    const int rw = wave - 8;
+    // the row waves are the youngest on every SIMD and would get only the VALU issue slots the MFMA waves
+    // leave (age arbitration); their chain is the longer one, so they take priority
+    __builtin_amdgcn_s_setprio(2);
+    PipeRowState<KP> rc{}, rp{};
+    // phase B of window j (its rows in cur) -> log_A rows, A_i, d logits, the state for its terms
+    auto phase_b = [&](int j, const CoopRow<DM, KP>& cur, PipeRowState<KP>& rs) {
+      const int64_t r0 = wr0(j);
+      const int nown = (int)min<int64_t>(WOWN, a.R - r0);
+      rs.r = r0 + prow;
+      const unsigned rcl = (unsigned)(rs.r < a.R ? rs.r : a.R - 1);
+      const int b = (int)(rcl / Tp);
+      rs.t = (int)(rcl - (unsigned)b * Tp) - 1;
+      rs.valid = rs.r < a.R && rs.t >= 0 && rs.t < a.T;
+      rs.own = prow < nown;
+      rs.m = rs.valid && rs.t < cur.L;
+      rs.wgt = (rs.valid && rs.t >= 1 && rs.t < cur.L) ? 1.f : 0.f;
+#pragma unroll
+      for (int k = 0; k < KP; ++k) rs.qv[k] = (rs.valid && k < K) ? cur.q[k] : 0.f;
+      const float qp = (rs.valid && rs.t >= 1 && si < K) ? cur.qprev : 0.f;
+      rs.qi = 0.f;
+#pragma unroll
+      for (int k = 0; k < KP; ++k) rs.qi = si == k ? rs.qv[k] : rs.qi;
+      float la[KP];
+      float A_i = 0.f;
+      {
+        const int o = prow * LDL + (si < K ? si : 0) * K;
+        const float* l0 = &sh.lgS[j & 1][0][o];
+        const float* l1 = &sh.lgS[j & 1][1][o];
+        float mx = -__builtin_inff();
+#pragma unroll
+        for (int jj = 0; jj < KP; ++jj) {
+          la[jj] = jj < K ? l0[jj] + l1[jj] : 0.f;
+          if (jj < K) mx = fmaxf(mx, la[jj]);
+        }
+        float se = 0.f;
+#pragma unroll
+        for (int jj = 0; jj < K; ++jj) se += __expf(la[jj] - mx);
+        const float ls = mx + __logf(se);
+#pragma unroll
+        for (int jj = 0; jj < K; ++jj) la[jj] -= ls;
+#pragma unroll
+        for (int jj = 0; jj < K; ++jj) A_i = fmaf(rs.qv[jj], la[jj], A_i);
+        if (si >= K) A_i = 0.f;
+        float c[KP];
+#pragma unroll
+        for (int jj = 0; jj < KP; ++jj) c[jj] = (jj < K && si < K) ? qp * la[jj] : 0.f;
+        rs.rsj = row_reduce_scatter<KP>(c, si);
+      }
+      if (rs.own && si < K) s_tr = fmaf(rs.wgt * qp, A_i, s_tr);
+      sh.aS[j & 1][prow * KP + si] = A_i;
+      if (si == 0) sh.wS[j & 1][prow] = rs.wgt;
+      if (grad && si < K) {
+        float qs = 0.f;
+#pragma unroll
+        for (int jj = 0; jj < K; ++jj) qs += rs.qv[jj];
+        const float g = rs.own ? cpri * rs.wgt * qp : 0.f;
+        const float rsum = g * qs;
+        float* dl = &sh.dlgS[j & 1][prow * LDL + si * K];
+#pragma unroll
+        for (int jj = 0; jj < K; ++jj) dl[jj] = g * rs.qv[jj] - __expf(la[jj]) * rsum;
+      }
+    };
+    // the terms of window j (its rows in prv, state rs): dq, recon NLL, entropy, init
+    auto phase_rest = [&](int j, const CoopRow<DM, KP>& prv, const PipeRowState<KP>& rs) {
+      const int64_t r = rs.r;
+      if (grad && rs.own) {  // dq (lane si = state j)
+        float v = cpri * (rs.wgt * rs.rsj + sh.wS[j & 1][prow + 1] * sh.aS[j & 1][(prow + 1) * KP + si]);
+        if (rs.valid && rs.t == 0) v = fmaf(cpri, lp_i, v);
+        a.dqx[r * KP + si] = (rs.valid && si < K) ? v : 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < NC; ++k) {
+        const int ch = si + KP * k;
+        float dmu = 0.f, dlv = 0.f;
+        if (rs.own && rs.m && ch < D) {
+          const float ev = __expf(prv.lv[k]);
+          const float var = ev < 1e-8f ? 1e-8f : ev;
+          const float df = prv.mu[k] - prv.x[k];
+          const float r2 = df * df / var;
+          s_rec += 0.5f * (__logf(6.2831855f * var) + r2);
+          dmu = df / var * inv_n;
+          dlv = (ev >= 1e-8f) ? 0.5f * (1.f - r2) * inv_n : 0.f;
+        }
+        if (grad && rs.own && ch < D) {
+          a.dpar[r * ldp + ch] = dmu;
+          a.dpar[r * ldp + D + ch] = dlv;
+        }
+      }
+      if (grad && rs.own && 2 * D + si < ldp) a.dpar[r * ldp + 2 * D + si] = 0.f;
+      {
+        const float lgv = (rs.valid && si < K) ? prv.lg : 0.f;
+        const float mx = row_max<KP>(si < K ? lgv : -__builtin_inff());
+        const float lse = mx + __logf(row_sum<KP>(si < K ? __expf(lgv - mx) : 0.f));
+        const float f = row_sum<KP>(si < K ? rs.qi * (lgv - lse) : 0.f);
+        if (rs.own && rs.m && si == 0) s_ent -= f;
+        if (grad && rs.own) a.dlx[r * KP + si] = (rs.m && si < K) ? cent * rs.qi * ((lgv - lse) - f) : 0.f;
+      }
+      if (rs.own && rs.valid && rs.t == 0 && si < K) {
+        s_init = fmaf(rs.qi, lp_i, s_init);
+        q0acc += rs.qi;
+      }
+    };
+    // a window's rows through LDS: loaded into registers at the start of a step, stored to slot j % 3 at its
+    // end, read there by phase B (next step) and the terms (the step after).  No register set is carried
+    // across a barrier, so the compiler's conservative wait counts never wait for a load issued elsewhere.
+    auto store_rows = [&](int j, const CoopRow<DM, KP>& v) {
+      float f[RL::RC * 4];
+#pragma unroll
+      for (int k = 0; k < RL::RC * 4; ++k) f[k] = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) f[k] = v.q[k];
+      f[4] = v.qprev;
+      f[5] = v.lg;
+#pragma unroll
+      for (int k = 0; k < NC; ++k) {
+        f[6 + k] = v.mu[k];
+        f[6 + NC + k] = v.lv[k];
+        f[6 + 2 * NC + k] = v.x[k];
+      }
+      f[6 + 3 * NC] = v.u;
+      f[7 + 3 * NC] = __builtin_bit_cast(float, (uint32_t)(uint64_t)v.L);
+      f[8 + 3 * NC] = __builtin_bit_cast(float, (uint32_t)((uint64_t)v.L >> 32));
+#pragma unroll
+      for (int c = 0; c < RL::RC; ++c) rl.v[j % 3][c][vt] = make_float4(f[4 * c], f[4 * c + 1], f[4 * c + 2], f[4 * c + 3]);
+    };
+    auto read_rows = [&](int j) {
+      float f[RL::RC * 4];
+#pragma unroll
+      for (int c = 0; c < RL::RC; ++c) {
+        const float4 q = rl.v[j % 3][c][vt];
+        f[4 * c] = q.x; f[4 * c + 1] = q.y; f[4 * c + 2] = q.z; f[4 * c + 3] = q.w;
+      }
+      CoopRow<DM, KP> v;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v.q[k] = f[k];
+      v.qprev = f[4];
+      v.lg = f[5];
+#pragma unroll
+      for (int k = 0; k < NC; ++k) {
+        v.mu[k] = f[6 + k];
+        v.lv[k] = f[6 + NC + k];
+        v.x[k] = f[6 + 2 * NC + k];
+      }
+      v.u = f[6 + 3 * NC];
+      v.L = (int64_t)(((uint64_t)__builtin_bit_cast(uint32_t, f[8 + 3 * NC]) << 32) |
+                      (uint64_t)__builtin_bit_cast(uint32_t, f[7 + 3 * NC]));
+      return v;
+    };
+    for (int j = -1; j <= nloc; ++j) {
+      CoopRow<DM, KP> ld;
+      float ul = 0.f;
+      if (j + 1 < nloc) load_row(wr0(j + 1), ld);  // stored at this step's end
+      if (j + 2 < nloc) ul = load_u(j + 2);
+      if (j >= 0 && j < nloc) phase_b(j, read_rows(j), rc);
+      if (j >= 1) phase_rest(j - 1, read_rows(j - 1), rp);
+      if (j + 1 < nloc) store_rows(j + 1, ld);
+      if (j + 2 < nloc) write_u(j + 2, ul);
+      if ((a.dbg & 16) && j == 1 && rw == 0 && lane == 0 && blockIdx.x < 256)  // row waves' step-1 work done
+        g_prof[blockIdx.x * 16 + 13] = __builtin_amdgcn_s_memrealtime();
+      lds_barrier();
+      rp = rc;
+    }
+  }
+  stamp_if(a.dbg & 16, 3);
+
+  // ---- epilogue: loss partials (row waves), q0 / db2 sums, weight-gradient partials (fixed order)
+  double ds[4] = {(double)s_rec, (double)s_init, (double)s_tr, (double)s_ent};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) ds[k] = wave_sum_dpp(ds[k]);
+  q0acc += __shfl_xor(q0acc, 4);
+  q0acc += __shfl_xor(q0acc, 8);
+  q0acc += xor16(q0acc);
+  q0acc += xor32(q0acc);
+  db2acc += xor16(db2acc);
+  db2acc += xor32(db2acc);
+  if (!mw) {
+    if (lane == 0)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) sh.red[wave - 8][k] = ds[k];
+    if (lane < KP) sh.q0w[wave - 8][lane] = q0acc;
+  }
+  __syncthreads();
+  if (tid < 4) a.part[blockIdx.x * 4 + tid] = ((sh.red[0][tid] + sh.red[1][tid]) + sh.red[2][tid]) + sh.red[3][tid];
+  if (!grad) return;
+  if (tid < K)
+    a.slab_q0[(int64_t)blockIdx.x * K + tid] = ((sh.q0w[0][tid] + sh.q0w[1][tid]) + sh.q0w[2][tid]) + sh.q0w[3][tid];
+  if (!mw) return;
+  if (wave == 0 && lane < 16 && lane < KK) a.slab_b2[(int64_t)blockIdx.x * KK + lane] = db2acc;
+  float* sW2 = a.slab_W2 + (int64_t)blockIdx.x * KK * TH;
+  float* sW1 = a.slab_W1 + (int64_t)blockIdx.x * TH * U;
+  float* sb1 = a.slab_b1 + (int64_t)blockIdx.x * TH;
+#pragma unroll
+  for (int hl = 0; hl < HBW2; ++hl) {
+    const int hb = wave * HBW2 + hl;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int ij = 4 * lg4 + v;
+      if (ij < KK) sW2[ij * TH + hb * 16 + l16] = gW2[hl][v];
+      const int h = hb * 16 + 4 * lg4 + v;
+      if (l16 < U) sW1[h * U + l16] = gW1[hl][v];
+      else if (l16 == U) sb1[h] = gW1[hl][v];
+    }
+  }
+  if (a.dbg & 16) {
+    stamp_if(true, 7);
+    if (threadIdx.x == 0 && blockIdx.x < 256) g_prof[blockIdx.x * 16 + 8] = (unsigned long long)nloc;
+  }
+}
+
+// TH = 128 (at 256 the phase-A operands no longer fit 168 registers)
+bool head_pipe_supported(const HeadArgs& a) { return head_coop_supported(a) && a.K <= 4 && a.TH == 128; }
+
+// one workgroup per CU (256 on MI355X), or one per window below that
+int head_pipe_grid(int64_t R) {
+  static const int cap = [] {
+    const char* e = VQHMM_PROF_ENV("VQHMM_HEAD_PIPE_GRID");
+    const int v = e ? atoi(e) : 0;
+    return v >= 32 && v <= 2048 ? v : 256;
+  }();
+  const int64_t nwin = cdiv(R, 63);
+  return (int)(nwin < cap ? (nwin > 0 ? nwin : 1) : cap);
+}
+
+int launch_head_pipe(const HeadArgs& a0, int grid, hipStream_t s) {
+  if (!head_pipe_supported(a0)) return VQHMM_EUNSUPPORTED;
+  static const int prof = prof_env("VQHMM_HEAD_PROF");
+  HeadArgs a = a0;
+  if (prof) a.dbg |= 16;
+  if (a.R == 0) return VQHMM_OK;
+#define VQHMM_HP(KV, HBWV)                                                                 \
+  {                                                                                        \
+    const size_t lds = (sizeof(PipeLds<KV, HBWV>) + 15) / 16 * 16;                          \
+    if (a.D <= 8) elbo_head_pipe_kernel<KV, HBWV, 8><<<grid, 768, lds + sizeof(PipeRowLds<8>), s>>>(a);   \
+    else elbo_head_pipe_kernel<KV, HBWV, 16><<<grid, 768, lds + sizeof(PipeRowLds<16>), s>>>(a);          \
+  }
+#define VQHMM_HP_TH(KV) VQHMM_HP(KV, 2)
+  switch (a.K) {
+    case 1: VQHMM_HP_TH(1) break;
+    case 2: VQHMM_HP_TH(2) break;
+    case 3: VQHMM_HP_TH(3) break;
+    default: VQHMM_HP_TH(4) break;
+  }
+#undef VQHMM_HP_TH
+#undef VQHMM_HP
+  VQHMM_LAUNCH_CHECK();
+  return VQHMM_OK;
 }
 
 int64_t head_coop_image_floats(int K, int TH) { return (int64_t)16 * ((K * K + 15) / 16) * (TH + 4) + (int64_t)TH * 8; }

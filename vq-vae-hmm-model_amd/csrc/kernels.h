@@ -314,6 +314,10 @@ bool head_coop_supported(const HeadArgs& a);
 int64_t head_coop_image_floats(int K, int TH);
 int head_coop_grid(int64_t R, int K);
 int launch_head_coop(const HeadArgs& a, int grid, hipStream_t s);
+// its pipelined form for K <= 4 (one 8-wave workgroup per CU: MFMA waves + row waves)
+bool head_pipe_supported(const HeadArgs& a);
+int head_pipe_grid(int64_t R);
+int launch_head_pipe(const HeadArgs& a, int grid, hipStream_t s);
 int launch_head(const HeadArgs& a, int grid, hipStream_t s);
 int launch_prior_fwd(const PriorArgs& p, hipStream_t s);
 // Prior.forward on MFMA (prior.hip): K*K <= 64, U <= 4, TH in {64, 128, 256}
