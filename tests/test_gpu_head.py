@@ -1,12 +1,15 @@
 """The fused ELBO heads across the shapes that select them (csrc/api.hip plan_elbo):
 
-  head_coop.hip  K <= 8, U <= 4, TH in {64, 128, 256}, D <= 16   (cfg1 / cfg2 / cfg4; the default)
+  head_coop.hip  elbo_head_pipe_kernel: K <= 4, U <= 4, TH = 128, D <= 16   (cfg1 / cfg2; the default there)
+                 elbo_head_coop_kernel: K <= 8, U <= 4, TH in {64, 128, 256}, D <= 16 otherwise (cfg4)
   head_mfma.hip  K <= 4, U in 5..7, TH in {64, 128}
   staged         everything else (cfg3: K = 32)
 
-head_coop keeps a wave's window-invariant phase-A operands in registers where its workgroup runs two or
-more windows (more than 512 windows: 63 rows each at K <= 4, 31 at K <= 8), so the cases marked "loops"
-run both forms in one launch.
+Both head_coop kernels keep a wave's window-invariant phase-A operands in registers where their
+workgroup runs two or more windows (coop: more than 512 windows of 63 rows at K <= 4, 31 at K <= 8;
+pipe: more than 256 windows), so the cases marked "loops" run both forms in one launch; the pipelined
+kernel's software pipeline (phase A one window ahead, the terms one behind) is exercised by every case
+with more than one window per workgroup.
 
 Each case is one training step's loss (1e-5 relative vs the fp32 CPU oracle) and all 18
 gradients (normwise vs the fp64 oracle on the device forward's ReLU branch), through
@@ -22,7 +25,10 @@ CASES = [
     # (D, H, K, H2, U, TH), B, T
     ((16, 32, 8, 16, 4, 128), 24, 70),
     ((16, 32, 8, 16, 4, 128), 96, 200),    # > 512 windows: workgroups loop over windows
-    ((5, 32, 3, 16, 4, 128), 256, 200),    # loops, K <= 4 (register-resident phase-A operands)
+    ((5, 32, 3, 16, 4, 128), 256, 200),    # pipe, loops (register-resident phase-A operands)
+    ((5, 32, 2, 16, 1, 128), 300, 150),    # pipe, loops, K = 2, U = 1
+    ((5, 32, 4, 16, 4, 128), 64, 200),     # pipe, one window per workgroup (operands from LDS)
+    ((16, 32, 1, 16, 4, 128), 40, 90),     # pipe, K = 1, D = 16
     ((5, 32, 5, 16, 4, 64), 96, 200),      # loops, K = 5
     ((5, 32, 3, 16, 2, 64), 200, 180),     # loops, U < 4
     ((5, 32, 5, 16, 4, 64), 24, 70),
