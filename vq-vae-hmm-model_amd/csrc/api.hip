@@ -35,7 +35,7 @@ struct Carver {
 };
 
 // Head choice (VQHMM_HEAD, read once): default the workgroup-cooperative head (head_coop.hip) wherever it
-// applies, pipelined (one 8-wave workgroup per CU, elbo_head_pipe_kernel) for K <= 4; "coop" = the
+// applies, pipelined (one 12-wave workgroup per CU, elbo_head_pipe_kernel) for K <= 4, TH = 128; "coop" = the
 // two-workgroups-per-CU form for K <= 4 too, "wave" = the wave-window head for K <= 4 (head_wave.hip),
 // "tile" = the tile-barrier MFMA head (head_mfma.hip) — A/B switches.
 int head_choice() {

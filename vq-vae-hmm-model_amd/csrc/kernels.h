@@ -121,7 +121,6 @@ struct WgradArgs {
   int64_t rows_per_chunk;  // multiple of 64
   float* slab;       // [nchunks][N][C][ks]
   float* bias_slab;  // [nchunks][N] or null
-  int pipe;          // wgrad2: software-pipelined operand reads (set by the launcher; VQHMM_WGRAD_PIPE=0 A/B)
   // the composed decoder conv1 (grouped launch; N = H outputs o, C = K inputs k, k = 3, N*C*3 <= 1536):
   // each chunk also writes its share of the embedding gradient,
   //   cmp_slab[chunk][k][h] = sum_{o, tap} dWc_chunk[o][k][tap] * cmpW[o][h][tap],
@@ -314,7 +313,7 @@ bool head_coop_supported(const HeadArgs& a);
 int64_t head_coop_image_floats(int K, int TH);
 int head_coop_grid(int64_t R, int K);
 int launch_head_coop(const HeadArgs& a, int grid, hipStream_t s);
-// its pipelined form for K <= 4 (one 8-wave workgroup per CU: MFMA waves + row waves)
+// its pipelined form for K <= 4, TH = 128 (one 12-wave workgroup per CU: MFMA waves + row waves)
 bool head_pipe_supported(const HeadArgs& a);
 int head_pipe_grid(int64_t R);
 int launch_head_pipe(const HeadArgs& a, int grid, hipStream_t s);

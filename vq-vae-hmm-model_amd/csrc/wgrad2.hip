@@ -217,32 +217,19 @@ __device__ __forceinline__ void wgrad2_body(const WgradArgs& a, int WN, int WC, 
           }
         }
       };
-      if (a.pipe) {
-        load(0, av[0], bv[0]);
+      load(0, av[0], bv[0]);
 #pragma unroll
-        for (int st = 0; st < NST; ++st) {
-          const int cb = st & 1;
-          if (st + 1 < NST) load(st + 1, av[cb ^ 1], bv[cb ^ 1]);
-          __builtin_amdgcn_sched_barrier(0);
+      for (int st = 0; st < NST; ++st) {
+        const int cb = st & 1;
+        if (st + 1 < NST) load(st + 1, av[cb ^ 1], bv[cb ^ 1]);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-          for (int tp = 0; tp < KA; ++tp)
+        for (int tp = 0; tp < KA; ++tp)
 #pragma unroll
-            for (int j = 0; j < CBW; ++j)
+          for (int j = 0; j < CBW; ++j)
 #pragma unroll
-              for (int i = 0; i < NBW; ++i) acc[tp][i][j] = mfma16x16x4(av[cb][i], bv[cb][tp][j], acc[tp][i][j]);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      } else {  // A/B reference: the compiler's own schedule
-#pragma unroll
-        for (int st = 0; st < NST; ++st) {
-          load(st, av[0], bv[0]);
-#pragma unroll
-          for (int tp = 0; tp < KA; ++tp)
-#pragma unroll
-            for (int j = 0; j < CBW; ++j)
-#pragma unroll
-              for (int i = 0; i < NBW; ++i) acc[tp][i][j] = mfma16x16x4(av[0][i], bv[0][tp][j], acc[tp][i][j]);
-        }
+            for (int i = 0; i < NBW; ++i) acc[tp][i][j] = mfma16x16x4(av[cb][i], bv[cb][tp][j], acc[tp][i][j]);
+        __builtin_amdgcn_sched_barrier(0);
       }
   };
   if constexpr (!DB) {
@@ -383,7 +370,7 @@ __global__ __launch_bounds__(256) void wgrad2_kernel(WgradArgs a, int WN, int WC
   case O + 8: wgrad2_body<1, 1, KSV, 16, 16, 4, false, RT_S4, DB>(a, WN, WC, ch, sm); break;
 
 template <bool DB>
-__global__ __launch_bounds__(256) void wgrad2_group_kernel(WgradGroup g) {
+__global__ __launch_bounds__(256, 3) void wgrad2_group_kernel(WgradGroup g) {
   extern __shared__ float4 smem4[];
   float* sm = reinterpret_cast<float*>(smem4);  // w2_lds_max<DB>() floats
   if (g.step_inc && blockIdx.x == 0 && threadIdx.x == 0) *g.step_inc = (*g.step_inc & 0xffffffffll) + 1;
@@ -456,10 +443,6 @@ int launch_wgrad2_group(const WgradArgs* jobs, int n, hipStream_t s, int64_t* st
   if (n < 1 || n > MAX_WJOBS) return VQHMM_EINVAL;
   WgradGroup g{};
   g.step_inc = step_inc;
-  static const bool pipe = [] {
-    const char* e = VQHMM_PROF_ENV("VQHMM_WGRAD_PIPE");
-    return !(e && e[0] == '0');
-  }();
   // biggest outputs first (their chunks run longest)
   int ord[MAX_WJOBS];
   for (int i = 0; i < n; ++i) ord[i] = i;
@@ -474,7 +457,6 @@ int launch_wgrad2_group(const WgradArgs* jobs, int n, hipStream_t s, int64_t* st
     const WgradArgs& a = jobs[ord[i]];
     if (!wgrad2_group_supported(a)) return VQHMM_EINVAL;
     g.job[i] = a;
-    g.job[i].pipe = pipe;
     g.variant[i] = w2_variant(a.N, a.C, a.ks, &g.wn[i], &g.wc[i]);
     if (a.rows_per_chunk % w2_group_rt(g.variant[i])) return VQHMM_EINVAL;
     g.blk0[i + 1] = g.blk0[i] + cdiv(a.R, a.rows_per_chunk);
@@ -537,12 +519,7 @@ static int launch_w2(const WgradArgs& a, int WN, int WC, hipStream_t s) {
   const int64_t nchunks = cdiv(a.R, a.rows_per_chunk);
   if (WR > 1 && (NBW * CBW != 1 || KS * 4 * 64 * (4 / WR) > 1536)) return VQHMM_EUNSUPPORTED;
   if (WN * WC * WR != 4) return VQHMM_EINVAL;
-  static const bool pipe = [] {
-    const char* e = VQHMM_PROF_ENV("VQHMM_WGRAD_PIPE");
-    return !(e && e[0] == '0');
-  }();
   WgradArgs ap = a;
-  ap.pipe = pipe;
   wgrad2_kernel<NBW, CBW, KS, NPAD, CPAD, WR>
       <<<(unsigned)nchunks, 256, w2_lds_floats<NPAD, CPAD>() * sizeof(float), s>>>(ap, WN, WC);
   VQHMM_LAUNCH_CHECK();
