@@ -58,6 +58,15 @@ bool wgroup_enabled() {
   }();
   return v;
 }
+// Grouped weight gradients: dec_conv2's 64 x 64 x 3 job as two 32-output halves (VQHMM_WGRAD_SPLIT, read
+// once): twice the workgroups, each half-length, on the enc_conv2 body.
+bool wgrad_split_on() {
+  static const bool v = [] {
+    const char* e = VQHMM_PROF_ENV("VQHMM_WGRAD_SPLIT");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
 int64_t wgroup_min_rows() {
   static const int64_t v = [] {
     const char* e = VQHMM_PROF_ENV("VQHMM_WGRAD_MINROWS");
@@ -126,6 +135,7 @@ struct ElboPlan {
   bool wave_head;  // head_wave.hip (K <= 4, VQHMM_HEAD=wave)
   bool coop_head;  // head_coop.hip (K <= 8, the default); else head_mfma / head.hip
   bool pipe_head;  // ... its pipelined kernel (K <= 4)
+  bool dec2_split; // grouped weight gradients: dec_conv2's job as two 32-output halves (slabs [half][chunk][32]..)
   bool strip_head;  // the head runs inside the forward strip launch (strip.hip; slabs = its workgroups)
   float *hid, *lgA, *dhid, *nx, *dqc, *trw, *logpi;
   // backward
@@ -228,6 +238,7 @@ ElboPlan plan_elbo(const vqhmm_dims_t* d, int64_t B, int64_t T, void* ws) {
   // the grouped path's tail forms the composed dW itself (a block reduces <= 256 dWc columns)
   p.wgroup = p.wgroup && composed_block_cols(H, K) <= 256;
   p.Wcopy = p.wgroup ? nullptr : c.take<float>((size_t)H * H * 3);
+  p.dec2_split = p.wgroup && wgrad_split_on() && H == 64;
   for (int i = 0; i < p.nwl; ++i) {
     WLayer& w = p.wl[i];
     w.N = shapes[i][0]; w.C = shapes[i][1]; w.ks = shapes[i][2];
@@ -520,8 +531,16 @@ void make_tail(const ElboPlan& p, const StepCtx& c, TailArgs& ta) {
   const WLayer* wl = p.wl;
   seg(wl[0].slab, wl[0].nchunks, (int64_t)wl[0].N * wl[0].C, g + off[PAR_W], gs);  // dpar is unscaled
   seg(wl[0].bslab, wl[0].nchunks, wl[0].N, g + off[PAR_B], gs);
-  seg(wl[1].slab, wl[1].nchunks, (int64_t)wl[1].N * wl[1].C * 3, g + off[DEC2_W], nullptr);
-  seg(wl[1].bslab, wl[1].nchunks, wl[1].N, g + off[DEC2_B], nullptr);
+  if (p.dec2_split) {  // two 32-output halves: [half][chunk][32][C][3], [half][chunk][32]
+    const int64_t hw = (int64_t)32 * wl[1].C * 3;
+    for (int h = 0; h < 2; ++h) {
+      seg(wl[1].slab + h * wl[1].nchunks * hw, wl[1].nchunks, hw, g + off[DEC2_W] + h * hw, nullptr);
+      seg(wl[1].bslab + h * wl[1].nchunks * 32, wl[1].nchunks, 32, g + off[DEC2_B] + h * 32, nullptr);
+    }
+  } else {
+    seg(wl[1].slab, wl[1].nchunks, (int64_t)wl[1].N * wl[1].C * 3, g + off[DEC2_W], nullptr);
+    seg(wl[1].bslab, wl[1].nchunks, wl[1].N, g + off[DEC2_B], nullptr);
+  }
   if (p.wgroup) {
     ta.s[n++] = SlabSeg{wl[2].slab, g + off[DEC1_W], nullptr, wl[2].nchunks, (int64_t)p.H * p.H * 3, p.Ecopy, p.H, p.K};
     seg(wl[2].cslab, wl[2].nchunks, (int64_t)p.K * p.H, g + off[EMB], nullptr);
@@ -758,7 +777,29 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
           return n ? launch_wgrad2_group(sel, n, s, c.adam && tail_fused_on() ? c.adam->step : nullptr) : VQHMM_OK;
         }
         // the fused tail applies Adam without a completion ticket: this launch advances the step counter
-        return launch_wgrad2_group(wa, 6, s, c.adam && tail_fused_on() ? c.adam->step : nullptr);
+        int64_t* step_inc = c.adam && tail_fused_on() ? c.adam->step : nullptr;
+        if (p.dec2_split) {
+          WgradArgs sp[7];
+          int n = 0;
+          for (int i = 0; i < 6; ++i) {
+            if (i != 1) {
+              sp[n++] = wa[i];
+              continue;
+            }
+            const WLayer& L = p.wl[1];
+            for (int h = 0; h < 2; ++h) {
+              WgradArgs hw = wa[1];
+              hw.dy = wa[1].dy + 32 * h;
+              hw.ld_dy = ld4(L.N);
+              hw.N = 32;
+              hw.slab = L.slab + (int64_t)h * L.nchunks * 32 * L.C * L.ks;
+              hw.bias_slab = L.bslab + (int64_t)h * L.nchunks * 32;
+              sp[n++] = hw;
+            }
+          }
+          return launch_wgrad2_group(sp, n, s, step_inc);
+        }
+        return launch_wgrad2_group(wa, 6, s, step_inc);
       }
       return launch_wgrad(wa[st - S_W_PAR], s);
     }

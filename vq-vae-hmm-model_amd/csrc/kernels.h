@@ -121,6 +121,7 @@ struct WgradArgs {
   int64_t rows_per_chunk;  // multiple of 64
   float* slab;       // [nchunks][N][C][ks]
   float* bias_slab;  // [nchunks][N] or null
+  int ld_dy;         // dY row stride in floats (grouped body; a slice of a wider dY), 0: ld4(N)
   // the composed decoder conv1 (grouped launch; N = H outputs o, C = K inputs k, k = 3, N*C*3 <= 1536):
   // each chunk also writes its share of the embedding gradient,
   //   cmp_slab[chunk][k][h] = sum_{o, tap} dWc_chunk[o][k][tap] * cmpW[o][h][tap],

@@ -113,7 +113,7 @@ __device__ __forceinline__ void wgrad2_body(const WgradArgs& a, int WN, int WC, 
   // channels are zero in memory).  No select next to a load, so the prefetch
   // stays in flight across the MFMAs; rows outside the chunk / channels past
   // the row are zeroed when the registers are written to LDS.
-  const int ldn = ld4(a.N), ldc = ld4(a.C);
+  const int ldn = a.ld_dy ? a.ld_dy : ld4(a.N), ldc = ld4(a.C);
   auto load_dy = [&](int64_t r0, float4* p) __attribute__((always_inline)) {
 #pragma unroll
     for (int k = 0; k < PD; ++k) {
