@@ -13,7 +13,7 @@ import sys
 
 # (bench.py section, stage / kernel key) -> substring of the profiled kernel name
 MAP = {
-    ("cfg2", "elbo_head"): "elbo_head_coop_kernel<3, 2, 8, 4>",
+    ("cfg2", "elbo_head"): "elbo_head_pipe_kernel<3, 2, 8>",
     ("cfg2", "strip_fwd(enc_conv1+enc_conv2+to_logits+dec_conv1+dec_conv2+to_params)"): "strip_fwd_kernel<2, 0, 0>",
     ("cfg2", "to_params_dgrad+dec_conv2_dgrad"): "conv2f_kernel<4, 0, 1, 2, false, 1>",
     ("cfg2", "tail(slab reduction+composed dW/dE[+adam])"): "tail_kernel<true>",
