@@ -85,15 +85,21 @@ def test_viterbi_cfg5_long_sequence():
 
 
 # K <= 8 forward-backward has two kernels: the LDS-resident one (whenever its table fits and one
-# round of workgroups covers the batch) and the streaming one (VQHMM_FB_RES=0, read per call)
-FB_KERNELS = ["resident", "streaming"]
+# round of workgroups covers the batch) and the streaming one (VQHMM_FB_RES=0, read per call).  The
+# streaming one forms gamma inside its chains where its LDS histories fit (T up to ~1000), else through
+# the workspace and a gamma pass (VQHMM_FB_FUSE=0 forces that form; both switches read per call).
+FB_KERNELS = ["resident", "streaming", "streaming-unfused"]
 
 
 def use_fb_kernel(monkeypatch, kernel):
-    if kernel == "streaming":
+    if kernel.startswith("streaming"):
         monkeypatch.setenv("VQHMM_FB_RES", "0")
     else:
         monkeypatch.delenv("VQHMM_FB_RES", raising=False)
+    if kernel == "streaming-unfused":
+        monkeypatch.setenv("VQHMM_FB_FUSE", "0")
+    else:
+        monkeypatch.delenv("VQHMM_FB_FUSE", raising=False)
 
 
 @pytest.mark.parametrize("kernel", FB_KERNELS)

@@ -30,6 +30,7 @@
 // writes its slice of the path.
 // Sequences are independent: no inter-workgroup communication.
 #include "hmm_lanes.h"
+#include "prof.h"
 
 namespace vqhmm {
 
@@ -353,18 +354,43 @@ __device__ __forceinline__ void read_fb_chunk(const float* sl, const LaneMap<K, 
   }
 }
 
+// FUSE (round 4): gamma formed beside the chains, as the resident kernel forms it.  Four waves: the two
+// chains and two flush waves; one LDS barrier per chunk iteration pairs alpha's chunk c with beta's data
+// chunk nch-1-c, and while the chains run iteration c + 1 the flush waves take iteration c's vectors
+// (double-buffered) and form gamma_t where the other direction's value is already in an LDS history (from
+// an earlier iteration), keeping their own value there otherwise; the t whose two chunks ran in the same
+// iteration follow after the loop.  No workspace and no gamma pass: HBM sees the tables twice and gamma
+// once.  The histories take the ring one chunk shallower (fb_fused_ok: two workgroups per CU still fit).
 template <int K, bool W16>
-__global__ __launch_bounds__(128) void fwdbwd_kernel(const float* __restrict__ log_pi,
+struct FbStream {
+  using Gm = Geo<K, W16>;
+  using Rg = Ring<K, W16>;
+  static constexpr bool CAN_FUSE = Rg::R >= 3;
+  static constexpr int VB = Gm::SPW * Gm::HC * Gm::KP;
+  __host__ __device__ static constexpr int ring(bool fuse) { return fuse ? Rg::R - 1 : Rg::R; }
+  __host__ __device__ static constexpr int pw(bool fuse) { return ring(fuse) * Gm::SLOT + (fuse ? 2 : 1) * VB; }
+  __host__ __device__ static int hh(int T) { return ((T + Gm::HC - 1) / Gm::HC / 2 + 1) * Gm::HC; }
+  static size_t lds_bytes(bool fuse, int T) {
+    return (2 * (size_t)pw(fuse) + (fuse ? 2 * (size_t)Gm::SPW * hh(T) * Gm::KP + 4 : 0)) * sizeof(float);
+  }
+};
+
+template <int K, bool W16, bool FUSE>
+__global__ __launch_bounds__(FUSE ? 256 : 128) void fwdbwd_kernel(const float* __restrict__ log_pi,
                                                      const float* __restrict__ log_A, const float* __restrict__ em,
                                                      const int64_t* __restrict__ lengths, int64_t B, int T,
                                                      float* __restrict__ gamma, float* __restrict__ logZ,
-                                                     float* __restrict__ ws, int lin_tier) {
+                                                     float* __restrict__ ws, int lin_tier, int no_gamma) {
   using Gm = Geo<K, W16>;
   using Rg = Ring<K, W16>;
-  constexpr int KP = Gm::KP, G = Gm::G, SPW = Gm::SPW, R = Rg::R, HC = Gm::HC;
-  constexpr int VB = SPW * HC * KP;       // per-wave vector buffer [SPW][HC][KP] (floats)
-  constexpr int PW = R * Gm::SLOT + VB;   // LDS floats per wave
-  __shared__ float lds[2 * PW];           // the only LDS object
+  using FS = FbStream<K, W16>;
+  static_assert(!FUSE || FS::CAN_FUSE, "fused gamma needs a ring of three chunks or more");
+  constexpr int KP = Gm::KP, G = Gm::G, SPW = Gm::SPW, R = FS::ring(FUSE), HC = Gm::HC;
+  constexpr int RWAIT = Rg::NI * (R - 1);  // the ring's counted wait: R - 1 chunks stay in flight
+  constexpr int VB = FS::VB;              // per-wave vector buffer [SPW][HC][KP] (floats)
+  constexpr int PW = FS::pw(FUSE);        // LDS floats per wave
+  extern __shared__ float4 smem_fbs[];
+  float* lds = reinterpret_cast<float*>(smem_fbs);  // [2][PW] (+ FUSE: the two histories)
 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63, grp = lane / G, g = lane % G;
@@ -384,8 +410,8 @@ __global__ __launch_bounds__(128) void fwdbwd_kernel(const float* __restrict__ l
   Lmax = __builtin_amdgcn_readfirstlane(Lmax);
   Lmin = __builtin_amdgcn_readfirstlane(Lmin);
   wait_vm<0>();
-  float* ring = lds + wave * PW;
-  float* vbuf = ring + R * Gm::SLOT;
+  float* ring = lds + (wave & 1) * PW;
+  float* vbuf = ring + R * Gm::SLOT;  // (FUSE: two buffers, chunk c in vbuf + (c & 1) VB)
   float* vrow = vbuf + grp * HC * KP;
   float* ws_al = ws;
   float* ws_be = ws + (size_t)B * T * K;
@@ -409,6 +435,67 @@ __global__ __launch_bounds__(128) void fwdbwd_kernel(const float* __restrict__ l
     }
     asm volatile("" ::: "memory");
   };
+  // ---- FUSE: the two histories and the flushes that form gamma (fwdbwd_resident_kernel's rules)
+  const int nchT = (int)cdiv(T, HC), HH = FS::hh(T);
+  (void)nchT;
+  float* hist_a = lds + 2 * PW;                 // al_t at [q][t][state], t < HH
+  float* hist_b = hist_a + SPW * HH * KP;        // be'[d] at [q][d - dbase][state]
+  const int dbase = ((nchunks - 1) / 2) * HC;    // first data step kept in hist_b
+  constexpr int NF = VB / 64;
+  static_assert(!FUSE || VB % 64 == 0, "flush covers whole wave passes");
+  int* fflags = reinterpret_cast<int*>(hist_b + SPW * HH * KP);  // [chain][buffer]: the chunk ran the linear tier
+  auto seqlen = [&](int q) {
+    const int64_t bq = b0 + q;
+    if (bq >= B) return -1;
+    const int64_t l = lengths[bq];
+    return (int)(l <= 0 ? 0 : (l < T ? l : T));
+  };
+  int Lfl[FUSE ? NF : 1];
+  if constexpr (FUSE) {
+#pragma unroll
+    for (int r = 0; r < NF; ++r) Lfl[r] = seqlen((r * 64 + lane) / (HC * KP));
+  }
+  // softmax over the KP-lane state group of lanes idx % KP (padding states masked)
+  auto store_gamma = [&](int q, int t, int j, float xs, bool own) {
+    const float xm = (j < K) ? xs : NEG_INF;
+    const float mx = allred<KP, true>(xm, OpMax{});
+    const float ex = (j < K && mx != NEG_INF) ? fexp2(xm - mx) : 0.f;
+    const float sm = allred<KP, true>(ex, OpAdd{});
+    if (own && j < K) gamma[((b0 + q) * (int64_t)T + t) * K + j] = ex * __builtin_amdgcn_rcpf(sm);
+  };
+  auto flush_alpha_f = [&](int c, bool linear, const float* vb) {
+#pragma unroll
+    for (int r = 0; r < NF; ++r) {
+      const int idx = r * 64 + lane;
+      const int q = idx / (HC * KP), rr = idx - q * (HC * KP), s = rr / KP, j = rr - s * KP;
+      const int t = c * HC + s;
+      const float v = linear ? flog2(vb[idx]) : vb[idx];
+      if (t < HH) hist_a[(q * HH + t) * KP + j] = v;
+      const int Lq = Lfl[r];
+      const bool ok = Lq >= 0 && t < T;
+      const bool own = ok && (t >= Lq - 1 || t / HC + (t + 1) / HC >= nchunks);
+      const bool past = ok && t >= Lq;  // gamma_t = 0 past the sequence
+      float xs = v;
+      if (own && t < Lq - 1) xs += hist_b[(q * HH + (t + 1 - dbase)) * KP + j];
+      store_gamma(q, t, j, xs, own && !past);
+      if (past && j < K) gamma[((b0 + q) * (int64_t)T + t) * K + j] = 0.f;
+    }
+  };
+  auto flush_beta_f = [&](int k, bool linear, const float* vb) {
+#pragma unroll
+    for (int r = 0; r < NF; ++r) {
+      const int idx = r * 64 + lane;
+      const int q = idx / (HC * KP), rr = idx - q * (HC * KP), s = rr / KP, j = rr - s * KP;
+      const int d = k * HC + s, t = d - 1;
+      const float v = linear ? flog2(vb[idx]) : vb[idx];
+      if (d >= dbase && d - dbase < HH) hist_b[(q * HH + (d - dbase)) * KP + j] = v;
+      const int Lq = Lfl[r];
+      const bool own = Lq >= 0 && t >= 0 && t < Lq - 1 && t / HC + d / HC <= nchunks - 2;
+      const float xs = own ? hist_a[(q * HH + t) * KP + j] + v : 0.f;
+      store_gamma(q, t, j, xs, own);
+    }
+  };
+
   float av[HC], dv[HC], xv[HC], mv[HC], ml[HC];
   float rng = 0.f;  // max |lg column sum| over the chunk's live fast steps
   float x = 0.f, lo = 1.f, hi = 1.f;  // linear tier: chain value, range of the live entries
@@ -488,9 +575,10 @@ __global__ __launch_bounds__(128) void fwdbwd_kernel(const float* __restrict__ l
       });
     };
     for (int c = 0; c < nchunks; ++c) {
+      if constexpr (FUSE) vrow = vbuf + (c & 1) * VB + grp * HC * KP;
       stage_chunk<K, W16>(log_A, em, b0, B, T, min(c + R - 1, nchunks - 1), ring + ((c + R - 1) % R) * Gm::SLOT,
                           lane);
-      wait_vm<Rg::WAIT>();
+      wait_vm<RWAIT>();
       const float* sl = ring + (c % R) * Gm::SLOT;
       const int t0 = c * HC;
       const float al_c = al;
@@ -530,8 +618,14 @@ __global__ __launch_bounds__(128) void fwdbwd_kernel(const float* __restrict__ l
         S2 += (double)tree_sum<HC>(mv);
         SE += (double)tree_sum<HC>(xv);
       }
-      flush(ws_al, t0, linear);
+      if constexpr (FUSE) {
+        if (lane == 0) fflags[c & 1] = linear;
+        lds_barrier();  // chunk c to the flush waves (they take it while this wave runs chunk c + 1)
+      } else {
+        flush(ws_al, t0, linear);
+      }
     }
+    if constexpr (FUSE) lds_barrier();  // the last chunk flushed
     // logZ from the state axis held after step L-1 (even t: inner)
     const int tl = L - 1;
     const bool held_inner = (tl <= 0) || ((tl & 1) == 0);
@@ -544,7 +638,7 @@ __global__ __launch_bounds__(128) void fwdbwd_kernel(const float* __restrict__ l
     if (live && g == 0)
       logZ[b] = L > 0 ? (float)(LN2_D * (S2 + (double)mxs + (double)flog2(sx)) + SE)
                       : __builtin_bit_cast(float, 0x7fc00000u);
-  } else {
+  } else if (!FUSE || wave == 1) {
     // ------------------------------------------------------------ beta
     // chunk k holds data steps [k HC, k HC + HC); data step d serves beta step t = d - 1
     if (nchunks > 0) {
@@ -598,9 +692,10 @@ __global__ __launch_bounds__(128) void fwdbwd_kernel(const float* __restrict__ l
       });
     };
     for (int c = 0; c < nchunks; ++c) {
+      if constexpr (FUSE) vrow = vbuf + (c & 1) * VB + grp * HC * KP;
       const int k = nchunks - 1 - c;
       stage_chunk<K, W16>(log_A, em, b0, B, T, max(k - (R - 1), 0), ring + ((c + R - 1) % R) * Gm::SLOT, lane);
-      wait_vm<Rg::WAIT>();
+      wait_vm<RWAIT>();
       const float* sl = ring + (c % R) * Gm::SLOT;
       const int d0 = k * HC;
       const float be_c = be;
@@ -629,7 +724,27 @@ __global__ __launch_bounds__(128) void fwdbwd_kernel(const float* __restrict__ l
           steps(d0, k == 0, std::true_type{}, std::true_type{});
         }
       }
-      flush(ws_be, d0, linear);
+      if constexpr (FUSE) {
+        if (lane == 0) fflags[2 + (c & 1)] = linear;
+        lds_barrier();
+      } else {
+        flush(ws_be, d0, linear);
+      }
+    }
+    if constexpr (FUSE) lds_barrier();
+  } else {
+    // ------------------------------------------------------------ (FUSE) flush waves: wave 2 alpha's chunks,
+    // wave 3 beta's, one iteration behind the chains
+    if constexpr (FUSE) {
+      const int ch = wave & 1;
+      for (int it = 0; it < nchunks; ++it) {
+        lds_barrier();
+        const bool lin = fflags[2 * ch + (it & 1)] != 0;
+        const float* vb = lds + ch * PW + R * Gm::SLOT + (it & 1) * VB;
+        if (ch == 0) flush_alpha_f(it, lin, vb);
+        else flush_beta_f(nchunks - 1 - it, lin, vb);
+      }
+      lds_barrier();
     }
   }
 
@@ -637,6 +752,29 @@ __global__ __launch_bounds__(128) void fwdbwd_kernel(const float* __restrict__ l
   // (sequence, t) items spread over both waves, GU per thread with all their loads in flight
   // before the first use
   __syncthreads();
+  if constexpr (FUSE) {
+    if (wave == 2) {  // the t whose alpha and beta chunks ran in the same iteration: t/HC + (t+1)/HC == nch - 1
+      const int tb = max(((nchunks - 1) / 2) * HC - 1, 0);
+      for (int idx = lane; idx < SPW * 2 * HC * KP; idx += 64) {  // wave-uniform trip count
+        const int q = idx / (2 * HC * KP), rr = idx - q * (2 * HC * KP), s = rr / KP, j = rr - s * KP;
+        const int t = tb + s;
+        const int Lq = seqlen(q);
+        const bool own = Lq >= 0 && t < Lq - 1 && t / HC + (t + 1) / HC == nchunks - 1;
+        const float xs =
+            own ? hist_a[(q * HH + t) * KP + j] + hist_b[(q * HH + (t + 1 - dbase)) * KP + j] : 0.f;
+        store_gamma(q, t, j, xs, own);
+      }
+    } else if (wave == 3) {  // steps no chain reached: t >= nch * HC
+      const int t0 = nchunks * HC, nt = T - t0;
+      for (int64_t idx = lane; idx < (int64_t)SPW * nt * K; idx += 64) {
+        const int q = (int)(idx / ((int64_t)nt * K));
+        const int64_t rr = idx - (int64_t)q * nt * K;
+        if (b0 + q < B) gamma[((b0 + q) * (int64_t)T + t0) * K + rr] = 0.f;
+      }
+    }
+    return;
+  }
+  if (no_gamma) return;  // timing experiment (profiling build, VQHMM_FB_NOGAMMA): gamma left unwritten
   constexpr int GU = 4;
   const int nit = SPW * T;
   for (int base = 0; base < nit; base += 128 * GU) {
@@ -684,11 +822,30 @@ __global__ __launch_bounds__(128) void fwdbwd_kernel(const float* __restrict__ l
 
 static int fb_lin_tier();
 
+// the fused-gamma streaming kernel where its ring allows it and two workgroups per CU fit (VQHMM_FB_FUSE=0:
+// the workspace + gamma-pass form; a test switch read per call, like VQHMM_FB_RES)
+template <int K, bool W16>
+static bool fb_fused_ok(int64_t T) {
+  const char* env = VQHMM_ENV("VQHMM_FB_FUSE");
+  if (env && env[0] == '0') return false;
+  if constexpr (!FbStream<K, W16>::CAN_FUSE) return false;
+  return T <= (1 << 20) && FbStream<K, W16>::lds_bytes(true, (int)T) <= 80 * 1024;
+}
+
 template <int K, bool W16>
 static void fwdbwd_go(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths, int64_t B,
                       int64_t T, float* gamma, float* logZ, float* ws, hipStream_t s) {
   const dim3 grid((unsigned)cdiv(B, Geo<K, W16>::SPW));
-  fwdbwd_kernel<K, W16><<<grid, 128, 0, s>>>(log_pi, log_A, em, lengths, B, (int)T, gamma, logZ, ws, fb_lin_tier());
+  static const int no_gamma = prof_env("VQHMM_FB_NOGAMMA");
+  if constexpr (FbStream<K, W16>::CAN_FUSE) {
+    if (fb_fused_ok<K, W16>(T)) {
+      fwdbwd_kernel<K, W16, true><<<grid, 256, FbStream<K, W16>::lds_bytes(true, (int)T), s>>>(
+          log_pi, log_A, em, lengths, B, (int)T, gamma, logZ, ws, fb_lin_tier(), 0);
+      return;
+    }
+  }
+  fwdbwd_kernel<K, W16, false><<<grid, 128, FbStream<K, W16>::lds_bytes(false, (int)T), s>>>(
+      log_pi, log_A, em, lengths, B, (int)T, gamma, logZ, ws, fb_lin_tier(), no_gamma);
 }
 
 // ------------------------------------------------- forward-backward, LDS-resident table
