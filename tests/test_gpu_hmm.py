@@ -87,8 +87,9 @@ def test_viterbi_cfg5_long_sequence():
 # K <= 8 forward-backward has two kernels: the LDS-resident one (whenever its table fits and one
 # round of workgroups covers the batch) and the streaming one (VQHMM_FB_RES=0, read per call).  The
 # streaming one forms gamma inside its chains where its LDS histories fit (T up to ~1000), else through
-# the workspace and a gamma pass (VQHMM_FB_FUSE=0 forces that form; both switches read per call).
-FB_KERNELS = ["resident", "streaming", "streaming-unfused"]
+# the workspace and a gamma pass (VQHMM_FB_FUSE=0 forces that form; both switches read per call).  The
+# fused form runs two sequence groups per 8-wave workgroup (VQHMM_FB_PAIR=0: one per 4-wave workgroup).
+FB_KERNELS = ["resident", "streaming", "streaming-single", "streaming-unfused"]
 
 
 def use_fb_kernel(monkeypatch, kernel):
@@ -100,6 +101,33 @@ def use_fb_kernel(monkeypatch, kernel):
         monkeypatch.setenv("VQHMM_FB_FUSE", "0")
     else:
         monkeypatch.delenv("VQHMM_FB_FUSE", raising=False)
+    if kernel == "streaming-single":
+        monkeypatch.setenv("VQHMM_FB_PAIR", "0")
+    else:
+        monkeypatch.delenv("VQHMM_FB_PAIR", raising=False)
+
+
+@pytest.mark.parametrize("K,B,T", [(8, 7, 300), (8, 64, 512), (4, 33, 200), (3, 9, 130)])
+def test_forward_backward_pair_matches_single(K, B, T, monkeypatch):
+    """The 8-wave two-group fused kernel equals the 4-wave one bit for bit: ragged lengths so the two
+    groups of a workgroup run different chunk counts of their own (the workgroup runs the longer), an
+    odd group count so the last workgroup's second group is past the batch."""
+    import vqhmm
+    log_pi, log_A, em = random_hmm(K * 7 + B, B, T, K)
+    rng = np.random.default_rng(B + T)
+    L = rng.integers(0, T + 1, B).astype(np.int64)
+    L[0], L[1] = T, 1
+    args = (*gpu(log_pi, log_A, em), torch.from_numpy(L))
+    monkeypatch.setenv("VQHMM_FB_RES", "0")
+    out = {}
+    for pair in ("1", "0"):
+        monkeypatch.setenv("VQHMM_FB_PAIR", pair)
+        g, z = vqhmm.forward_backward(*args)
+        out[pair] = (g.cpu().numpy(), z.cpu().numpy())
+    assert np.array_equal(out["1"][0].view(np.uint32), out["0"][0].view(np.uint32))
+    assert np.array_equal(out["1"][1].view(np.uint32), out["0"][1].view(np.uint32))
+    rg, _ = hmm_ref.forward_backward_f64(log_pi, log_A, em, L)
+    check_gamma(out["1"][0], rg)
 
 
 @pytest.mark.parametrize("kernel", FB_KERNELS)

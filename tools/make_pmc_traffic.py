@@ -23,7 +23,7 @@ MAP = {
     ("cfg2", "enc_conv2_dgrad"): "conv2w_kernel<4, 2, 3, 2",
     ("vq_cfg3", "vq_argmin"): "vq_rows_kernel<16, 2, false, 2, false>",
     ("viterbi_cfg5", "viterbi_cfg5"): "viterbi_kernel<8, true>",
-    ("fwdbwd_cfg4", "fwdbwd_cfg4"): "fwdbwd_kernel<8, true, true>",
+    ("fwdbwd_cfg4", "fwdbwd_cfg4"): "fwdbwd_kernel<8, true, true, 2>",
 }
 
 

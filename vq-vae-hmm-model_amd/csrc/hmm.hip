@@ -361,6 +361,12 @@ __device__ __forceinline__ void read_fb_chunk(const float* sl, const LaneMap<K, 
 // an earlier iteration), keeping their own value there otherwise; the t whose two chunks ran in the same
 // iteration follow after the loop.  No workspace and no gamma pass: HBM sees the tables twice and gamma
 // once.  The histories take the ring one chunk shallower (fb_fused_ok: two workgroups per CU still fit).
+// NSQ = 2 (the default where it fits): ONE 8-wave workgroup per CU pair of sequence groups, waves 0-3 the
+// four chains (alpha / beta of group 0, then of group 1) so that each chain has a SIMD of its own, at
+// raised priority, and waves 4-7 their flush waves beside them.  Two 4-wave workgroups per CU instead put
+// their waves on the same SIMDs, two chains sharing one (measured below).  Both groups run the
+// workgroup's longest chunk count, so the barrier counts agree; a group past its own length keeps its
+// state, as lanes of one wave with different lengths already do.
 template <int K, bool W16>
 struct FbStream {
   using Gm = Geo<K, W16>;
@@ -370,13 +376,15 @@ struct FbStream {
   __host__ __device__ static constexpr int ring(bool fuse) { return fuse ? Rg::R - 1 : Rg::R; }
   __host__ __device__ static constexpr int pw(bool fuse) { return ring(fuse) * Gm::SLOT + (fuse ? 2 : 1) * VB; }
   __host__ __device__ static int hh(int T) { return ((T + Gm::HC - 1) / Gm::HC / 2 + 1) * Gm::HC; }
-  static size_t lds_bytes(bool fuse, int T) {
-    return (2 * (size_t)pw(fuse) + (fuse ? 2 * (size_t)Gm::SPW * hh(T) * Gm::KP + 4 : 0)) * sizeof(float);
+  // LDS floats of one sequence group (a multiple of 4: every group's base stays 16-B aligned)
+  __host__ __device__ static int group_floats(bool fuse, int T) {
+    return 2 * pw(fuse) + (fuse ? 2 * Gm::SPW * hh(T) * Gm::KP + 4 : 0);
   }
+  static size_t lds_bytes(bool fuse, int T) { return (size_t)group_floats(fuse, T) * sizeof(float); }
 };
 
-template <int K, bool W16, bool FUSE>
-__global__ __launch_bounds__(FUSE ? 256 : 128) void fwdbwd_kernel(const float* __restrict__ log_pi,
+template <int K, bool W16, bool FUSE, int NSQ = 1>
+__global__ __launch_bounds__(FUSE ? 256 * NSQ : 128) void fwdbwd_kernel(const float* __restrict__ log_pi,
                                                      const float* __restrict__ log_A, const float* __restrict__ em,
                                                      const int64_t* __restrict__ lengths, int64_t B, int T,
                                                      float* __restrict__ gamma, float* __restrict__ logZ,
@@ -385,16 +393,22 @@ __global__ __launch_bounds__(FUSE ? 256 : 128) void fwdbwd_kernel(const float* _
   using Rg = Ring<K, W16>;
   using FS = FbStream<K, W16>;
   static_assert(!FUSE || FS::CAN_FUSE, "fused gamma needs a ring of three chunks or more");
+  static_assert(NSQ == 1 || (FUSE && NSQ == 2), "two sequence groups per workgroup: fused form only");
   constexpr int KP = Gm::KP, G = Gm::G, SPW = Gm::SPW, R = FS::ring(FUSE), HC = Gm::HC;
   constexpr int RWAIT = Rg::NI * (R - 1);  // the ring's counted wait: R - 1 chunks stay in flight
   constexpr int VB = FS::VB;              // per-wave vector buffer [SPW][HC][KP] (floats)
   constexpr int PW = FS::pw(FUSE);        // LDS floats per wave
   extern __shared__ float4 smem_fbs[];
-  float* lds = reinterpret_cast<float*>(smem_fbs);  // [2][PW] (+ FUSE: the two histories)
+  const int hwave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // NSQ = 2: sequence group sq, role wave (0 alpha, 1 beta, 2 / 3 their flush waves)
+  const int sq = NSQ == 1 ? 0 : (hwave < 4 ? hwave >> 1 : (hwave - 4) >> 1);
+  const int wave = NSQ == 1 ? hwave : (hwave < 4 ? (hwave & 1) : 2 + (hwave & 1));
+  // one sequence group's LDS: [2][PW] (+ FUSE: the two histories and the flags)
+  float* lds = reinterpret_cast<float*>(smem_fbs) + (NSQ == 1 ? 0 : sq * FS::group_floats(FUSE, T));
+  if (NSQ == 2 && wave < 2) __builtin_amdgcn_s_setprio(2);  // the chains first on the SIMD they share
 
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63, grp = lane / G, g = lane % G;
-  const int64_t b0 = (int64_t)blockIdx.x * SPW;
+  const int64_t b0 = ((int64_t)blockIdx.x * NSQ + sq) * SPW;
   const int64_t b = b0 + grp;
   const bool live = b < B;
   const int64_t Lr = live ? lengths[b] : 0;
@@ -402,6 +416,12 @@ __global__ __launch_bounds__(FUSE ? 256 : 128) void fwdbwd_kernel(const float* _
   const int jo = g % KP, ji = g / KP;  // lane's inner / outer coordinate
   const float lp2 = jo < K ? log_pi[jo] * LOG2E_F : 0.f;
   int Lmax = L, Lmin = L;
+  if constexpr (NSQ == 2) {  // the workgroup's chunk count: over the other group's lengths too
+    const int64_t bo = ((int64_t)blockIdx.x * NSQ + (sq ^ 1)) * SPW + grp;
+    const int64_t Lo = bo < B ? lengths[bo] : 0;
+    const int Lc = (int)(Lo <= 0 ? 0 : (Lo < T ? Lo : T));
+    Lmax = max(Lmax, Lc);  // (Lmin stays the group's own: it only picks the unchecked step form)
+  }
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     Lmax = max(Lmax, __shfl_xor(Lmax, o));
@@ -824,6 +844,11 @@ static int fb_lin_tier();
 
 // the fused-gamma streaming kernel where its ring allows it and two workgroups per CU fit (VQHMM_FB_FUSE=0:
 // the workspace + gamma-pass form; a test switch read per call, like VQHMM_FB_RES)
+// NSQ = 2 unless VQHMM_FB_PAIR=0 (a test switch read per call; bit-identical to NSQ = 1)
+static bool fb_pair_on() {
+  const char* env = VQHMM_ENV("VQHMM_FB_PAIR");
+  return !(env && env[0] == '0');
+}
 template <int K, bool W16>
 static bool fb_fused_ok(int64_t T) {
   const char* env = VQHMM_ENV("VQHMM_FB_FUSE");
@@ -839,8 +864,14 @@ static void fwdbwd_go(const float* log_pi, const float* log_A, const float* em, 
   static const int no_gamma = prof_env("VQHMM_FB_NOGAMMA");
   if constexpr (FbStream<K, W16>::CAN_FUSE) {
     if (fb_fused_ok<K, W16>(T)) {
-      fwdbwd_kernel<K, W16, true><<<grid, 256, FbStream<K, W16>::lds_bytes(true, (int)T), s>>>(
-          log_pi, log_A, em, lengths, B, (int)T, gamma, logZ, ws, fb_lin_tier(), 0);
+      if (fb_pair_on()) {
+        const dim3 grid2((unsigned)cdiv(B, 2 * Geo<K, W16>::SPW));
+        fwdbwd_kernel<K, W16, true, 2><<<grid2, 512, 2 * FbStream<K, W16>::lds_bytes(true, (int)T), s>>>(
+            log_pi, log_A, em, lengths, B, (int)T, gamma, logZ, ws, fb_lin_tier(), 0);
+      } else {
+        fwdbwd_kernel<K, W16, true><<<grid, 256, FbStream<K, W16>::lds_bytes(true, (int)T), s>>>(
+            log_pi, log_A, em, lengths, B, (int)T, gamma, logZ, ws, fb_lin_tier(), 0);
+      }
       return;
     }
   }
