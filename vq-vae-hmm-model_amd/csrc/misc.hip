@@ -637,11 +637,22 @@ __device__ __forceinline__ void to_pcl_slot(const float* __restrict__ src, int C
   const int L4 = ld4(C) / 4;
   const int64_t R = B * (int64_t)(T + 2);
   if (i >= R * L4) return;
-  const int64_t r = i / L4;
-  const int c0 = (int)(i - r * L4) * 4;
-  int64_t b;
-  int t;
-  const bool valid = row_bt(r, R, T, b, t);
+  int64_t r, b;
+  int c0, t;
+  bool valid;
+  if (R * L4 <= 0x7fffffffll) {  // 32-bit index math (a 64-bit division is ~100 VALU ops per thread)
+    const uint32_t i32 = (uint32_t)i, l4 = (uint32_t)L4, tp = (uint32_t)T + 2u;
+    const uint32_t r32 = i32 / l4, b32 = r32 / tp;
+    c0 = (int)(i32 - r32 * l4) * 4;
+    t = (int)(r32 - b32 * tp) - 1;
+    r = r32;
+    b = b32;
+    valid = t >= 0 && t < T;
+  } else {
+    r = i / L4;
+    c0 = (int)(i - r * L4) * 4;
+    valid = row_bt(r, R, T, b, t);
+  }
   float e[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k)
