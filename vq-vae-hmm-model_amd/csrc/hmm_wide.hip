@@ -22,6 +22,7 @@
 // step's spread of 0.
 // gamma = softmax(alpha + beta) over the workspace once both waves finish.
 #include "kernels.h"
+#include "prof.h"
 
 namespace vqhmm {
 
@@ -38,11 +39,11 @@ __device__ __forceinline__ int64_t wide_len(const int64_t* lengths, int64_t b, i
 
 // column orientation (alpha, Viterbi): a[s][ii] = A_t(i0 + ii, j), e[s] = em_t(j), t = t0 + s
 // (clamped into [0, T), values past the chain's end are unused)
-template <int IH>
+template <int IH, int W = WHC>
 __device__ __forceinline__ void load_col_chunk(const float* __restrict__ A, const float* __restrict__ E, int K, int T,
-                                               int t0, int j, int i0, float (&a)[WHC][IH], float (&e)[WHC]) {
+                                               int t0, int j, int i0, float (&a)[W][IH], float (&e)[W]) {
 #pragma unroll
-  for (int s = 0; s < WHC; ++s) {
+  for (int s = 0; s < W; ++s) {
     const int t = min(t0 + s, T - 1);
     const float* At = A + (int64_t)t * K * K;
 #pragma unroll
@@ -55,17 +56,29 @@ __device__ __forceinline__ void load_col_chunk(const float* __restrict__ A, cons
 }
 
 // row orientation (beta): a[s][jj] = A_t(i, j0 + jj), e[s] = em_t(i), t = t0 - s
-template <int IH>
+// V4 (K % 4 == 0, 16-B aligned A): one 16-B load per 4 entries (a quad is wholly inside or outside the row);
+// the scalar form's 32 lanes of a half each read a different row, 32 cache lines per instruction
+template <int IH, int W = WHC, bool V4 = false>
 __device__ __forceinline__ void load_row_chunk(const float* __restrict__ A, const float* __restrict__ E, int K, int T,
-                                               int t0, int i, int j0, float (&a)[WHC][IH], float (&e)[WHC]) {
+                                               int t0, int i, int j0, float (&a)[W][IH], float (&e)[W]) {
 #pragma unroll
-  for (int s = 0; s < WHC; ++s) {
+  for (int s = 0; s < W; ++s) {
     const int t = max(min(t0 - s, T - 1), 0);
     const float* Ar = A + (int64_t)t * K * K + (int64_t)(i < K ? i : 0) * K;
+    if constexpr (V4) {
 #pragma unroll
-    for (int jj = 0; jj < IH; ++jj) {
-      const int jc = j0 + jj;
-      a[s][jj] = (i < K && jc < K) ? Ar[jc] : WNEG_INF;
+      for (int q = 0; q < IH / 4; ++q) {
+        const int jc = j0 + 4 * q;
+        const float4 v = (i < K && jc < K) ? *reinterpret_cast<const float4*>(Ar + jc)
+                                           : make_float4(WNEG_INF, WNEG_INF, WNEG_INF, WNEG_INF);
+        a[s][4 * q] = v.x; a[s][4 * q + 1] = v.y; a[s][4 * q + 2] = v.z; a[s][4 * q + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int jj = 0; jj < IH; ++jj) {
+        const int jc = j0 + jj;
+        a[s][jj] = (i < K && jc < K) ? Ar[jc] : WNEG_INF;
+      }
     }
     e[s] = i < K ? E[(int64_t)t * K + i] : 0.f;
   }
@@ -201,13 +214,14 @@ __global__ __launch_bounds__(64) void viterbi_wide_kernel(const float* __restric
 
 // ------------------------------------------------------------ forward-backward
 // ws: alpha [B][T][K] then beta [B][T][K] (both in natural log, per-step shifted)
-template <int IH>
+template <int IH, int W, bool V4>
 __global__ __launch_bounds__(128) void fwdbwd_wide_kernel(const float* __restrict__ log_pi,
                                                           const float* __restrict__ log_A,
                                                           const float* __restrict__ em,
                                                           const int64_t* __restrict__ lengths, int64_t B, int K,
                                                           int T, float* __restrict__ gamma,
-                                                          float* __restrict__ logZ, float* __restrict__ ws) {
+                                                          float* __restrict__ logZ, float* __restrict__ ws,
+                                                          int dbg) {
   __shared__ __attribute__((aligned(16))) float vsh[2][2][32];  // [wave][parity][state]
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5, i0 = h * IH;
   const int64_t b = blockIdx.x;
@@ -216,9 +230,9 @@ __global__ __launch_bounds__(128) void fwdbwd_wide_kernel(const float* __restric
   const float* E = em + b * (int64_t)T * K;
   float* AL = ws + b * (int64_t)T * K;
   float* BE = ws + (B + b) * (int64_t)T * K;
-  float ca[WHC][IH], ce[WHC], na[WHC][IH], ne[WHC];
+  float ca[W][IH], ce[W], na[W][IH], ne[W];
 
-  if (L > 0 && wave == 0) {
+  if (L > 0 && wave == 0 && !(dbg & 4)) {
     // ---------------------------------------------------------------- alpha
     float e0 = j < K ? E[j] : WNEG_INF;
 #pragma unroll
@@ -230,11 +244,11 @@ __global__ __launch_bounds__(128) void fwdbwd_wide_kernel(const float* __restric
       if (j < K) AL[j] = al;
     }
     double S = (double)e0;  // sum of the subtracted maxima (of alpha_{t-1} and of em_t)
-    if (L > 1) load_col_chunk<IH>(A, E, K, T, 1, j, i0, ca, ce);
-    for (int t0 = 1; t0 < L; t0 += WHC) {
+    if (L > 1) load_col_chunk<IH, W>(A, E, K, T, 1, j, i0, ca, ce);
+    for (int t0 = 1; t0 < L; t0 += W) {
       // emissions shifted by their max over the states, off the chain: em_t(j) - E_t
 #pragma unroll
-      for (int s = 0; s < WHC; ++s) {
+      for (int s = 0; s < W; ++s) {
         float em = j < K ? ce[s] : WNEG_INF;
 #pragma unroll
         for (int o = 1; o < 32; o <<= 1) em = fmaxf(em, __shfl_xor(em, o));
@@ -242,9 +256,9 @@ __global__ __launch_bounds__(128) void fwdbwd_wide_kernel(const float* __restric
         ce[s] -= em;
         if (t0 + s < L) S += (double)em;
       }
-      if (t0 + WHC < L) load_col_chunk<IH>(A, E, K, T, t0 + WHC, j, i0, na, ne);
+      if (t0 + W < L) load_col_chunk<IH, W>(A, E, K, T, t0 + W, j, i0, na, ne);
 #pragma unroll
-      for (int s = 0; s < WHC; ++s) {
+      for (int s = 0; s < W; ++s) {
         const int t = t0 + s;
         if (t >= L) break;
         float v[IH];
@@ -266,7 +280,7 @@ __global__ __launch_bounds__(128) void fwdbwd_wide_kernel(const float* __restric
         }
       }
 #pragma unroll
-      for (int s = 0; s < WHC; ++s) {
+      for (int s = 0; s < W; ++s) {
         ce[s] = ne[s];
 #pragma unroll
         for (int k = 0; k < IH; ++k) ca[s][k] = na[s][k];
@@ -280,16 +294,16 @@ __global__ __launch_bounds__(128) void fwdbwd_wide_kernel(const float* __restric
 #pragma unroll
     for (int o = 1; o < 32; o <<= 1) ex += __shfl_xor(ex, o);
     if (lane == 0) logZ[b] = (float)(S + (double)mx + (double)__logf(ex));
-  } else if (L > 0) {
+  } else if (L > 0 && wave == 1 && !(dbg & 2)) {
     // ----------------------------------------------------------------- beta
     // lane's row state i = j; beta_{L-1} = 0
     float bv = j < K ? 0.f : WNEG_INF;
     if (h == 0 && j < K) BE[(int64_t)(L - 1) * K + j] = 0.f;
-    if (L > 1) load_row_chunk<IH>(A, E, K, T, L - 1, j, i0, ca, ce);
-    for (int t0 = L - 1; t0 >= 1; t0 -= WHC) {  // data step t0 - s serves beta_{t0 - s - 1}
-      if (t0 - WHC >= 1) load_row_chunk<IH>(A, E, K, T, t0 - WHC, j, i0, na, ne);
+    if (L > 1) load_row_chunk<IH, W, V4>(A, E, K, T, L - 1, j, i0, ca, ce);
+    for (int t0 = L - 1; t0 >= 1; t0 -= W) {  // data step t0 - s serves beta_{t0 - s - 1}
+      if (t0 - W >= 1) load_row_chunk<IH, W, V4>(A, E, K, T, t0 - W, j, i0, na, ne);
 #pragma unroll
-      for (int s = 0; s < WHC; ++s) {
+      for (int s = 0; s < W; ++s) {
         const int td = t0 - s;
         if (td < 1) break;
         // w(j') = em_td(j') + beta_td(j') of every state j', through LDS
@@ -309,7 +323,7 @@ __global__ __launch_bounds__(128) void fwdbwd_wide_kernel(const float* __restric
         if (h == 0 && j < K) BE[(int64_t)(td - 1) * K + j] = bv;
       }
 #pragma unroll
-      for (int s = 0; s < WHC; ++s) {
+      for (int s = 0; s < W; ++s) {
         ce[s] = ne[s];
 #pragma unroll
         for (int k = 0; k < IH; ++k) ca[s][k] = na[s][k];
@@ -320,19 +334,26 @@ __global__ __launch_bounds__(128) void fwdbwd_wide_kernel(const float* __restric
 
   // ------------------------------------------------------------------- gamma
   __syncthreads();
-  for (int t = threadIdx.x; t < T; t += 128) {
+  if (dbg & 1) return;  // timing experiment (profiling build, VQHMM_WIDE_DBG): no gamma pass
+  // one row per 32-lane half (lane j = state j), four rows per pass: coalesced row reads and writes, the
+  // softmax's max and sum as xor-shuffle trees inside the half
+  for (int t0 = 0; t0 < T; t0 += 4) {
+    const int t = t0 + 2 * wave + h;  // half-uniform
+    if (t >= T) continue;
     float* g = gamma + (b * (int64_t)T + t) * K;
     if (t >= L) {
-      for (int i = 0; i < K; ++i) g[i] = 0.f;
+      if (j < K) g[j] = 0.f;
       continue;
     }
-    const float* ar = AL + (int64_t)t * K;
-    const float* br = BE + (int64_t)t * K;
-    float mx = WNEG_INF;
-    for (int i = 0; i < K; ++i) mx = fmaxf(mx, ar[i] + br[i]);
-    float sm = 0.f;
-    for (int i = 0; i < K; ++i) sm += mx == WNEG_INF ? 0.f : __expf((ar[i] + br[i]) - mx);
-    for (int i = 0; i < K; ++i) g[i] = mx == WNEG_INF ? 0.f : __expf((ar[i] + br[i]) - mx) / sm;
+    const float x = j < K ? AL[(int64_t)t * K + j] + BE[(int64_t)t * K + j] : WNEG_INF;
+    float mx = x;
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    const float e = (j < K && mx != WNEG_INF) ? __expf(x - mx) : 0.f;
+    float sm = e;
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) sm += __shfl_xor(sm, o);
+    if (j < K) g[j] = mx == WNEG_INF ? 0.f : e / sm;
   }
 }
 
@@ -352,12 +373,20 @@ int launch_viterbi_wide(const float* log_pi, const float* log_A, const float* em
 
 int launch_fwdbwd_wide(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths, int64_t B,
                        int64_t T, int64_t K, float* gamma, float* logZ, float* ws, hipStream_t s) {
-  if (K <= 16)
-    fwdbwd_wide_kernel<8><<<(unsigned)B, 128, 0, s>>>(log_pi, log_A, em, lengths, B, (int)K, (int)T, gamma, logZ,
-                                                      ws);
-  else
-    fwdbwd_wide_kernel<16><<<(unsigned)B, 128, 0, s>>>(log_pi, log_A, em, lengths, B, (int)K, (int)T, gamma, logZ,
-                                                       ws);
+  // VQHMM_WIDE_DBG (profiling build; results invalid): 1 no gamma pass, 2 no beta chain, 4 no alpha chain
+  static const int dbg = prof_env("VQHMM_WIDE_DBG");
+  const bool v4 = K % 4 == 0 && (reinterpret_cast<uintptr_t>(log_A) & 15) == 0;
+#define VQHMM_FBW(IHV, V4V)                                                                                       \
+  fwdbwd_wide_kernel<IHV, WHC, V4V><<<(unsigned)B, 128, 0, s>>>(log_pi, log_A, em, lengths, B, (int)K, (int)T, gamma, \
+                                                                logZ, ws, dbg)
+  if (K <= 16) {
+    if (v4) VQHMM_FBW(8, true);
+    else VQHMM_FBW(8, false);
+  } else {
+    if (v4) VQHMM_FBW(16, true);
+    else VQHMM_FBW(16, false);
+  }
+#undef VQHMM_FBW
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
 }
