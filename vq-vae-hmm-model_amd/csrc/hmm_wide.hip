@@ -19,8 +19,10 @@
 // step is a max-shifted log-sum-exp over the lane's IH terms, joined across the
 // halves, with the previous vector's max and the step's max emission subtracted
 // (their running sum is logZ's offset), so every stored value stays within a
-// step's spread of 0.
-// gamma = softmax(alpha + beta) over the workspace once both waves finish.
+// step's spread of 0.  For K <= 16 its lanes are 16 columns x 4 quarters of the
+// reduced axis (IH = 4; a permlane16 then a permlane32 join), so no lane idles.
+// gamma = softmax(alpha + beta) over the workspace once both waves finish, one
+// row per 32-lane half.
 #include "kernels.h"
 #include "prof.h"
 
@@ -95,7 +97,9 @@ __device__ __forceinline__ void read_half(const float* v32, int i0, float (&v)[I
 
 // log-sum-exp of the lane's IH terms joined with the other half's (same result,
 // bit for bit, in both halves: the join is evaluated half 0 first in each)
-template <int IH>
+// NQ = 4 (K <= 16: 16 columns, the reduced axis in quarters): quarters 0+1 and 2+3 join first (xor16), then
+// the pairs (xor32), the lower group first in every join, so all lanes of a column hold the same bits
+template <int IH, int NQ = 2>
 __device__ __forceinline__ float lse_join(const float (&x)[IH], int h) {
   float m = x[0];
 #pragma unroll
@@ -104,6 +108,15 @@ __device__ __forceinline__ float lse_join(const float (&x)[IH], int h) {
   if (m != WNEG_INF) {
 #pragma unroll
     for (int k = 0; k < IH; ++k) s += __expf(x[k] - m);
+  }
+  if constexpr (NQ == 4) {
+    const float qm = xor16(m), qs = xor16(s);
+    const bool up = h & 1;
+    const float m0 = up ? qm : m, m1 = up ? m : qm, s0 = up ? qs : s, s1 = up ? s : qs;
+    const float mq = fmaxf(m0, m1);
+    s = mq == WNEG_INF ? 0.f : s0 * __expf(m0 - mq) + s1 * __expf(m1 - mq);
+    m = mq;
+    h >>= 1;
   }
   const float pm = xor32(m), ps = xor32(s);
   const float m0 = h ? pm : m, m1 = h ? m : pm, s0 = h ? ps : s, s1 = h ? s : ps;
@@ -214,7 +227,14 @@ __global__ __launch_bounds__(64) void viterbi_wide_kernel(const float* __restric
 
 // ------------------------------------------------------------ forward-backward
 // ws: alpha [B][T][K] then beta [B][T][K] (both in natural log, per-step shifted)
-template <int IH, int W, bool V4>
+// the max over the NQ lane groups of a column (exact: every lane gets the same value)
+template <int NQ>
+__device__ __forceinline__ float group_max(float m) {
+  if constexpr (NQ == 4) m = fmaxf(m, xor16(m));
+  return fmaxf(m, xor32(m));
+}
+
+template <int IH, int W, bool V4, int NQ>
 __global__ __launch_bounds__(128) void fwdbwd_wide_kernel(const float* __restrict__ log_pi,
                                                           const float* __restrict__ log_A,
                                                           const float* __restrict__ em,
@@ -223,7 +243,9 @@ __global__ __launch_bounds__(128) void fwdbwd_wide_kernel(const float* __restric
                                                           float* __restrict__ logZ, float* __restrict__ ws,
                                                           int dbg) {
   __shared__ __attribute__((aligned(16))) float vsh[2][2][32];  // [wave][parity][state]
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5, i0 = h * IH;
+  // lane (h, j): column j of COLS = 64 / NQ, reduced-axis group h (NQ = 4 for K <= 16: every lane busy)
+  constexpr int COLS = 64 / NQ;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, j = lane % COLS, h = lane / COLS, i0 = h * IH;
   const int64_t b = blockIdx.x;
   const int L = (int)wide_len(lengths, b, T);
   const float* A = log_A + b * (int64_t)T * K * K;
@@ -236,7 +258,7 @@ __global__ __launch_bounds__(128) void fwdbwd_wide_kernel(const float* __restric
     // ---------------------------------------------------------------- alpha
     float e0 = j < K ? E[j] : WNEG_INF;
 #pragma unroll
-    for (int o = 1; o < 32; o <<= 1) e0 = fmaxf(e0, __shfl_xor(e0, o));
+    for (int o = 1; o < COLS; o <<= 1) e0 = fmaxf(e0, __shfl_xor(e0, o));
     e0 = e0 == WNEG_INF ? 0.f : e0;
     float al = j < K ? log_pi[j] + (E[j] - e0) : WNEG_INF;
     if (h == 0) {
@@ -251,7 +273,7 @@ __global__ __launch_bounds__(128) void fwdbwd_wide_kernel(const float* __restric
       for (int s = 0; s < W; ++s) {
         float em = j < K ? ce[s] : WNEG_INF;
 #pragma unroll
-        for (int o = 1; o < 32; o <<= 1) em = fmaxf(em, __shfl_xor(em, o));
+        for (int o = 1; o < COLS; o <<= 1) em = fmaxf(em, __shfl_xor(em, o));
         em = em == WNEG_INF ? 0.f : em;
         ce[s] -= em;
         if (t0 + s < L) S += (double)em;
@@ -266,13 +288,13 @@ __global__ __launch_bounds__(128) void fwdbwd_wide_kernel(const float* __restric
         float mh = v[0];
 #pragma unroll
         for (int k = 1; k < IH; ++k) mh = fmaxf(mh, v[k]);
-        float M = fmaxf(mh, xor32(mh));
+        float M = group_max<NQ>(mh);
         M = M == WNEG_INF ? 0.f : M;
         S += (double)M;
         float x[IH];
 #pragma unroll
         for (int k = 0; k < IH; ++k) x[k] = (v[k] - M) + ca[s][k];
-        const float lse = lse_join<IH>(x, h);
+        const float lse = lse_join<IH, NQ>(x, h);
         al = j < K ? lse + ce[s] : WNEG_INF;
         if (h == 0) {
           vsh[0][t & 1][j] = al;
@@ -289,10 +311,10 @@ __global__ __launch_bounds__(128) void fwdbwd_wide_kernel(const float* __restric
     // logZ = S + LSE_j alpha_{L-1}(j)
     float mx = al;
 #pragma unroll
-    for (int o = 1; o < 32; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    for (int o = 1; o < COLS; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
     float ex = (j < K && mx != WNEG_INF) ? __expf(al - mx) : 0.f;
 #pragma unroll
-    for (int o = 1; o < 32; o <<= 1) ex += __shfl_xor(ex, o);
+    for (int o = 1; o < COLS; o <<= 1) ex += __shfl_xor(ex, o);
     if (lane == 0) logZ[b] = (float)(S + (double)mx + (double)__logf(ex));
   } else if (L > 0 && wave == 1 && !(dbg & 2)) {
     // ----------------------------------------------------------------- beta
@@ -313,12 +335,12 @@ __global__ __launch_bounds__(128) void fwdbwd_wide_kernel(const float* __restric
         float nh = w[0];
 #pragma unroll
         for (int k = 1; k < IH; ++k) nh = fmaxf(nh, w[k]);
-        float N = fmaxf(nh, xor32(nh));
+        float N = group_max<NQ>(nh);
         N = N == WNEG_INF ? 0.f : N;
         float x[IH];
 #pragma unroll
         for (int k = 0; k < IH; ++k) x[k] = ca[s][k] + (w[k] - N);
-        const float lse = lse_join<IH>(x, h);
+        const float lse = lse_join<IH, NQ>(x, h);
         bv = j < K ? lse : WNEG_INF;
         if (h == 0 && j < K) BE[(int64_t)(td - 1) * K + j] = bv;
       }
@@ -337,23 +359,24 @@ __global__ __launch_bounds__(128) void fwdbwd_wide_kernel(const float* __restric
   if (dbg & 1) return;  // timing experiment (profiling build, VQHMM_WIDE_DBG): no gamma pass
   // one row per 32-lane half (lane j = state j), four rows per pass: coalesced row reads and writes, the
   // softmax's max and sum as xor-shuffle trees inside the half
+  const int gj = lane & 31, gh = lane >> 5;
   for (int t0 = 0; t0 < T; t0 += 4) {
-    const int t = t0 + 2 * wave + h;  // half-uniform
+    const int t = t0 + 2 * wave + gh;  // half-uniform
     if (t >= T) continue;
     float* g = gamma + (b * (int64_t)T + t) * K;
     if (t >= L) {
-      if (j < K) g[j] = 0.f;
+      if (gj < K) g[gj] = 0.f;
       continue;
     }
-    const float x = j < K ? AL[(int64_t)t * K + j] + BE[(int64_t)t * K + j] : WNEG_INF;
+    const float x = gj < K ? AL[(int64_t)t * K + gj] + BE[(int64_t)t * K + gj] : WNEG_INF;
     float mx = x;
 #pragma unroll
     for (int o = 1; o < 32; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-    const float e = (j < K && mx != WNEG_INF) ? __expf(x - mx) : 0.f;
+    const float e = (gj < K && mx != WNEG_INF) ? __expf(x - mx) : 0.f;
     float sm = e;
 #pragma unroll
     for (int o = 1; o < 32; o <<= 1) sm += __shfl_xor(sm, o);
-    if (j < K) g[j] = mx == WNEG_INF ? 0.f : e / sm;
+    if (gj < K) g[gj] = mx == WNEG_INF ? 0.f : e / sm;
   }
 }
 
@@ -376,15 +399,15 @@ int launch_fwdbwd_wide(const float* log_pi, const float* log_A, const float* em,
   // VQHMM_WIDE_DBG (profiling build; results invalid): 1 no gamma pass, 2 no beta chain, 4 no alpha chain
   static const int dbg = prof_env("VQHMM_WIDE_DBG");
   const bool v4 = K % 4 == 0 && (reinterpret_cast<uintptr_t>(log_A) & 15) == 0;
-#define VQHMM_FBW(IHV, V4V)                                                                                       \
-  fwdbwd_wide_kernel<IHV, WHC, V4V><<<(unsigned)B, 128, 0, s>>>(log_pi, log_A, em, lengths, B, (int)K, (int)T, gamma, \
+#define VQHMM_FBW(IHV, V4V, NQV)                                                                                  \
+  fwdbwd_wide_kernel<IHV, WHC, V4V, NQV><<<(unsigned)B, 128, 0, s>>>(log_pi, log_A, em, lengths, B, (int)K, (int)T, gamma, \
                                                                 logZ, ws, dbg)
-  if (K <= 16) {
-    if (v4) VQHMM_FBW(8, true);
-    else VQHMM_FBW(8, false);
-  } else {
-    if (v4) VQHMM_FBW(16, true);
-    else VQHMM_FBW(16, false);
+  if (K <= 16) {  // 16 columns x 4 quarters of 4 reduced entries
+    if (v4) VQHMM_FBW(4, true, 4);
+    else VQHMM_FBW(4, false, 4);
+  } else {  // 32 columns x 2 halves of 16
+    if (v4) VQHMM_FBW(16, true, 2);
+    else VQHMM_FBW(16, false, 2);
   }
 #undef VQHMM_FBW
   VQHMM_LAUNCH_CHECK();
