@@ -3,10 +3,11 @@
 // contracts as hmm.hip (include/vqhmm.h, oracle/hmm_ref.py); the K <= 8 lane
 // maps there hold a whole K x K step block in one wave, which stops at K = 8.
 //
-// Lane map: one sequence per wave.  Lane l owns column j = l % 32 and the half
-// h = l / 32 of the reduced axis (IH = 8 for K <= 16, 16 for K <= 32 entries),
-// so a step is IH independent adds per lane, one permlane32 swap to join the
-// halves, and one LDS broadcast of the new 32-vector (no per-entry shuffles).
+// Lane map: one sequence per wave.  K <= 32: lane l owns column j = l % 32 and
+// the half h = l / 32 of the reduced axis (IH = 16 entries), one permlane32 swap
+// joins the halves; K <= 16: column j = l % 16 and the quarter h = l / 16 (IH =
+// 4), a permlane16 then a permlane32 join.  A step is IH independent adds per
+// lane and one LDS broadcast of the new vector (no per-entry shuffles).
 // The tables stream from HBM straight into registers one WHC-step chunk ahead
 // of the chain (for a fixed reduced index the 32 lanes of a half read one
 // contiguous row of log_A: coalesced).
@@ -19,8 +20,7 @@
 // step is a max-shifted log-sum-exp over the lane's IH terms, joined across the
 // halves, with the previous vector's max and the step's max emission subtracted
 // (their running sum is logZ's offset), so every stored value stays within a
-// step's spread of 0.  For K <= 16 its lanes are 16 columns x 4 quarters of the
-// reduced axis (IH = 4; a permlane16 then a permlane32 join), so no lane idles.
+// step's spread of 0.
 // gamma = softmax(alpha + beta) over the workspace once both waves finish, one
 // row per 32-lane half.
 #include "kernels.h"
@@ -129,7 +129,7 @@ __device__ __forceinline__ float lse_join(const float (&x)[IH], int h) {
 }  // namespace
 
 // --------------------------------------------------------------------- Viterbi
-template <int IH>
+template <int IH, int NQ>
 __global__ __launch_bounds__(64) void viterbi_wide_kernel(const float* __restrict__ log_pi,
                                                           const float* __restrict__ log_A,
                                                           const float* __restrict__ em,
@@ -139,7 +139,9 @@ __global__ __launch_bounds__(64) void viterbi_wide_kernel(const float* __restric
   __shared__ __attribute__((aligned(16))) float dsh[2][32];
   __shared__ uint32_t win[WWIN / 4 * 32];
   __shared__ int pbuf[WWIN];
-  const int lane = threadIdx.x, j = lane & 31, h = lane >> 5, i0 = h * IH;
+  // lane (h, j): column j of COLS = 64 / NQ, reduced-axis group h (NQ = 4 for K <= 16: every lane busy)
+  constexpr int COLS = 64 / NQ;
+  const int lane = threadIdx.x, j = lane % COLS, h = lane / COLS, i0 = h * IH;
   const int64_t b = blockIdx.x;
   const int L = (int)wide_len(lengths, b, T);
   int32_t* P = path + b * (int64_t)T;
@@ -173,10 +175,24 @@ __global__ __launch_bounds__(64) void viterbi_wide_kernel(const float* __restric
         const float v = dv[ii] + ca[s][ii];
         if (v > m) { m = v; arg = i0 + ii; }
       }
+      // join the groups, the lower one first (strict '>': its first max wins ties): quarters 0+1 and 2+3
+      // (permlane16), then the pairs (permlane32); every lane of a column ends with the same (max, arg)
+      int hh = h;
+      if constexpr (NQ == 4) {
+        const float qm = xor16(m);
+        const int qa = xor16(arg);
+        const bool hi = hh & 1;
+        const float q0 = hi ? qm : m, q1 = hi ? m : qm;
+        const int b0 = hi ? qa : arg, b1 = hi ? arg : qa;
+        const bool upq = q1 > q0;
+        m = upq ? q1 : q0;
+        arg = upq ? b1 : b0;
+        hh >>= 1;
+      }
       const float pm = xor32(m);
       const int pa = xor32(arg);
-      const float m0 = h ? pm : m, m1 = h ? m : pm;
-      const int a0 = h ? pa : arg, a1 = h ? arg : pa;
+      const float m0 = hh ? pm : m, m1 = hh ? m : pm;
+      const int a0 = hh ? pa : arg, a1 = hh ? arg : pa;
       const bool up = m1 > m0;
       d = (up ? m1 : m0) + ce[s];
       bpw |= (uint32_t)(up ? a1 : a0) << (8 * (t & 3));
@@ -197,7 +213,7 @@ __global__ __launch_bounds__(64) void viterbi_wide_kernel(const float* __restric
   float best = j < K ? d : WNEG_INF;
   int arg = j;
 #pragma unroll
-  for (int o = 1; o < 32; o <<= 1) {
+  for (int o = 1; o < COLS; o <<= 1) {
     const float ov = __shfl_xor(best, o);
     const int oa = __shfl_xor(arg, o);
     if (ov > best || (ov == best && oa < arg)) { best = ov; arg = oa; }
@@ -384,12 +400,12 @@ size_t viterbi_wide_ws_bytes(int64_t B, int64_t T) { return (size_t)B * (size_t)
 
 int launch_viterbi_wide(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths, int64_t B,
                         int64_t T, int64_t K, int32_t* path, float* score, void* ws, hipStream_t s) {
-  if (K <= 16)
-    viterbi_wide_kernel<8><<<(unsigned)B, 64, 0, s>>>(log_pi, log_A, em, lengths, (int)K, (int)T, path, score,
-                                                      (uint32_t*)ws);
-  else
-    viterbi_wide_kernel<16><<<(unsigned)B, 64, 0, s>>>(log_pi, log_A, em, lengths, (int)K, (int)T, path, score,
-                                                       (uint32_t*)ws);
+  if (K <= 16)  // 16 columns x 4 quarters of 4 reduced entries
+    viterbi_wide_kernel<4, 4><<<(unsigned)B, 64, 0, s>>>(log_pi, log_A, em, lengths, (int)K, (int)T, path, score,
+                                                         (uint32_t*)ws);
+  else  // 32 columns x 2 halves of 16
+    viterbi_wide_kernel<16, 2><<<(unsigned)B, 64, 0, s>>>(log_pi, log_A, em, lengths, (int)K, (int)T, path, score,
+                                                          (uint32_t*)ws);
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
 }
