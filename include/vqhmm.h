@@ -136,8 +136,8 @@ int vqhmm_fwdbwd_f32(const float* log_pi, const float* log_A, const float* em, c
  * loss: device fp32 scalar; loss_accum (nullable): device fp64 scalar += loss
  *   (train_model's epoch_loss, :158, without a per-step host sync).
  * need_grad = 0 computes only the loss; 2 = as 1, but the loss (and loss_accum) are left to the
- *   backward: vqhmm_elbo_bwd_adam_f32 with its loss pointers finalizes them in its own last
- *   launches (one launch fewer per step).
+ *   backward: vqhmm_elbo_bwd_adam_f32 or vqhmm_elbo_bwd_loss_f32 with its loss pointers finalizes
+ *   them in its own last launch (one launch fewer per step).
  * norm: NULL, or a device int64[2] {valid_count, batch} replacing the batch's own
  *   loss normalisers mask.sum() (:120) and B (:131, :135).  Pass the GLOBAL batch's
  *   values when this batch is one shard of it: the shards' losses and gradients then
@@ -153,6 +153,13 @@ int vqhmm_elbo_fwd_f32(const vqhmm_dims_t* dims, const float* const* params, con
 int vqhmm_elbo_bwd_f32(const vqhmm_dims_t* dims, const float* const* params, const float* x,
                        const int64_t* norm, int64_t B, int64_t T, float beta, const float* grad_scale,
                        void* workspace, size_t ws_bytes, float* grad, void* stream);
+/* vqhmm_elbo_bwd_f32 that also finalizes the loss of a forward run with need_grad = 2 into loss /
+ * loss_accum (the data-parallel step form: forward + backward, then the gradient all-reduce and
+ * vqhmm_adam_f32; VQ_VAE_HMM_fixed.py:137,156,158). */
+int vqhmm_elbo_bwd_loss_f32(const vqhmm_dims_t* dims, const float* const* params, const float* x,
+                            const int64_t* norm, int64_t B, int64_t T, float beta, const float* grad_scale,
+                            void* workspace, size_t ws_bytes, float* grad, float* loss, double* loss_accum,
+                            void* stream);
 /* Backward + torch.optim.Adam step (the single-process train_model step,
  * VQ_VAE_HMM_fixed.py:155-157): vqhmm_elbo_bwd_f32 (grad_scale NULL) whose last launch
  * also applies vqhmm_adam_f32's update to every parameter element (same formula, same

@@ -215,8 +215,10 @@ def test_strip_forward_matches_pair_launches(tmp_path, dims, bt):
                                      ((5, 64, 3, 32), (256, 150))])
 def test_strip_backward_matches_pair_launches(tmp_path, dims, bt):
     """The backward's data-gradient convolutions (to_params -> dec_conv2 -> dec_conv1 + softmax backward
-    + to_logits -> enc_conv2) as ONE strip launch against the pair launches (VQHMM_STRIP_BWD=0): same bits."""
-    _run_both(tmp_path, "VQHMM_STRIP_BWD", dims, bt)
+    + to_logits -> enc_conv2) as ONE strip launch against the pair launches (VQHMM_STRIP_BWD=0): same bits
+    (the weight gradients as the grouped launch in both: folded into the strip they sum in another order,
+    test_strip_wgrad_fold_*)."""
+    _run_both(tmp_path, "VQHMM_STRIP_BWD", dims, bt, {"VQHMM_STRIP_WGRAD": "0"})
 
 
 _HEAD_RUN = r"""
@@ -248,12 +250,9 @@ torch.save(out, sys.argv[2])
 """
 
 
-@pytest.mark.parametrize("dims,bt", [((5, 64, 3, 32, 128), (96, 150)), ((4, 64, 2, 16, 64), (40, 77)),
-                                     ((5, 64, 4, 32, 128), (256, 150))])
-def test_strip_head_matches_head_launch(tmp_path, dims, bt):
-    """The ELBO head fused into the forward strip launch (VQHMM_STRIP_HEAD=1, an A/B switch; its slabs / loss
-    partials per strip workgroup) against the head's own launch: per-row outputs feed the same backward, the
-    loss and the gradient differ only in the slab / partial summation order (1e-6 relative)."""
+def _run_both_tol(tmp_path, env, dims, bt):
+    """_HEAD_RUN in two fresh processes, env=1 and env=0: losses within 1e-6 relative, gradients within
+    1e-6 normwise (the two forms differ only in a summation order)."""
     import os
     import subprocess
     import sys
@@ -263,7 +262,7 @@ def test_strip_head_matches_head_launch(tmp_path, dims, bt):
     for flag in ("1", "0"):
         f = str(tmp_path / f"h{flag}.pt")
         subprocess.run([sys.executable, "-c", _HEAD_RUN, pkg, f, ",".join(map(str, dims)), ",".join(map(str, bt))],
-                       check=True, timeout=300, env=dict(os.environ, VQHMM_STRIP_HEAD=flag))
+                       check=True, timeout=300, env=dict(os.environ, **{env: flag}))
         out[flag] = torch.load(f, weights_only=True)
     for k in ("loss0", "loss1", "mloss"):
         a, b = out["1"][k].double(), out["0"][k].double()
@@ -271,6 +270,29 @@ def test_strip_head_matches_head_launch(tmp_path, dims, bt):
     for k in ("grad0", "grad1", "mgrad"):
         a, b = out["1"][k].double(), out["0"][k].double()
         assert (a - b).norm() <= 1e-6 * b.norm(), (k, ((a - b).norm() / b.norm()).item())
+    return out
+
+
+@pytest.mark.parametrize("dims,bt", [((5, 64, 3, 32, 128), (96, 150)), ((4, 64, 2, 16, 64), (40, 77)),
+                                     ((5, 64, 4, 32, 128), (256, 150))])
+def test_strip_head_matches_head_launch(tmp_path, dims, bt):
+    """The ELBO head fused into the forward strip launch (VQHMM_STRIP_HEAD=1, an A/B switch; its slabs / loss
+    partials per strip workgroup) against the head's own launch: per-row outputs feed the same backward, the
+    loss and the gradient differ only in the slab / partial summation order (1e-6 relative)."""
+    _run_both_tol(tmp_path, "VQHMM_STRIP_HEAD", dims, bt)
+
+
+@pytest.mark.parametrize("dims,bt", [((5, 64, 3, 32, 128), (96, 150)), ((3, 64, 2, 32, 64), (40, 77)),
+                                     ((5, 64, 4, 31, 128), (8, 50)), ((4, 64, 3, 29, 128), (30, 200)),
+                                     ((5, 64, 3, 32, 128), (128, 200)),   # the cfg2 N = 8 shard: 249 strips of 104
+                                     ((5, 64, 3, 32, 128), (256, 150))])  # 512 strips: two per workgroup
+def test_strip_wgrad_fold_matches_grouped(tmp_path, dims, bt):
+    """The six weight gradients folded into the backward strip launch (strip_bwdw.hip, the default below 2^17
+    rows) against the grouped weight-gradient launch (VQHMM_STRIP_WGRAD=0): the data-gradient chain is the
+    same code, the weight / bias gradients sum per strip workgroup instead of per row chunk, so loss and
+    gradients agree within 1e-6 (and every step's gradient against the oracle: test_strong_scaling_shards_*)."""
+    out = _run_both_tol(tmp_path, "VQHMM_STRIP_WGRAD", dims, bt)
+    assert torch.equal(out["1"]["loss0"], out["0"]["loss0"])  # the forward is untouched
 
 
 def test_tail_rerun_after_one_forward_is_identical():

@@ -97,6 +97,16 @@ bool strip_head_on() {
   }();
   return on && strip_fwd_env();
 }
+// VQHMM_STRIP_WGRAD=0: the backward strip without the weight gradients (they then run as the grouped
+// wgrad2 launch), A/B switch read once.  The fold sums each weight gradient in another order (per strip
+// workgroup instead of per row chunk), so the two forms agree within rounding, not bit for bit
+bool strip_wgrad_env() {
+  static const bool on = [] {
+    const char* e = VQHMM_ENV("VQHMM_STRIP_WGRAD");
+    return !e || atoi(e) != 0;
+  }();
+  return on;
+}
 // the shapes the forward strip covers (strip_fwd_supported on the plan's ConvArgs agrees)
 bool strip_fwd_shapes_ok(int D, int H, int H2, int K, int64_t R) {
   return D >= 1 && 3 * D <= 16 && H == 64 && H2 >= 1 && H2 <= 32 && K >= 1 && K <= 4 && R > 0 && R < (1ll << 31);
@@ -144,6 +154,8 @@ struct ElboPlan {
                          // launch that also Adam-updates them (tail: E; compose_adam: both; Wcopy null when grouped)
   float* himg;           // the cooperative head's weight image (built by the prologue), or null
   bool wgroup;           // the six weight gradients run as one grouped launch (wgrad2_group)
+  bool wfold;            // ... or inside the backward strip launch (strip_bwdw.hip; slabs = its workgroups).
+                         // Either way the tail sees the grouped layout (composed segment + dE shares)
   int nwl;
   WLayer wl[8];  // 0 to_params, 1 dec2, 2 dec1', 3 to_logits, 4 enc2, 5 enc1, [6 Prior W1, 7 Prior W2]
   float* img[32];  // per stage: packed conv2_kernel weight image (WImgJob), built by the prologue, or null
@@ -151,6 +163,7 @@ struct ElboPlan {
 };
 
 void plan_images(ElboPlan& p, Carver& c);
+bool strip_wfold_planned(const ElboPlan& p);
 
 ElboPlan plan_elbo(const vqhmm_dims_t* d, int64_t B, int64_t T, void* ws) {
   // size / shape queries: carve from a non-null base (kernel choices test pointers for presence;
@@ -238,7 +251,9 @@ ElboPlan plan_elbo(const vqhmm_dims_t* d, int64_t B, int64_t T, void* ws) {
   // the grouped path's tail forms the composed dW itself (a block reduces <= 256 dWc columns)
   p.wgroup = p.wgroup && composed_block_cols(H, K) <= 256;
   p.Wcopy = p.wgroup ? nullptr : c.take<float>((size_t)H * H * 3);
-  p.dec2_split = p.wgroup && wgrad_split_on() && H == 64;
+  plan_images(p, c);
+  p.wfold = p.wgroup && strip_wfold_planned(p);
+  p.dec2_split = p.wgroup && !p.wfold && wgrad_split_on() && H == 64;
   for (int i = 0; i < p.nwl; ++i) {
     WLayer& w = p.wl[i];
     w.N = shapes[i][0]; w.C = shapes[i][1]; w.ks = shapes[i][2];
@@ -248,12 +263,12 @@ ElboPlan plan_elbo(const vqhmm_dims_t* d, int64_t B, int64_t T, void* ws) {
     w.rows = (w.N <= 64 && w.C <= 64) ? wgrad2_rows(R, w.N, w.C, w.ks)
              : wgradbig_supported(probe) ? wgradbig_rows(R, w.N, w.C) : wgrad_chunks(R, tiles);
     if (i < 6 && p.wgroup) w.rows = wgrad2_group_rows(std::max<int64_t>(w.rows, wgroup_min_rows()), w.N, w.C, w.ks);
-    w.nchunks = cdiv(R, w.rows);
+    if (i < 6 && p.wfold) w.rows = cdiv(R, strip_bwdw_grid(R));  // one slab row per strip workgroup
+    w.nchunks = (i < 6 && p.wfold) ? strip_bwdw_grid(R) : cdiv(R, w.rows);
     w.slab = c.take<float>((size_t)w.nchunks * w.N * w.C * w.ks);
     w.bslab = c.take<float>((size_t)w.nchunks * w.N);
     w.cslab = (i == 2 && p.wgroup) ? c.take<float>((size_t)w.nchunks * K * H) : nullptr;
   }
-  plan_images(p, c);
   p.bytes = c.off + 256;
   return p;
 }
@@ -652,6 +667,15 @@ bool strip_bwd_on(const ElboPlan& p) {
                              conv_of(p, nullptr, S_ENC2_DG));
 }
 
+// The six weight gradients folded into the backward strip launch (strip_bwdw.hip): wherever the backward
+// strip runs and its packed-tap weight-gradient tiles apply (D <= 5, K <= 4); VQHMM_STRIP_WGRAD=0 keeps the
+// grouped launch
+bool strip_wfold_planned(const ElboPlan& p) {
+  return strip_wgrad_env() && strip_bwd_on(p) &&
+         strip_bwdw_supported(conv_of(p, nullptr, S_PAR_DG), conv_of(p, nullptr, S_DEC2_DG), dec1_dg_args(p, nullptr, nullptr),
+                              conv_of(p, nullptr, S_ENC2_DG), p.D);
+}
+
 // VQHMM_TAIL_FUSED=0 (grouped weight gradients): the tail without Adam, then the Adam launch (A/B; the
 // same bits); read once
 bool tail_fused_on() {
@@ -661,6 +685,12 @@ bool tail_fused_on() {
   }();
   return v;
 }
+
+// The Adam step counter of the fused tail (tail_kernel<true> applies Adam with the count some earlier launch of
+// the same backward advanced: the grouped weight-gradient launch or the folded backward strip, workgroup 0), or
+// null.  The one place that decides it, for the launch that advances the counter and the tail that applies it.
+bool tail_applies_adam(const ElboPlan& p, const StepCtx& c) { return c.adam && p.wgroup && tail_fused_on(); }
+int64_t* adam_step_inc(const ElboPlan& p, const StepCtx& c) { return tail_applies_adam(p, c) ? c.adam->step : nullptr; }
 
 HeadArgs head_args(const ElboPlan& p, const StepCtx& c) {
   const float* const* w = c.w;
@@ -725,6 +755,18 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       if (strip_bwd_on(p)) {
         ConvArgs pd = conv_of(p, w, S_PAR_DG);
         pd.scale = c.gscale;  // dpar is the head's gradient for dloss = 1
+        if (p.wfold) {  // + all six weight gradients (slab row per workgroup); advances the fused tail's Adam step
+          StripWgradArgs sw{};
+          sw.x = p.xp; sw.cmpW = w[DEC1_W];
+          for (int i = 0; i < 6; ++i) {
+            sw.slab[i] = p.wl[i].slab;
+            sw.bslab[i] = p.wl[i].bslab;
+          }
+          sw.cslab = p.wl[2].cslab;
+          sw.D = p.D; sw.K = p.K; sw.H2 = p.H2;
+          sw.step_inc = adam_step_inc(p, c);
+          return launch_strip_bwdw(pd, conv_of(p, w, S_DEC2_DG), dec1_dg_args(p, w, c.gscale), conv_of(p, w, st), sw, s);
+        }
         return launch_strip_bwd(pd, conv_of(p, w, S_DEC2_DG), dec1_dg_args(p, w, c.gscale), conv_of(p, w, st), s);
       }
       if (bwd_pair_fused(p, w, c.gscale))
@@ -760,6 +802,7 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       if (logits_bwd_fused(p)) return VQHMM_OK;  // ran in S_DEC1_DG's epilogue
       return launch_logits_bwd(p.q, p.dqd, p.dqx, p.dlx, c.gscale, p.R, p.K, p.dlog, s);
     case S_W_PAR: case S_W_DEC2: case S_W_DEC1: case S_W_LOGIT: case S_W_ENC2: case S_W_ENC1: {
+      if (p.wfold) return VQHMM_OK;  // in S_ENC2_DG's backward strip launch
       WgradArgs wa[6];
       wgrad_jobs(p, w, wa);
       if (p.wgroup) {  // all six in S_W_ENC1's launch (every dY is ready by then, in any stage order)
@@ -774,10 +817,10 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
           int n = 0;
           for (int i = 0; i < 6; ++i)
             if (jmask >> i & 1) sel[n++] = wa[i];
-          return n ? launch_wgrad2_group(sel, n, s, c.adam && tail_fused_on() ? c.adam->step : nullptr) : VQHMM_OK;
+          return n ? launch_wgrad2_group(sel, n, s, adam_step_inc(p, c)) : VQHMM_OK;
         }
         // the fused tail applies Adam without a completion ticket: this launch advances the step counter
-        int64_t* step_inc = c.adam && tail_fused_on() ? c.adam->step : nullptr;
+        int64_t* step_inc = adam_step_inc(p, c);
         if (p.dec2_split) {
           WgradArgs sp[7];
           int n = 0;
@@ -817,7 +860,7 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
         if (tail_fused_on()) {  // slab reduction (+ Adam on each reduced column) in one launch
           TailArgs ta{};
           make_tail(p, c, ta);
-          return launch_tail(ta, c.adam, c.g, s);
+          return launch_tail(ta, tail_applies_adam(p, c) ? c.adam : nullptr, c.g, s);
         }
         if (!c.adam) return VQHMM_OK;
         const AdamArgs& ad = *c.adam;
@@ -915,6 +958,18 @@ int vqhmm_elbo_bwd_f32(const vqhmm_dims_t* d, const float* const* w, const float
   return VQHMM_OK;
 }
 
+int vqhmm_elbo_bwd_loss_f32(const vqhmm_dims_t* d, const float* const* w, const float* x, const int64_t* norm,
+                            int64_t B, int64_t T, float beta, const float* grad_scale, void* ws, size_t ws_bytes,
+                            float* g, float* loss, double* loss_accum, void* stream) {
+  if (!dims_ok(d) || !w || B <= 0 || T <= 0 || !x || !ws || !g || !loss) return VQHMM_EINVAL;
+  ElboPlan p = plan_elbo(d, B, T, ws);
+  if (ws_bytes < p.bytes) return VQHMM_EWORKSPACE;
+  StepCtx c{w, x, nullptr, 0, nullptr, norm, beta, 1, loss, loss_accum, grad_scale, g, nullptr};
+  for (int st = BWD_FIRST; st <= BWD_LAST; ++st)  // the tail launch finalizes the loss (make_tail: c.loss)
+    if (int rc = run_stage(p, c, st, (hipStream_t)stream)) return rc;
+  return VQHMM_OK;
+}
+
 int vqhmm_elbo_bwd_adam_f32(const vqhmm_dims_t* d, const float* const* w, const float* x, const int64_t* norm,
                             int64_t B, int64_t T, float beta, void* ws, size_t ws_bytes, float* g, float* param,
                             float* exp_avg, float* exp_avg_sq, double lr, double beta1, double beta2, double eps,
@@ -959,9 +1014,11 @@ int vqhmm_elbo_stage_info(const vqhmm_dims_t* d, int64_t B, int64_t T, int stage
                           : "strip_fwd(enc_conv1+enc_conv2+to_logits+dec_conv1+dec_conv2+to_params)";
     if (p.strip_head && stage == S_HEAD) nm = "(elbo_head: in strip_fwd)";
     if (in_bstrip)
-      nm = stage == S_ENC2_DG ? "strip_bwd(to_params_dgrad+dec_conv2_dgrad+dec_conv1_dgrad+logits_bwd+to_logits_dgrad+enc_conv2_dgrad)"
-                              : "(in strip_bwd)";
-    if (p.wgroup && stage == S_W_ENC1) nm = "wgrad_group(all 6 weight gradients)";
+      nm = stage != S_ENC2_DG ? "(in strip_bwd)"
+           : p.wfold ? "strip_bwdw(to_params_dgrad+dec_conv2_dgrad+dec_conv1_dgrad+logits_bwd+to_logits_dgrad+enc_conv2_dgrad+6 wgrads)"
+                     : "strip_bwd(to_params_dgrad+dec_conv2_dgrad+dec_conv1_dgrad+logits_bwd+to_logits_dgrad+enc_conv2_dgrad)";
+    if (p.wfold && stage >= S_W_PAR && stage <= S_W_ENC1) nm = "(wgrad: in strip_bwdw)";
+    else if (p.wgroup && stage == S_W_ENC1) nm = "wgrad_group(all 6 weight gradients)";
     else if (p.wgroup && stage >= S_W_PAR && stage < S_W_ENC1) nm = "(wgrad: in wgrad_group)";
     else if (in_strip || in_bstrip || (p.strip_head && stage == S_HEAD)) {
     } else if (fused_front && (stage == S_ENC1 || stage == S_DEC1 || stage == S_PAR_DG))
@@ -1013,9 +1070,22 @@ int vqhmm_elbo_stage_info(const vqhmm_dims_t* d, int64_t B, int64_t T, int stage
         f += f1;
       }
       const double R = (double)p.R;
-      b = 4.0 * R * (ld4(2 * p.D) + 3 * ld4(p.H) + 3 * ld4(p.K) + ld4(p.H2) +          // dpar, g2, g1, h1, q, dqx, dlx, h2
-                     2 * ld4(p.H) + 2 * ld4(p.K) + ld4(p.H2) + ld4(p.H));             // dg2, dg1, dqd, dlog, dh2, dh1
+      if (!p.wfold) {
+        b = 4.0 * R * (ld4(2 * p.D) + 3 * ld4(p.H) + 3 * ld4(p.K) + ld4(p.H2) +          // dpar, g2, g1, h1, q, dqx, dlx, h2
+                       2 * ld4(p.H) + 2 * ld4(p.K) + ld4(p.H2) + ld4(p.H));             // dg2, dg1, dqd, dlog, dh2, dh1
+      } else {  // + the six weight gradients: x in, the dY never leave the chip, one slab row per workgroup out
+        double fw, bw;
+        int mw;
+        stage_work(p, S_W_ENC1, &fw, &bw, &mw);
+        f += fw;
+        b = 4.0 * R * (ld4(2 * p.D) + 3 * ld4(p.H) + 3 * ld4(p.K) + ld4(p.H2) + ld4(p.D));
+        for (int i = 0; i < 6; ++i)
+          b += 4.0 * p.wl[i].nchunks * ((double)p.wl[i].N * p.wl[i].C * p.wl[i].ks + p.wl[i].N);
+        b += 4.0 * p.wl[2].nchunks * (double)p.K * p.H;
+      }
     }
+  } else if (p.wfold && stage >= S_W_PAR && stage <= S_W_ENC1) {
+    f = 0; b = 0;  // counted with the backward strip
   } else if (fused_front && pair_of != stage) {
     f = 0; b = 0;  // counted with the launch it runs in
   } else if (fused_front) {
@@ -1112,6 +1182,7 @@ int vqhmm_debug_prof(int which, uint64_t* out, int64_t n) {
     case 0: return strip_prof_copy(out, n);
     case 1: return conv2_prof_copy(out, n);
     case 2: return head_prof_copy(out, n);
+    case 3: return bwdw_prof_copy(out, n);
   }
   return VQHMM_EINVAL;
 }

@@ -25,10 +25,10 @@
 #define VQHMM_STATUS_TAIL_TIMEOUT 1ull  // reserved (include/vqhmm.h): no kernel sets it
 
 // Environment knobs.  VQHMM_ENV: the A/B switches the release library honours, each choosing between
-// launch paths the tests prove bit-identical (or, VQHMM_STRIP_HEAD / VQHMM_HEAD, equal within the
-// stated tolerance).  VQHMM_PROF_ENV: tuning and timing experiments that change summation orders,
-// skip work or invalidate results; they exist only in the profiling build (`make PROFILING=1` ->
-// vqhmm/libvqhmm_prof.so, loaded with VQHMM_LIB_PATH).  In the release build the name never reaches
+// launch paths the tests prove bit-identical (or equal within the
+// stated tolerance: VQHMM_STRIP_HEAD, VQHMM_STRIP_WGRAD, VQHMM_HEAD).  VQHMM_PROF_ENV: tuning and timing
+// experiments that change summation orders, skip work or invalidate results; they exist only in the profiling
+// build (`make prof` -> vqhmm/libvqhmm_prof.so, loaded with VQHMM_LIB_PATH).  In the release build the name never reaches
 // the binary and the knob reads as unset.
 #define VQHMM_ENV(name) getenv(name)
 #ifdef VQHMM_PROFILING

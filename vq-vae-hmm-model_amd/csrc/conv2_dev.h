@@ -148,6 +148,8 @@ __device__ __forceinline__ void c2_mfma_pk(const float* Ws, const float* Xw, int
 // rows xs_q + l16 * xs_q_ld (channels c0 < xs_q_ld).
 // TB = 2: a second 16-channel tail block (channels 16 .. C2-1, C2 <= 32: to_params at D <= 16) with
 // weights tw2 / bias tb1; no softmax outputs then.
+// xs_dl (ACT 3, strip_bwdw): the row's softmax-backward output dl[0..3] also goes to LDS row xs_dl + 8 l16
+// (zeros for rows outside [0, R)).
 template <int NB, int PB, int ACT, int TB = 1>
 __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a, int64_t m0, int wave, int lg4, int l16,
                                                f32x4 (&acc)[NB][PB], const float4 (&auxv)[NB][PB],
@@ -155,7 +157,7 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a, int64_t m0, in
                                                f32x4 tb0, float sc, bool tail, int rlo = 0, int rhi = 16,
                                                float* xs_dh = nullptr, int xs_ld = 0,
                                                const float (*tw2)[4] = nullptr, f32x4 tb1 = f32x4{0.f, 0.f, 0.f, 0.f},
-                                               float* xs_q = nullptr, int xs_q_ld = 0) {
+                                               float* xs_q = nullptr, int xs_q_ld = 0, float* xs_dl = nullptr) {
   // lane (lg4, l16) holds channels nb*16 + 4*lg4 + v of row m0 + (wave*PB+pb)*16 + l16
   const bool own = l16 >= rlo && l16 < rhi;
 #pragma unroll
@@ -223,6 +225,7 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a, int64_t m0, in
                 for (int v = 0; v < 4; ++v) o4[v] = lg4 == 0 ? dl[v] : dl[(4 + v) % KM];
                 *reinterpret_cast<f32x4*>(a.lb_dlog + r * KM + 4 * lg4) = o4;
               }
+              if (xs_dl && lg4 == 0) *reinterpret_cast<f32x4*>(xs_dl + l16 * 8) = f32x4{dl[0], dl[1], dl[2], dl[3]};
               if (a.lb_dh) {
                 // dh[r][c] = (h[r][c] > 0) * sum_k W[k][c] dl[k]: to_logits (1x1, K -> C) dgrad with the
                 // ReLU mask of its input h, the same k-ordered fma chain as the MFMA path; lane group
@@ -244,10 +247,13 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a, int64_t m0, in
                   if (xs_dh) *reinterpret_cast<f32x4*>(xs_dh + l16 * xs_ld + c0) = o;
                 }
               }
-            } else if (xs_dh && a.lb_dh) {  // rows outside [0, R): the zero padding of the next conv
-              const int L = ld4(a.lb_C), per = L / 4;
-              for (int c0 = lg4 * per; c0 < (lg4 + 1) * per; c0 += 4)
-                *reinterpret_cast<f32x4*>(xs_dh + l16 * xs_ld + c0) = f32x4{0.f, 0.f, 0.f, 0.f};
+            } else {
+              if (xs_dh && a.lb_dh) {  // rows outside [0, R): the zero padding of the next conv
+                const int L = ld4(a.lb_C), per = L / 4;
+                for (int c0 = lg4 * per; c0 < (lg4 + 1) * per; c0 += 4)
+                  *reinterpret_cast<f32x4*>(xs_dh + l16 * xs_ld + c0) = f32x4{0.f, 0.f, 0.f, 0.f};
+              }
+              if (xs_dl && lg4 == 0) *reinterpret_cast<f32x4*>(xs_dl + l16 * 8) = f32x4{0.f, 0.f, 0.f, 0.f};
             }
           }
         }

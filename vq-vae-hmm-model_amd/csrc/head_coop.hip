@@ -189,6 +189,9 @@ __global__ __launch_bounds__(256, 2) void elbo_head_coop_kernel(HeadArgs a) {
     for (int k = 0; k < K; ++k) s += __expf(a.log_prior[k] - m);
     if (si < K) lp_i = a.log_prior[si] - (m + __logf(s));
   }
+  // the weight image's LDS DMA is complete before the barrier publishes it (its writes are not covered by the
+  // compiler's own wait insertion for LDS stores)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (!a.norm && !a.cnt_in) {  // valid positions of the batch (mask.sum(), :120)
     unsigned c = 0;
@@ -688,6 +691,7 @@ __global__ __launch_bounds__(768, 1) void elbo_head_pipe_kernel(HeadArgs a) {
     if (si < K) lp_i = a.log_prior[si] - (m + __logf(s));
   }
   if (!mw && nloc > 0) write_u(0, u0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the weight image's LDS DMA, as in elbo_head_coop_kernel
   __syncthreads();
   if (!a.norm && !a.cnt_in) {
     unsigned c = 0;

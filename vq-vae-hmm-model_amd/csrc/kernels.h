@@ -252,10 +252,30 @@ int launch_strip_fwd(const ConvArgs& e1, const ConvArgs& e2, const ConvArgs& d1,
 // f = dec_conv1's ACT 3 args with lb_dh; H = 64, H2 in (16, 32], K <= 4, 2D <= 16)
 bool strip_bwd_supported(const ConvArgs& pd, const ConvArgs& d2, const ConvArgs& f, const ConvArgs& e2);
 int launch_strip_bwd(const ConvArgs& pd, const ConvArgs& d2, const ConvArgs& f, const ConvArgs& e2, hipStream_t s);
+// The backward strip with the six weight gradients folded in (strip_bwdw.hip): the same four ConvArgs plus
+// the X operands the chain does not carry and one slab row per workgroup for every layer (S_W_PAR .. S_W_ENC1
+// order, wgrad2's [chunk][N][C][ks] / [chunk][N] layouts; chunk = workgroup, strip_bwdw_grid(R) of them);
+// D <= 5, K <= 4 (packed-tap enc_conv1 / dec_conv1 weight gradients)
+struct StripWgradArgs {
+  const float* x;        // PCL (R, ld4(D)): enc_conv1's input
+  const float* cmpW;     // decoder.conv1.weight (H, H, 3): the composed layer's dE shares
+  float* slab[6];
+  float* bslab[6];
+  float* cslab;          // [grid][K][H]
+  int D, K, H2;
+  int64_t* step_inc;     // non-null: workgroup 0 advances the fused tail's Adam step counter
+  int store;             // 1: also store dg2 / dg1 / dh1 (the separate launches' dY; never needed by the step)
+};
+bool strip_bwdw_supported(const ConvArgs& pd, const ConvArgs& d2, const ConvArgs& f, const ConvArgs& e2, int D);
+int strip_bwdw_own(int64_t R);
+int strip_bwdw_grid(int64_t R);
+int launch_strip_bwdw(const ConvArgs& pd, const ConvArgs& d2, const ConvArgs& f, const ConvArgs& e2,
+                      const StripWgradArgs& w, hipStream_t s);
 // phase stamps of the last profiled launch (prof.h): strip.hip (VQHMM_STRIP_PROF), conv2.hip (VQHMM_CONV_PROF)
 int strip_prof_copy(uint64_t* out, int64_t n);
 int conv2_prof_copy(uint64_t* out, int64_t n);
 int head_prof_copy(uint64_t* out, int64_t n);  // head_coop.hip (VQHMM_HEAD_PROF)
+int bwdw_prof_copy(uint64_t* out, int64_t n);  // strip_bwdw.hip (VQHMM_STRIP_PROF)
 int launch_wgrad(const WgradArgs& a, hipStream_t s);
 bool wgradbig_supported(const WgradArgs& a);
 int64_t wgradbig_rows(int64_t R, int N, int C);

@@ -10,6 +10,8 @@
 //   prologue         x, u -> PCL + compose_fwd in one launch (the step's first stage)
 //   logits_bwd       softmax backward of q = softmax(logits) (:114) + entropy's direct term
 //   adam             torch.optim.Adam update (defaults of train_model, :146)
+#include <algorithm>
+
 #include "kernels.h"
 
 namespace vqhmm {
@@ -32,14 +34,21 @@ __device__ __forceinline__ AdamElem adam_load(const AdamArgs& a, int64_t i, int6
   e.p = a.p[i];
   return e;
 }
-__device__ __forceinline__ void adam_apply(const AdamArgs& a, int64_t i, float g, const AdamElem& e) {
+struct AdamOut {
+  float m, v, p;
+};
+__device__ __forceinline__ AdamOut adam_elem(const AdamArgs& a, float g, const AdamElem& e) {
   const float gi = g * a.gmul;
   const float mi = e.m + (float)(1.0 - a.b1) * (gi - e.m);
   const float vi = e.v * (float)a.b2 + (float)(1.0 - a.b2) * gi * gi;
-  a.m[i] = mi;
-  a.v[i] = vi;
   const float denom = sqrtf(vi) / e.bc2s + (float)a.eps;
-  a.p[i] = e.p + (-e.step_size) * (mi / denom);
+  return AdamOut{mi, vi, e.p + (-e.step_size) * (mi / denom)};
+}
+__device__ __forceinline__ void adam_apply(const AdamArgs& a, int64_t i, float g, const AdamElem& e) {
+  const AdamOut o = adam_elem(a, g, e);
+  a.m[i] = o.m;
+  a.v[i] = o.v;
+  a.p[i] = o.p;
 }
 // The step counter advances inside the update's own launch: every workgroup read
 // t = (*step & 0xffffffff) + 1 at its start, then takes a ticket in the upper 32 bits here; the
@@ -555,14 +564,43 @@ __device__ void log_prior_grad_body(const LogPriorGradArgs& a) {
 // 32 bits; the last workgroup to do so (all reads are behind it) stores t with a
 // zero ticket.  Between launches *step is the plain step count.  gmul scales the
 // gradient first (1/world_size after a SUM all-reduce).
+// Each thread takes float4 groups of all four buffers (vec: every pointer 16-byte aligned) strided over a
+// grid of ~n / 1024 workgroups, and forms the bias corrections once (adam_load's expressions, so the same
+// bits as the tail's fused update); the elements past the last whole group (and everything when !vec) go
+// one per thread.  Few workgroups: few tickets on the step counter.
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, int64_t n,
                                                    double lr, double b1, double b2, double eps, int64_t* step,
-                                                   float gmul) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+                                                   float gmul, int vec) {
   const int64_t tn = (*step & 0xffffffffll) + 1;
   const AdamArgs a{p, m, v, step, lr, b1, b2, eps, gmul};
-  if (i < n) adam_apply(a, i, g[i], adam_load(a, i, tn));
+  AdamElem e;
+  {
+    const double t = (double)tn;
+    e.step_size = (float)(a.lr / (1.0 - pow(a.b1, t)));
+    e.bc2s = (float)sqrt(1.0 - pow(a.b2, t));
+  }
+  const int64_t stride = (int64_t)gridDim.x * 256, n4 = vec ? n / 4 : 0;
+  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < n4; j += stride) {
+    const float4 gv = reinterpret_cast<const float4*>(g)[j], mv = reinterpret_cast<const float4*>(m)[j];
+    const float4 vv = reinterpret_cast<const float4*>(v)[j], pv = reinterpret_cast<const float4*>(p)[j];
+    const float ga[4] = {gv.x, gv.y, gv.z, gv.w}, ma[4] = {mv.x, mv.y, mv.z, mv.w};
+    const float va[4] = {vv.x, vv.y, vv.z, vv.w}, pa[4] = {pv.x, pv.y, pv.z, pv.w};
+    float mo[4], vo[4], po[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      e.m = ma[k]; e.v = va[k]; e.p = pa[k];
+      const AdamOut o = adam_elem(a, ga[k], e);
+      mo[k] = o.m; vo[k] = o.v; po[k] = o.p;
+    }
+    reinterpret_cast<float4*>(m)[j] = make_float4(mo[0], mo[1], mo[2], mo[3]);
+    reinterpret_cast<float4*>(v)[j] = make_float4(vo[0], vo[1], vo[2], vo[3]);
+    reinterpret_cast<float4*>(p)[j] = make_float4(po[0], po[1], po[2], po[3]);
+  }
+  for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    e.m = m[i]; e.v = v[i]; e.p = p[i];
+    adam_apply(a, i, g[i], e);
+  }
   adam_ticket(step, tn);
 }
 
@@ -606,8 +644,10 @@ int launch_clip_grad_norm(float* g, int64_t n, float pre_scale, float max_norm, 
 
 int launch_adam(float* p, const float* g, float* m, float* v, int64_t n, double lr, double beta1, double beta2,
                 double eps, int64_t* step, float gmul, hipStream_t s) {
-  const int64_t nb = n > 0 ? cdiv(n, 256) : 1;  // one workgroup still advances the step when n == 0
-  adam_kernel<<<(unsigned)nb, 256, 0, s>>>(p, g, m, v, n, lr, beta1, beta2, eps, step, gmul);
+  const auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  const int vec = al(p) && al(g) && al(m) && al(v);
+  const int64_t nb = std::min<int64_t>(std::max<int64_t>(cdiv(n, 1024), 1), 1024);  // >= 1: the step still advances
+  adam_kernel<<<(unsigned)nb, 256, 0, s>>>(p, g, m, v, n, lr, beta1, beta2, eps, step, gmul, vec);
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
 }

@@ -20,8 +20,8 @@
 #include <stddef.h>
 #include <stdlib.h>
 
-#include "conv2_dev.h"
 #include "prof.h"
+#include "strip_dev.h"
 
 namespace vqhmm {
 
@@ -40,14 +40,6 @@ struct StripFwdArgs {
 };
 
 namespace {
-constexpr int ST_WIN = 128;                    // window rows: 8 MFMA row blocks, one per wave
-constexpr int ST_HALO = 2;                     // inexact rows on each side
-constexpr int ST_OWN = ST_WIN - 2 * ST_HALO;   // rows a strip stores
-constexpr int ST_XR = ST_WIN + 4;              // rows of the shared x / q buffers (s0 - 2 .. s0 + 129)
-constexpr int ST_XLD = 8;                      // their row stride
-constexpr int ST_LDW = 72;                     // c2_ldx(64): 64-channel slots and weight images
-constexpr int ST_LDF = 24;                     // the prologue's packed-front image row stride
-
 
 template <int NB2>
 struct StripFwdLds {
@@ -82,13 +74,6 @@ struct StripHeadLds {
   double red[8][4];
   float q0w[8][4];
 };
-
-// row_bt's validity test with 32-bit arithmetic (R < 2^31): PCL row r is a sequence position
-__device__ __forceinline__ bool row_valid(int64_t r, int64_t R, int T) {
-  if (r < 0 || r >= R) return false;
-  const unsigned Tp = (unsigned)T + 2u, m = (unsigned)r % Tp;
-  return m >= 1u && m <= (unsigned)T;
-}
 
 // A packed-tap front's weights as c2_mfma_pk gathers them (k-column 4 lg4 + e, channel nb*16 + l16),
 // from the compact [tap][n][8] LDS image into registers for the whole launch; columns past 3C are 0
@@ -266,11 +251,6 @@ __device__ __forceinline__ float row4_reduce_scatter(const float (&c)[4], int i)
   }
   const float send = hi1 ? h2[0] : h2[1];
   return (hi1 ? h2[1] : h2[0]) + dppf<0xB1>(send);
-}
-
-__device__ __forceinline__ void dma16(const float* src, float* dst) {
-  __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint32_t*>(src), (__attribute__((address_space(3))) void*)dst,
-                                   16, 0, 0);
 }
 }  // namespace
 
@@ -807,8 +787,6 @@ struct StripBwdArgs {
 };
 
 namespace {
-constexpr int SB_LDE = 40;  // c2_ldx(32): enc_conv2's dgrad input rows (dh2) and its image
-
 struct StripBwdLds {
   float Wd2[3 * 64 * ST_LDW];    // dec_conv2 dgrad image
   float We2[3 * 64 * SB_LDE];    // enc_conv2 dgrad image (32 input channels)
@@ -818,40 +796,6 @@ struct StripBwdLds {
 };
 static_assert(8 * 18 * ST_LDW >= (ST_WIN + 2) * ST_LDW, "dg1 rows alias the slots");
 
-// conv2_epilogue's ACT = 2 arithmetic (scale, no bias, ReLU-backward mask, pad rows 0) on a 64-wide
-// block: rows r0 + l16, stored (PCL, 64 channels) for l16 in [slo, shi), optionally to LDS rows xs (every
-// row, or only row `only` when only >= 0), row 0 also to the row xlo and row 15 to the row xhi (when given)
-__device__ __forceinline__ void mask_epi(f32x4 (&acc)[4], const float4 (&aux)[4], float sc, int64_t r0, int64_t R,
-                                         int T, int lg4, int l16, int slo, int shi, float* out, float* xs, int xld,
-                                         int only = -1, float* xlo = nullptr, float* xhi = nullptr) {
-  const int64_t r = r0 + l16;
-  const bool valid = row_valid(r, R, T);
-  const bool st = l16 >= slo && l16 < shi && r < R;
-#pragma unroll
-  for (int nb = 0; nb < 4; ++nb) {
-    const float av[4] = {aux[nb].x, aux[nb].y, aux[nb].z, aux[nb].w};
-    f32x4 y;
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      float yy = acc[nb][v] * sc + 0.f;
-      yy = av[v] > 0.f ? yy : 0.f;
-      y[v] = valid ? yy : 0.f;
-    }
-    acc[nb] = y;
-    if (st) *reinterpret_cast<f32x4*>(out + r * 64 + nb * 16 + 4 * lg4) = y;
-    if (xs && (only < 0 || l16 == only)) *reinterpret_cast<f32x4*>(xs + l16 * xld + nb * 16 + 4 * lg4) = y;
-    if (xlo && l16 == 0) *reinterpret_cast<f32x4*>(xlo + nb * 16 + 4 * lg4) = y;
-    if (xhi && l16 == 15) *reinterpret_cast<f32x4*>(xhi + nb * 16 + 4 * lg4) = y;
-  }
-}
-
-// the 64-channel mask rows r0 + l16 of a block (clamped into [0, R): rows outside are not stored)
-__device__ __forceinline__ void load_mask(const float* m, int64_t r0, int64_t R, int lg4, int l16, float4 (&aux)[4]) {
-  int64_t r = r0 + l16;
-  r = r < 0 ? 0 : (r >= R ? R - 1 : r);
-#pragma unroll
-  for (int nb = 0; nb < 4; ++nb) aux[nb] = *reinterpret_cast<const float4*>(m + r * 64 + nb * 16 + 4 * lg4);
-}
 }  // namespace
 
 template <int PROF>

@@ -52,6 +52,8 @@ _SIGS = {
                                           c_vp]),
     "vqhmm_elbo_bwd_f32": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(c_vp), c_vp, c_vp, c_i64, c_i64, c_f32,
                                           c_vp, c_vp, c_sz, c_vp, c_vp]),
+    "vqhmm_elbo_bwd_loss_f32": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(c_vp), c_vp, c_vp, c_i64, c_i64,
+                                               c_f32, c_vp, c_vp, c_sz, c_vp, c_vp, c_vp, c_vp]),
     "vqhmm_elbo_bwd_adam_f32": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(c_vp), c_vp, c_vp, c_i64, c_i64,
                                                c_f32, c_vp, c_sz, c_vp, c_vp, c_vp, c_vp, ctypes.c_double,
                                                ctypes.c_double, ctypes.c_double, ctypes.c_double, c_vp, c_f32, c_vp,

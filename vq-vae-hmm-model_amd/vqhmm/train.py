@@ -136,14 +136,18 @@ class TrainState:
         ws = self.workspace(B, T)
         st = _ext.stream_ptr(self.device)
         d = ctypes.byref(self.dims)
+        # need_grad = 2: the loss is finalized in the backward's tail launch (vqhmm_elbo_bwd_loss_f32), one
+        # launch fewer (the overlapped backward runs stage by stage, so its forward finalizes the loss itself)
+        ng = 1 if self.overlap_bwd else 2
         _ext.check(self.lib.vqhmm_elbo_fwd_f32(d, self.ptrs, _ext.ptr(x), _ext.ptr(u), lay, _ext.ptr(lengths),
-                                               _ext.ptr(norm), B, T, float(beta), 1, _ext.ptr(ws), ws.numel(),
+                                               _ext.ptr(norm), B, T, float(beta), ng, _ext.ptr(ws), ws.numel(),
                                                _ext.ptr(self.loss), _ext.ptr(self.epoch_acc), st), "elbo forward")
         if self.overlap_bwd:
             self._backward_overlapped(x, B, T, beta, ws, norm)
         else:
-            _ext.check(self.lib.vqhmm_elbo_bwd_f32(d, self.ptrs, _ext.ptr(x), _ext.ptr(norm), B, T, float(beta), None,
-                                                   _ext.ptr(ws), ws.numel(), _ext.ptr(self.grad), st),
+            _ext.check(self.lib.vqhmm_elbo_bwd_loss_f32(d, self.ptrs, _ext.ptr(x), _ext.ptr(norm), B, T, float(beta),
+                                                        None, _ext.ptr(ws), ws.numel(), _ext.ptr(self.grad),
+                                                        _ext.ptr(self.loss), _ext.ptr(self.epoch_acc), st),
                        "elbo backward")
 
     def _backward_overlapped(self, x, B, T, beta, ws, norm=None):
