@@ -107,17 +107,28 @@ def stage_timings(lib, st, x, u, L, B, T, beta, nsteps):
     return out
 
 
-def traffic_for(kernel_name, cfg):
-    """PMC-measured HBM bytes per launch, if committed under profiles/ for this kernel + config."""
+def traffic_for(kernel_name, cfg, batch=None):
+    """PMC-measured HBM bytes per launch, if committed under profiles/ for this kernel at this config AND
+    batch (training-step sections are keyed "cfg/B<batch>"; the fixed-shape kernel legs by name): null when
+    no PMC pass ran at this shape, never another batch's figure."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
         return None
     try:
         with open(path) as f:
             tab = json.load(f)
-        return tab.get(cfg, {}).get(kernel_name)
+        sec = f"{cfg}/B{batch}" if batch is not None else cfg
+        return tab.get(sec, {}).get(kernel_name)
     except (OSError, ValueError):
         return None
+
+
+def traffic_checked(traffic, avg_us):
+    """A PMC byte count is kept only if it is physically possible for the launch it is quoted with
+    (traffic / duration <= the 8 TB/s HBM peak); otherwise null."""
+    if traffic is None or avg_us is None or avg_us <= 0:
+        return traffic
+    return traffic if traffic / (avg_us * 1e-6) <= HBM_PEAK_GBPS * 1e9 else None
 
 
 def vq_cfg3(lib):
@@ -144,7 +155,7 @@ def vq_cfg3(lib):
     gbps = byts / (us * 1e-6) / 1e9
     out = {"kernel": "vq_rows_kernel (vqhmm_vq_argmin_f32)", "bound": "hbm", "avg_us": round(us, 2),
            "achieved": round(gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(gbps / HBM_PEAK_GBPS, 4),
-           "traffic": traffic_for("vq_argmin", "vq_cfg3"), "shape": "B2048 Dv64 T200 K32"}
+           "traffic": traffic_checked(traffic_for("vq_argmin", "vq_cfg3"), us), "shape": "B2048 Dv64 T200 K32"}
     # the fused quantize (pseudocode.txt:12-18): argmin + z_q gather + straight-through value written +
     # squared-error partials, then the fixed-order partial sum: z read once, z_q_st and idx written
     zq = torch.empty_like(z)
@@ -215,7 +226,7 @@ def hmm_kernels(lib):
         gbps = byts / (us * 1e-6) / 1e9
         out[name] = {"kernel": kern, "bound": "hbm", "avg_us": round(us, 2), "achieved": round(gbps, 1),
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(gbps / HBM_PEAK_GBPS, 4),
-                     "traffic": traffic_for(name, name), "shape": f"B{B} T{T} K{K}"}
+                     "traffic": traffic_checked(traffic_for(name, name), us), "shape": f"B{B} T{T} K{K}"}
         del log_A, em, ws
     # the fused Prior-MLP -> Viterbi at the same cfg5 shard: log_A is built on the chip
     # from u, so the kernel is bound by the MLP on the f32 MFMA: 2 (U + K^2) TH flops per position
@@ -452,8 +463,8 @@ def main():
             ach = dom["bytes"] / dur / 1e9
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBPS, 4)}
-        roof.update({"traffic": traffic_for(dom["name"], a.config), "kernel": dom["name"],
-                     "avg_us": round(dom["us"], 2)})
+        roof.update({"traffic": traffic_checked(traffic_for(dom["name"], a.config, B), dom["us"]),
+                     "kernel": dom["name"], "avg_us": round(dom["us"], 2)})
         kernels = {s["name"]: round(s["us"], 2) for s in stages}
         # every launch's own roofline (SURVEY 8d asks for the H->H convs' MFMA fraction, not only the
         # dominant stage's): algorithmic flops (MFMA-bound) or bytes (HBM-bound) over the event-timed

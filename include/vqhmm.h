@@ -40,8 +40,8 @@ extern "C" {
 /* Bits of the training step's device status word (vqhmm_elbo_status_offset).  Kernels only
  * ever OR bits in; the caller zeroes the word when it allocates the workspace and reads it
  * after a synchronisation (TrainState.check_status raises RuntimeError on any bit). */
-#define VQHMM_STATUS_TAIL_TIMEOUT 1ull /* reserved: raised by the round-3 tail's in-launch wait; the tail has
-                                          * had no cross-workgroup wait since, so no kernel sets it */
+#define VQHMM_STATUS_TAIL_TIMEOUT 1ull /* reserved: no kernel sets it (no launch waits on another
+                                          * workgroup); kept so callers' status checks stay valid */
 
 /* Number of parameter tensors of a VAE_HMM, in nn.Module.parameters() order
  * (VQ_VAE_HMM_fixed.py:92-98 -> encoder :32-36, prior :44-57, decoder :74-79). */
@@ -100,9 +100,10 @@ int vqhmm_vq_quantize_f32(const float* z, int64_t B, int64_t Dv, int64_t T, cons
  * log_A (B,T,K,K) [t = transition t-1 -> t], em (B,T,K) emission log-potentials,
  * lengths (B) int64 -> path (B,T) int32 (-1 at t >= length), score (B) fp32.
  * d_t[j] = (max_i d_{t-1}[i] + log_A[t,i,j]) + em[t,j] in fp32, ties -> lowest i;
- * last state = first argmax.  Bit-exact vs oracle/c/hmm_oracle.c.  K <= 256 (K <= 8: packed lane
- * groups, hmm.hip; 8 < K <= 32: one sequence per wave, hmm_wide.hip; 32 < K <= 256: one workgroup
- * per sequence, thread = state, hmm_generic.hip); larger K -> VQHMM_EUNSUPPORTED.
+ * last state = first argmax.  Bit-exact vs oracle/c/hmm_oracle.c.  K <= 4096 (K <= 8: packed lane
+ * groups, hmm.hip; 8 < K <= 32: one sequence per wave, hmm_wide.hip; 32 < K <= 4096: one workgroup
+ * per sequence, states j, j + 256, .. per thread, 16-bit backpointers past 256 states,
+ * hmm_generic.hip); larger K -> VQHMM_EUNSUPPORTED.
  * Workspace: vqhmm_viterbi_workspace_size(B, T, K) bytes (backpointers as one
  * 64-bit lane ballot per step per wave of 64 / KP^2 sequences, KP = K rounded
  * up to a power of two; T rounded up to 64). */
@@ -117,7 +118,7 @@ int vqhmm_viterbi_f32(const float* log_pi, const float* log_A, const float* em, 
  * Base-2 log-space alpha/beta with per-step shifts; a chunk whose fast step
  * leaves float range is recomputed with the max-shifted log-sum-exp.
  * Workspace: vqhmm_fwdbwd_workspace_size(B, T, K) = 2 * B * T * K * 4 bytes.
- * Accuracy target vs the fp64 oracle: |gamma| abs 1e-5, logZ rel 1e-5.  K <= 256 (as Viterbi). */
+ * Accuracy target vs the fp64 oracle: |gamma| abs 1e-5, logZ rel 1e-5.  K <= 4096 (as Viterbi). */
 size_t vqhmm_fwdbwd_workspace_size(int64_t B, int64_t T, int64_t K);
 int vqhmm_fwdbwd_f32(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths,
                      int64_t B, int64_t T, int64_t K, float* gamma, float* logZ, void* workspace,
@@ -255,6 +256,24 @@ int vqhmm_forward_f32(const vqhmm_dims_t* dims, const float* const* params, cons
                       size_t ws_bytes, void* stream);
 int vqhmm_prior_f32(const vqhmm_dims_t* dims, const float* const* params, const float* u, int u_layout,
                     int64_t B, int64_t T, float* log_pi, float* log_A, void* stream);
+/* Autograd of the module surface (VAE_HMM.encode / decode / forward under torch autograd, :100-104,
+ * :139-143; examples/backtest_example.py:30 calls encode with grad enabled).  Each recomputes its module's
+ * forward into the workspace (vqhmm_module_bwd_workspace_size), then runs the data gradients, the weight
+ * gradients and one fixed-order slab reduction.  grad: the flat buffer of vqhmm_param_layout(dims); only the
+ * module's own entries are written (encode: encoder.*; decode: decoder.*; forward: both).  Output gradients
+ * are channels-first like the outputs: dlogits (B,K,T); dpar = [dmu | dlogvar] (B,2D,T); dq (B,K,T) the
+ * gradient of forward's q output (NULL: 0; forward's dpar NULL: 0).  Input gradients dx (B,D,T) / dq (B,K,T)
+ * are written when non-NULL. */
+int vqhmm_module_bwd_workspace_size(const vqhmm_dims_t* dims, int64_t B, int64_t T, size_t* bytes);
+int vqhmm_encode_bwd_f32(const vqhmm_dims_t* dims, const float* const* params, const float* x,
+                         const float* dlogits, int64_t B, int64_t T, void* workspace, size_t ws_bytes,
+                         float* grad, float* dx, void* stream);
+int vqhmm_decode_bwd_f32(const vqhmm_dims_t* dims, const float* const* params, const float* q,
+                         const float* dpar, int64_t B, int64_t T, void* workspace, size_t ws_bytes,
+                         float* grad, float* dq, void* stream);
+int vqhmm_forward_bwd_f32(const vqhmm_dims_t* dims, const float* const* params, const float* x,
+                          const float* dpar, const float* dq, int64_t B, int64_t T, void* workspace,
+                          size_t ws_bytes, float* grad, float* dx, void* stream);
 
 /* ------------------------------------------- fused Prior -> Viterbi ----
  * the Viterbi path of vqhmm_viterbi_f32 over the tables vqhmm_prior_f32 would write

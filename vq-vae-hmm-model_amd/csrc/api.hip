@@ -1331,6 +1331,229 @@ int vqhmm_regimes_f32(const vqhmm_dims_t* d, const float* const* w, const float*
   return encode_impl(d, w, x, B, T, nullptr, q, nullptr, b.in, b.A, b.B, (hipStream_t)stream, regimes);
 }
 
+// ---------------------------------------------------------------- autograd of the module surface
+// VAE_HMM.encode / decode / forward under autograd (VQ_VAE_HMM_fixed.py:100-104, :139-143): the module's forward
+// recomputed into the workspace (ReLU outputs kept as the backward's masks), the data gradients on the conv
+// kernels (transposed + flipped weights, ReLU-backward masks), the weight gradients as split-K slabs, and one
+// fixed-order slab reduction (tail_kernel) into the flat gradient; the composed decoder conv1's dW / dE by
+// compose_bwd.  Layers as ElboPlan::wl: 0 to_params, 1 dec_conv2, 2 dec_conv1 (composed), 3 to_logits,
+// 4 enc_conv2, 5 enc_conv1.
+namespace {
+struct ModBwd {
+  int64_t R;
+  float *xin, *h1, *h2, *q, *dlog, *dh2, *dh1;
+  float *qin, *g1, *g2, *dpar, *dg2, *dg1, *dq, *dqx, *zero, *Wc, *dWc;
+  WLayer wl[6];
+  size_t bytes;
+};
+
+ModBwd plan_modbwd(const vqhmm_dims_t* d, int64_t B, int64_t T, void* ws) {
+  ModBwd m{};
+  Carver c{reinterpret_cast<char*>(ws ? ws : reinterpret_cast<void*>(4096))};
+  const int64_t R = B * (T + 2);
+  const int D = d->input_dim, H = d->hidden_dim, H2 = d->hidden_dim2, K = d->K;
+  m.R = R;
+  m.xin = c.take<float>(R * ld4(D));
+  m.h1 = c.take<float>(R * ld4(H));
+  m.h2 = c.take<float>(R * ld4(H2));
+  m.q = c.take<float>(R * ld4(K));
+  m.dlog = c.take<float>(R * ld4(K));
+  m.dh2 = c.take<float>(R * ld4(H2));
+  m.dh1 = c.take<float>(R * ld4(H));
+  m.qin = c.take<float>(R * ld4(K));
+  m.g1 = c.take<float>(R * ld4(H));
+  m.g2 = c.take<float>(R * ld4(H));
+  m.dpar = c.take<float>(R * ld4(2 * D));
+  m.dg2 = c.take<float>(R * ld4(H));
+  m.dg1 = c.take<float>(R * ld4(H));
+  m.dq = c.take<float>(R * ld4(K));
+  m.dqx = c.take<float>(R * ld4(K));
+  m.zero = c.take<float>(R * ld4(K));
+  m.Wc = c.take<float>((size_t)H * K * 3);
+  m.dWc = c.take<float>((size_t)H * K * 3);
+  const int shapes[6][3] = {{2 * D, H, 1}, {H, H, 3}, {H, K, 3}, {K, H2, 1}, {H2, H, 3}, {H, D, 3}};
+  for (int i = 0; i < 6; ++i) {
+    WLayer& w = m.wl[i];
+    w.N = shapes[i][0]; w.C = shapes[i][1]; w.ks = shapes[i][2];
+    WgradArgs probe{};
+    probe.N = w.N; probe.C = w.C; probe.ks = w.ks; probe.rows_per_chunk = 64;
+    w.rows = (w.N <= 64 && w.C <= 64) ? wgrad2_rows(R, w.N, w.C, w.ks)
+             : wgradbig_supported(probe) ? wgradbig_rows(R, w.N, w.C)
+                                         : wgrad_chunks(R, cdiv(w.N, 64) * cdiv(w.C, 64));
+    w.nchunks = cdiv(R, w.rows);
+    w.slab = c.take<float>((size_t)w.nchunks * w.N * w.C * w.ks);
+    w.bslab = c.take<float>((size_t)w.nchunks * w.N);
+  }
+  m.bytes = c.off + 256;
+  return m;
+}
+
+ConvArgs mconv(const ModBwd& m, int T, const float* src, int Kc, int ks, const float* W, const float* bias, int N,
+               int act, const float* aux, float* out, int w_dgrad) {
+  ConvArgs a{};
+  a.R = m.R; a.T = T;
+  a.src = src; a.Kc = Kc; a.ks = ks; a.W = W; a.bias = bias; a.N = N; a.act = act; a.aux = aux; a.out = out;
+  a.w_dgrad = w_dgrad;
+  return a;
+}
+
+int mwgrad(const ModBwd& m, int T, int i, const float* dy, const float* x, hipStream_t s) {
+  const WLayer& L = m.wl[i];
+  WgradArgs wa{};
+  wa.dy = dy; wa.x = x; wa.R = m.R; wa.T = T;
+  wa.N = L.N; wa.C = L.C; wa.ks = L.ks; wa.rows_per_chunk = L.rows; wa.slab = L.slab; wa.bias_slab = L.bslab;
+  return launch_wgrad(wa, s);
+}
+
+// encoder forward (x CF -> xin, h1, h2; with q_pcl: + to_logits and its softmax -> q_pcl)
+int mod_enc_fwd(const vqhmm_dims_t* d, const float* const* w, const float* x, int64_t B, int T, const ModBwd& m,
+                float* q_pcl, hipStream_t s) {
+  int rc;
+  if ((rc = launch_to_pcl(x, d->input_dim, B, T, T, 1, m.xin, s))) return rc;
+  if ((rc = launch_conv(mconv(m, T, m.xin, d->input_dim, 3, w[ENC1_W], w[ENC1_B], d->hidden_dim, 1, nullptr, m.h1, 0), s)))
+    return rc;
+  ConvArgs a = mconv(m, T, m.h1, d->hidden_dim, 3, w[ENC2_W], w[ENC2_B], d->hidden_dim2, 1, nullptr, m.h2, 0);
+  if (q_pcl) {
+    a.tW = w[LOGIT_W]; a.tb = w[LOGIT_B]; a.C2 = d->K; a.q_out = q_pcl;
+  }
+  return launch_conv(a, s);
+}
+// encoder backward from m.dlog: to_logits / enc_conv2 data gradients (+ enc_conv1's into dx, CF), weight gradients
+int mod_enc_bwd(const vqhmm_dims_t* d, const float* const* w, int T, const ModBwd& m, float* dx, hipStream_t s) {
+  int rc;
+  if ((rc = launch_conv(mconv(m, T, m.dlog, d->K, 1, w[LOGIT_W], nullptr, d->hidden_dim2, 2, m.h2, m.dh2, 1), s)))
+    return rc;
+  if ((rc = launch_conv(mconv(m, T, m.dh2, d->hidden_dim2, 3, w[ENC2_W], nullptr, d->hidden_dim, 2, m.h1, m.dh1, 1), s)))
+    return rc;
+  if (dx) {
+    ConvArgs a = mconv(m, T, m.dh1, d->hidden_dim, 3, w[ENC1_W], nullptr, d->input_dim, 0, nullptr, nullptr, 1);
+    a.out_cf = dx;
+    if ((rc = launch_conv(a, s))) return rc;
+  }
+  if ((rc = mwgrad(m, T, 3, m.dlog, m.h2, s))) return rc;
+  if ((rc = mwgrad(m, T, 4, m.dh2, m.h1, s))) return rc;
+  return mwgrad(m, T, 5, m.dh1, m.xin, s);
+}
+// decoder forward from q (PCL) -> g1, g2 (composed conv1 W' = W E^T into m.Wc)
+int mod_dec_fwd(const vqhmm_dims_t* d, const float* const* w, const float* qp, int T, const ModBwd& m, hipStream_t s) {
+  int rc;
+  const int H = d->hidden_dim;
+  if ((rc = launch_compose_fwd(w[DEC1_W], w[EMB], H, d->K, m.Wc, s))) return rc;
+  if ((rc = launch_conv(mconv(m, T, qp, d->K, 3, m.Wc, w[DEC1_B], H, 1, nullptr, m.g1, 0), s))) return rc;
+  return launch_conv(mconv(m, T, m.g1, H, 3, w[DEC2_W], w[DEC2_B], H, 1, nullptr, m.g2, 0), s);
+}
+// decoder backward from m.dpar: to_params / dec_conv2 / composed dec_conv1 data gradients (dq: PCL m.dq and/or CF
+// dq_cf), weight gradients of the three layers
+int mod_dec_bwd(const vqhmm_dims_t* d, const float* const* w, const float* qp, int T, const ModBwd& m, float* dq_cf,
+                hipStream_t s) {
+  int rc;
+  const int H = d->hidden_dim;
+  if ((rc = launch_conv(mconv(m, T, m.dpar, 2 * d->input_dim, 1, w[PAR_W], nullptr, H, 2, m.g2, m.dg2, 1), s))) return rc;
+  if ((rc = launch_conv(mconv(m, T, m.dg2, H, 3, w[DEC2_W], nullptr, H, 2, m.g1, m.dg1, 1), s))) return rc;
+  ConvArgs a = mconv(m, T, m.dg1, H, 3, m.Wc, nullptr, d->K, 0, nullptr, m.dq, 1);
+  a.out_cf = dq_cf;
+  if ((rc = launch_conv(a, s))) return rc;
+  if ((rc = mwgrad(m, T, 0, m.dpar, m.g2, s))) return rc;
+  if ((rc = mwgrad(m, T, 1, m.dg2, m.g1, s))) return rc;
+  return mwgrad(m, T, 2, m.dg1, qp, s);
+}
+// the slabs of layers [i0, i1) summed into grad (the composed layer's dWc into m.dWc, then dW / dE)
+int mod_reduce(const vqhmm_dims_t* d, const float* const* w, const ModBwd& m, int i0, int i1, float* g, hipStream_t s) {
+  int64_t off[VQHMM_NPARAMS + 1];
+  vqhmm_param_layout(d, off);
+  const int wout[6] = {PAR_W, DEC2_W, DEC1_W, LOGIT_W, ENC2_W, ENC1_W};
+  const int bout[6] = {PAR_B, DEC2_B, DEC1_B, LOGIT_B, ENC2_B, ENC1_B};
+  TailArgs ta{};
+  int n = 0;
+  for (int i = i0; i < i1; ++i) {
+    const WLayer& L = m.wl[i];
+    float* wo = i == 2 ? m.dWc : g + off[wout[i]];
+    ta.s[n++] = SlabSeg{L.slab, wo, nullptr, L.nchunks, (int64_t)L.N * L.C * L.ks, nullptr, 0, 0};
+    ta.s[n++] = SlabSeg{L.bslab, g + off[bout[i]], nullptr, L.nchunks, L.N, nullptr, 0, 0};
+  }
+  ta.nseg = n;
+  int rc;
+  if ((rc = launch_grad_tail(ta, s))) return rc;
+  if (i0 <= 2 && 2 < i1) {
+    const LogPriorGradArgs lp{};
+    return launch_compose_bwd(m.dWc, w[DEC1_W], w[EMB], d->hidden_dim, d->K, g + off[DEC1_W], g + off[EMB], lp, s);
+  }
+  return VQHMM_OK;
+}
+}  // namespace
+
+int vqhmm_module_bwd_workspace_size(const vqhmm_dims_t* d, int64_t B, int64_t T, size_t* bytes) {
+  if (!dims_ok(d) || B < 0 || T < 0 || !bytes) return VQHMM_EINVAL;
+  *bytes = plan_modbwd(d, B, T, nullptr).bytes;
+  return VQHMM_OK;
+}
+
+int vqhmm_encode_bwd_f32(const vqhmm_dims_t* d, const float* const* w, const float* x, const float* dlogits, int64_t B,
+                         int64_t T, void* ws, size_t ws_bytes, float* grad, float* dx, void* stream) {
+  if (!dims_ok(d) || !w || !x || !dlogits || !ws || !grad || B < 0 || T < 0) return VQHMM_EINVAL;
+  for (int i = ENC1_W; i <= LOGIT_B; ++i)
+    if (!w[i]) return VQHMM_EINVAL;
+  if (B * T == 0) return VQHMM_OK;
+  const ModBwd m = plan_modbwd(d, B, T, ws);
+  if (ws_bytes < m.bytes) return VQHMM_EWORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  int rc;
+  if ((rc = mod_enc_fwd(d, w, x, B, (int)T, m, nullptr, s))) return rc;
+  if ((rc = launch_to_pcl(dlogits, d->K, B, (int)T, T, 1, m.dlog, s))) return rc;
+  if ((rc = mod_enc_bwd(d, w, (int)T, m, dx, s))) return rc;
+  return mod_reduce(d, w, m, 3, 6, grad, s);
+}
+
+int vqhmm_decode_bwd_f32(const vqhmm_dims_t* d, const float* const* w, const float* q, const float* dpar, int64_t B,
+                         int64_t T, void* ws, size_t ws_bytes, float* grad, float* dq, void* stream) {
+  if (!dims_ok(d) || !w || !q || !dpar || !ws || !grad || B < 0 || T < 0) return VQHMM_EINVAL;
+  for (int i = EMB; i <= PAR_B; ++i)
+    if (!w[i]) return VQHMM_EINVAL;
+  if (B * T == 0) return VQHMM_OK;
+  const ModBwd m = plan_modbwd(d, B, T, ws);
+  if (ws_bytes < m.bytes) return VQHMM_EWORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  int rc;
+  if ((rc = launch_to_pcl(q, d->K, B, (int)T, T, 1, m.qin, s))) return rc;
+  if ((rc = mod_dec_fwd(d, w, m.qin, (int)T, m, s))) return rc;
+  if ((rc = launch_to_pcl(dpar, 2 * d->input_dim, B, (int)T, T, 1, m.dpar, s))) return rc;
+  if ((rc = mod_dec_bwd(d, w, m.qin, (int)T, m, dq, s))) return rc;
+  return mod_reduce(d, w, m, 0, 3, grad, s);
+}
+
+int vqhmm_forward_bwd_f32(const vqhmm_dims_t* d, const float* const* w, const float* x, const float* dpar,
+                          const float* dq, int64_t B, int64_t T, void* ws, size_t ws_bytes, float* grad, float* dx,
+                          void* stream) {
+  if (!dims_ok(d) || !w || !x || !ws || !grad || B < 0 || T < 0) return VQHMM_EINVAL;
+  for (int i = ENC1_W; i <= PAR_B; ++i)
+    if (!w[i] && (i < LOG_PRIOR || i > TN2_B)) return VQHMM_EINVAL;
+  if (B * T == 0) return VQHMM_OK;
+  const ModBwd m = plan_modbwd(d, B, T, ws);
+  if (ws_bytes < m.bytes) return VQHMM_EWORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  const int Ti = (int)T;
+  const size_t kbytes = (size_t)m.R * ld4(d->K) * sizeof(float);
+  int rc;
+  if ((rc = mod_enc_fwd(d, w, x, B, Ti, m, m.q, s))) return rc;  // q = softmax(logits) (PCL), the decoder's input
+  if ((rc = mod_dec_fwd(d, w, m.q, Ti, m, s))) return rc;
+  if (dpar) {
+    if ((rc = launch_to_pcl(dpar, 2 * d->input_dim, B, Ti, T, 1, m.dpar, s))) return rc;
+  } else if (hipMemsetAsync(m.dpar, 0, (size_t)m.R * ld4(2 * d->input_dim) * sizeof(float), s) != hipSuccess) {
+    return VQHMM_ELAUNCH;
+  }
+  if ((rc = mod_dec_bwd(d, w, m.q, Ti, m, nullptr, s))) return rc;
+  // dL/dq = the decoder's + the caller's (q is also an output); the softmax backward of q = softmax(logits)
+  if (dq) {
+    if ((rc = launch_to_pcl(dq, d->K, B, Ti, T, 1, m.dqx, s))) return rc;
+  } else if (hipMemsetAsync(m.dqx, 0, kbytes, s) != hipSuccess) {
+    return VQHMM_ELAUNCH;
+  }
+  if (hipMemsetAsync(m.zero, 0, kbytes, s) != hipSuccess) return VQHMM_ELAUNCH;
+  if ((rc = launch_logits_bwd(m.q, m.dq, m.dqx, m.zero, nullptr, m.R, d->K, m.dlog, s))) return rc;
+  if ((rc = mod_enc_bwd(d, w, Ti, m, dx, s))) return rc;
+  return mod_reduce(d, w, m, 0, 6, grad, s);
+}
+
 int vqhmm_argmax_f32(const float* q, int64_t B, int64_t K, int64_t T, int32_t* idx, void* stream) {
   if (B < 0 || K < 1 || T < 0 || K > INT32_MAX || (B * T > 0 && (!q || !idx))) return VQHMM_EINVAL;
   return launch_argmax_cf(q, B, K, T, idx, (hipStream_t)stream);
@@ -1347,6 +1570,93 @@ int vqhmm_prior_f32(const vqhmm_dims_t* d, const float* const* w, const float* u
   if (u_layout == 0) { p.u_sc = T; p.u_st = 1; } else { p.u_sc = 1; p.u_st = d->u_dim; }
   p.W1 = w[TN0_W]; p.b1 = w[TN0_B]; p.W2 = w[TN2_W]; p.b2 = w[TN2_B]; p.log_A = log_A;
   return launch_prior_fwd(p, s);
+}
+
+// Autograd of Prior.forward alone (VQ_VAE_HMM_fixed.py:59-71): the MLP recomputed on PCL rows (1x1 convs), the
+// log_softmax backward (prior_lsm_bwd), the hidden layer's masked data gradient and the two weight gradients,
+// one slab reduction; du (CF (B, U, T), nullable) by the first layer's data gradient.
+namespace {
+struct PriorBwd {
+  int64_t R;
+  float *up, *hid, *lg, *dA, *dlg, *dhid;
+  WLayer wl[2];  // 0: transition_net.2 (K^2, TH), 1: transition_net.0 (TH, U)
+  size_t bytes;
+};
+PriorBwd plan_prior_bwd(const vqhmm_dims_t* d, int64_t B, int64_t T, void* ws) {
+  PriorBwd p{};
+  Carver c{reinterpret_cast<char*>(ws ? ws : reinterpret_cast<void*>(4096))};
+  const int64_t R = B * (T + 2);
+  const int K2 = d->K * d->K, TH = d->trans_hidden, U = d->u_dim;
+  p.R = R;
+  p.up = c.take<float>(R * ld4(U));
+  p.hid = c.take<float>(R * ld4(TH));
+  p.lg = c.take<float>(R * ld4(K2));
+  p.dA = c.take<float>(R * ld4(K2));
+  p.dlg = c.take<float>(R * ld4(K2));
+  p.dhid = c.take<float>(R * ld4(TH));
+  const int shapes[2][2] = {{K2, TH}, {TH, U}};
+  for (int i = 0; i < 2; ++i) {
+    WLayer& w = p.wl[i];
+    w.N = shapes[i][0]; w.C = shapes[i][1]; w.ks = 1;
+    WgradArgs probe{};
+    probe.N = w.N; probe.C = w.C; probe.ks = 1; probe.rows_per_chunk = 64;
+    w.rows = (w.N <= 64 && w.C <= 64) ? wgrad2_rows(R, w.N, w.C, 1)
+             : wgradbig_supported(probe) ? wgradbig_rows(R, w.N, w.C)
+                                         : wgrad_chunks(R, cdiv(w.N, 64) * cdiv(w.C, 64));
+    w.nchunks = cdiv(R, w.rows);
+    w.slab = c.take<float>((size_t)w.nchunks * w.N * w.C);
+    w.bslab = c.take<float>((size_t)w.nchunks * w.N);
+  }
+  p.bytes = c.off + 256;
+  return p;
+}
+}  // namespace
+
+int vqhmm_prior_bwd_workspace_size(const vqhmm_dims_t* d, int64_t B, int64_t T, size_t* bytes) {
+  if (!dims_ok(d) || B < 0 || T < 0 || !bytes) return VQHMM_EINVAL;
+  *bytes = plan_prior_bwd(d, B, T, nullptr).bytes;
+  return VQHMM_OK;
+}
+
+int vqhmm_prior_bwd_f32(const vqhmm_dims_t* d, const float* const* w, const float* u, int u_layout,
+                        const float* dlog_pi, const float* dlog_A, int64_t B, int64_t T, void* ws, size_t ws_bytes,
+                        float* grad, float* du, void* stream) {
+  if (!dims_ok(d) || !w || !ws || !grad || B < 0 || T < 0 || (B * T > 0 && (!u || !dlog_A))) return VQHMM_EINVAL;
+  for (int i = LOG_PRIOR; i <= TN2_B; ++i)
+    if (!w[i]) return VQHMM_EINVAL;
+  const PriorBwd p = plan_prior_bwd(d, B, T, ws);
+  if (ws_bytes < p.bytes) return VQHMM_EWORKSPACE;
+  int64_t off[VQHMM_NPARAMS + 1];
+  vqhmm_param_layout(d, off);
+  hipStream_t s = (hipStream_t)stream;
+  const int Ti = (int)T, K = d->K, K2 = K * K, TH = d->trans_hidden, U = d->u_dim;
+  int rc;
+  if (B * T == 0)  // only log_pi's gradient
+    return launch_prior_lsm_bwd(nullptr, nullptr, 0, K, nullptr, w[LOG_PRIOR], dlog_pi, grad + off[LOG_PRIOR], s);
+  ModBwd m{};  // mconv / mwgrad take the row count from it
+  m.R = p.R;
+  if ((rc = launch_to_pcl(u, U, B, Ti, u_layout == 0 ? T : 1, u_layout == 0 ? 1 : U, p.up, s))) return rc;
+  if ((rc = launch_conv(mconv(m, Ti, p.up, U, 1, w[TN0_W], w[TN0_B], TH, 1, nullptr, p.hid, 0), s))) return rc;
+  if ((rc = launch_conv(mconv(m, Ti, p.hid, TH, 1, w[TN2_W], w[TN2_B], K2, 0, nullptr, p.lg, 0), s))) return rc;
+  if ((rc = launch_to_pcl(dlog_A, K2, B, Ti, 1, K2, p.dA, s))) return rc;  // (B, T, K, K) = (B, T, K^2)
+  if ((rc = launch_prior_lsm_bwd(p.lg, p.dA, p.R, K, p.dlg, w[LOG_PRIOR], dlog_pi, grad + off[LOG_PRIOR], s))) return rc;
+  if ((rc = launch_conv(mconv(m, Ti, p.dlg, K2, 1, w[TN2_W], nullptr, TH, 2, p.hid, p.dhid, 1), s))) return rc;
+  if (du) {
+    ConvArgs a = mconv(m, Ti, p.dhid, TH, 1, w[TN0_W], nullptr, U, 0, nullptr, nullptr, 1);
+    a.out_cf = du;
+    if ((rc = launch_conv(a, s))) return rc;
+  }
+  m.wl[0] = p.wl[0];
+  m.wl[1] = p.wl[1];
+  if ((rc = mwgrad(m, Ti, 0, p.dlg, p.hid, s))) return rc;
+  if ((rc = mwgrad(m, Ti, 1, p.dhid, p.up, s))) return rc;
+  TailArgs ta{};
+  ta.s[0] = SlabSeg{p.wl[0].slab, grad + off[TN2_W], nullptr, p.wl[0].nchunks, (int64_t)K2 * TH, nullptr, 0, 0};
+  ta.s[1] = SlabSeg{p.wl[0].bslab, grad + off[TN2_B], nullptr, p.wl[0].nchunks, K2, nullptr, 0, 0};
+  ta.s[2] = SlabSeg{p.wl[1].slab, grad + off[TN0_W], nullptr, p.wl[1].nchunks, (int64_t)TH * U, nullptr, 0, 0};
+  ta.s[3] = SlabSeg{p.wl[1].bslab, grad + off[TN0_B], nullptr, p.wl[1].nchunks, TH, nullptr, 0, 0};
+  ta.nseg = 4;
+  return launch_grad_tail(ta, s);
 }
 
 size_t vqhmm_prior_viterbi_workspace_size(const vqhmm_dims_t* d, int64_t B, int64_t T) {

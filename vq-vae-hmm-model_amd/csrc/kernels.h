@@ -405,6 +405,9 @@ int launch_finalize_loss(const double* part, int nblk, const int64_t* lengths, c
 int launch_compose_fwd(const float* W, const float* E, int H, int K, float* Wc, hipStream_t s);
 int launch_compose_bwd(const float* dWc, const float* W, const float* E, int H, int K, float* dW, float* dE,
                        const LogPriorGradArgs& lp, hipStream_t s);
+// Prior.forward's log_softmax backward (rows of K of each PCL row's K*K logits) + log_pi's (misc.hip)
+int launch_prior_lsm_bwd(const float* lg, const float* dA, int64_t R, int K, float* dlg, const float* log_prior,
+                         const float* dlog_pi, float* dlp, hipStream_t s);
 int launch_logits_bwd(const float* q, const float* dq_dec, const float* dqx, const float* dlx, const float* scale,
                       int64_t R, int K, float* dlog, hipStream_t s);
 // CF / (B,T,C) tensor -> PCL (R, ld4(C)) with zero pad rows / channels:

@@ -554,6 +554,50 @@ __device__ void log_prior_grad_body(const LogPriorGradArgs& a) {
   for (int k = 0; k < K; ++k) a.out[k] = sc * (c * a.q0sum[k] - __expf(a.log_prior[k] - m) / se * tot);
 }
 
+// ------------------------------------------------------------ Prior backward (autograd of Prior.forward alone)
+// log_A = log_softmax(lg) over each row i of a position's K x K logits (VQ_VAE_HMM_fixed.py:68-69):
+//   dlg[i][j] = dA[i][j] - softmax(lg[i])_j * sum_j dA[i][j]   (thread per (PCL row, i); pad channels 0)
+// and, by thread 0, log_pi = log_softmax(log_prior) (:71): dlp[k] = dlog_pi[k] - softmax(log_prior)_k sum dlog_pi
+__global__ __launch_bounds__(256) void prior_lsm_bwd_kernel(const float* lg, const float* dA, int64_t R, int K,
+                                                            float* dlg, const float* log_prior, const float* dlog_pi,
+                                                            float* dlp) {
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (g == 0 && dlp) {
+    float m = -__builtin_inff();
+    for (int k = 0; k < K; ++k) m = fmaxf(m, log_prior[k]);
+    float se = 0.f, s = 0.f;
+    for (int k = 0; k < K; ++k) {
+      se += expf(log_prior[k] - m);
+      s += dlog_pi ? dlog_pi[k] : 0.f;
+    }
+    for (int k = 0; k < K; ++k) dlp[k] = (dlog_pi ? dlog_pi[k] : 0.f) - expf(log_prior[k] - m) / se * s;
+  }
+  const int64_t r = g / K;
+  const int i = (int)(g - r * K);
+  if (r >= R) return;
+  const int L = ld4(K * K);
+  const float* lr = lg + r * L + i * K;
+  const float* ar = dA + r * L + i * K;
+  float m = -__builtin_inff();
+  for (int j = 0; j < K; ++j) m = fmaxf(m, lr[j]);
+  float se = 0.f, s = 0.f;
+  for (int j = 0; j < K; ++j) {
+    se += expf(lr[j] - m);
+    s += ar[j];
+  }
+  for (int j = 0; j < K; ++j) dlg[r * L + i * K + j] = ar[j] - expf(lr[j] - m) / se * s;
+  if (i == 0)
+    for (int c = K * K; c < L; ++c) dlg[r * L + c] = 0.f;
+}
+
+int launch_prior_lsm_bwd(const float* lg, const float* dA, int64_t R, int K, float* dlg, const float* log_prior,
+                         const float* dlog_pi, float* dlp, hipStream_t s) {
+  const int64_t n = R * K > 0 ? R * K : 1;
+  prior_lsm_bwd_kernel<<<(unsigned)cdiv(n, 256), 256, 0, s>>>(lg, dA, R, K, dlg, log_prior, dlog_pi, dlp);
+  VQHMM_LAUNCH_CHECK();
+  return VQHMM_OK;
+}
+
 // ------------------------------------------------------------ Adam
 // torch.optim.Adam (no weight decay, no amsgrad), as its foreach/fused CUDA path computes it:
 //   m = m + (1-b1)*(g-m);  v = b2*v + (1-b2)*g*g;

@@ -38,10 +38,109 @@ PARAM_ORDER = (
 _PtrArray = ctypes.c_void_p * _ext.NPARAMS
 
 
+def _tracks_grad(*tensors):
+    return torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in tensors)
+
+
 def _no_grad_through(name, *tensors):
-    if torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in tensors):
+    if _tracks_grad(*tensors):
         raise RuntimeError(f"vqhmm: autograd through {name}() alone is not implemented; "
                            "train through VAE_HMM.compute_loss (or call under torch.no_grad())")
+
+
+def _module_ws(d, B, T, device):
+    nb = ctypes.c_size_t()
+    _ext.check(_ext.load().vqhmm_module_bwd_workspace_size(ctypes.byref(d), B, T, ctypes.byref(nb)), "workspace")
+    return _workspace(device, nb.value), nb.value
+
+
+class _EncodeFn(torch.autograd.Function):
+    """Encoder.forward as one autograd node (VQ_VAE_HMM_fixed.py:38-41): forward vqhmm_encode_f32, backward
+    vqhmm_encode_bwd_f32 (the encoder's data and weight gradients on the HIP kernels)."""
+
+    @staticmethod
+    def forward(ctx, enc, x, *params):
+        ctx.dims = enc._dims()
+        ctx.save_for_backward(x, *params)
+        return enc._infer(x)
+
+    @staticmethod
+    def backward(ctx, glogits):
+        x, *params = ctx.saved_tensors
+        d = ctx.dims
+        B, _, T = x.shape
+        off = param_offsets(d)
+        grad = torch.zeros(off[-1], device=x.device)
+        dx = torch.empty_like(x) if ctx.needs_input_grad[1] else None
+        ws, nb = _module_ws(d, B, T, x.device)
+        w = [None] * _ext.NPARAMS
+        w[0:6] = params
+        _ext.check(_ext.load().vqhmm_encode_bwd_f32(ctypes.byref(d), _ptr_array(w), _ext.ptr(x),
+                                                    _ext.ptr(glogits.contiguous().float()), B, T, _ext.ptr(ws), nb,
+                                                    _ext.ptr(grad), _ext.ptr(dx), _ext.stream_ptr(x.device)),
+                   "encode backward")
+        return (None, dx, *[grad[off[i]:off[i + 1]].view_as(p) for i, p in enumerate(params)])
+
+
+class _DecodeFn(torch.autograd.Function):
+    """Decoder.forward as one autograd node (VQ_VAE_HMM_fixed.py:81-90): forward vqhmm_decode_f32, backward
+    vqhmm_decode_bwd_f32 (dq, and the embedding / conv / to_params gradients; the embedding's through the
+    composed conv1, dE = sum_{o,tap} dW'[o][k][tap] W[o][h][tap])."""
+
+    @staticmethod
+    def forward(ctx, dec, q, *params):
+        ctx.dims = dec._dims()
+        ctx.save_for_backward(q, *params)
+        return dec._infer(q)
+
+    @staticmethod
+    def backward(ctx, gmu, glogvar):
+        q, *params = ctx.saved_tensors
+        d = ctx.dims
+        B, _, T = q.shape
+        off = param_offsets(d)
+        grad = torch.zeros(off[-1], device=q.device)
+        dq = torch.empty_like(q) if ctx.needs_input_grad[1] else None
+        dpar = torch.cat([gmu, glogvar], 1).contiguous().float()  # [dmu | dlogvar]: to_params' output channels
+        ws, nb = _module_ws(d, B, T, q.device)
+        w = [None] * _ext.NPARAMS
+        w[11:18] = params
+        _ext.check(_ext.load().vqhmm_decode_bwd_f32(ctypes.byref(d), _ptr_array(w), _ext.ptr(q), _ext.ptr(dpar), B, T,
+                                                    _ext.ptr(ws), nb, _ext.ptr(grad), _ext.ptr(dq),
+                                                    _ext.stream_ptr(q.device)), "decode backward")
+        return (None, dq, *[grad[off[11 + i]:off[12 + i]].view_as(p) for i, p in enumerate(params)])
+
+
+class _ForwardFn(torch.autograd.Function):
+    """VAE_HMM.forward as one autograd node (VQ_VAE_HMM_fixed.py:139-143): (mu, logvar, q) by vqhmm_forward_f32;
+    backward vqhmm_forward_bwd_f32 through decode, the softmax of q and encode."""
+
+    @staticmethod
+    def forward(ctx, model, x, *params):
+        ctx.dims = model._dims()
+        ctx.save_for_backward(x, *params)
+        (mu, logvar), q = model._infer(x)
+        return mu, logvar, q
+
+    @staticmethod
+    def backward(ctx, gmu, glogvar, gq):
+        x, *params = ctx.saved_tensors
+        d = ctx.dims
+        B, _, T = x.shape
+        off = param_offsets(d)
+        grad = torch.zeros(off[-1], device=x.device)
+        dx = torch.empty_like(x) if ctx.needs_input_grad[1] else None
+        dpar = torch.cat([gmu, glogvar], 1).contiguous().float()
+        ws, nb = _module_ws(d, B, T, x.device)
+        w = [None] * _ext.NPARAMS
+        w[0:6] = params[0:6]
+        w[11:18] = params[6:13]
+        _ext.check(_ext.load().vqhmm_forward_bwd_f32(ctypes.byref(d), _ptr_array(w), _ext.ptr(x), _ext.ptr(dpar),
+                                                     _ext.ptr(gq.contiguous().float()), B, T, _ext.ptr(ws), nb,
+                                                     _ext.ptr(grad), _ext.ptr(dx), _ext.stream_ptr(x.device)),
+                   "forward backward")
+        idx = list(range(0, 6)) + list(range(11, 18))
+        return (None, dx, *[grad[off[i]:off[i + 1]].view_as(p) for i, p in zip(idx, params)])
 
 
 def _ptr_array(tensors):
@@ -73,12 +172,20 @@ class Encoder(nn.Module):
         K = self.to_logits.weight.shape[0]
         return _ext.Dims(D, H, K, H2, 1, 1)
 
+    def _params(self):
+        return [self.conv1.weight, self.conv1.bias, self.conv2.weight, self.conv2.bias, self.to_logits.weight,
+                self.to_logits.bias]
+
     def forward(self, x):
         _ext.require_device(x)
-        _no_grad_through("Encoder.forward", x, self.conv1.weight)
         if x.dim() != 3 or x.shape[1] != self.conv1.weight.shape[1]:
             raise RuntimeError(f"Encoder: expected input (B, {self.conv1.weight.shape[1]}, T), got {tuple(x.shape)}")
         x = x.contiguous().float()
+        if _tracks_grad(x, *self._params()):  # differentiable: the backward runs on the HIP kernels too
+            return _EncodeFn.apply(self, x, *self._params())
+        return self._infer(x)
+
+    def _infer(self, x):
         B, _, T = x.shape
         d = self._dims()
         lib = _ext.load()
@@ -89,8 +196,7 @@ class Encoder(nn.Module):
         _ext.check(lib.vqhmm_infer_workspace_size(ctypes.byref(d), B, T, ctypes.byref(nb)), "workspace")
         ws = _workspace(x.device, nb.value)
         w = [None] * _ext.NPARAMS
-        w[0:6] = [self.conv1.weight, self.conv1.bias, self.conv2.weight, self.conv2.bias,
-                  self.to_logits.weight, self.to_logits.bias]
+        w[0:6] = self._params()
         _ext.check(lib.vqhmm_encode_f32(ctypes.byref(d), _ptr_array(w), _ext.ptr(x), B, T, _ext.ptr(logits),
                                         _ext.ptr(ws), nb.value, _ext.stream_ptr(x.device)), "encode")
         return logits
@@ -168,11 +274,17 @@ class Decoder(nn.Module):
 
     def forward(self, q):
         _ext.require_device(q)
-        _no_grad_through("Decoder.forward", q, self.conv1.weight)
         d = self._dims()
         if q.dim() != 3 or q.shape[1] != d.K:
             raise RuntimeError(f"Decoder: expected q of shape (B, {d.K}, T), got {tuple(q.shape)}")
         q = q.contiguous().float()
+        params = self._ptrs()[11:18]
+        if _tracks_grad(q, *params):  # differentiable: the backward runs on the HIP kernels too
+            return _DecodeFn.apply(self, q, *params)
+        return self._infer(q)
+
+    def _infer(self, q):
+        d = self._dims()
         B, _, T = q.shape
         mu = torch.empty((B, d.input_dim, T), device=q.device)
         logvar = torch.empty((B, d.input_dim, T), device=q.device)
@@ -277,8 +389,14 @@ class VAE_HMM(nn.Module):
 
     def forward(self, x):
         _ext.require_device(x)
-        _no_grad_through("VAE_HMM.forward", x, self.encoder.conv1.weight)
         x = x.contiguous().float()
+        params = self.encoder._params() + self.decoder._ptrs()[11:18]
+        if _tracks_grad(x, *params):  # differentiable: the backward runs on the HIP kernels too
+            mu, logvar, q = _ForwardFn.apply(self, x, *params)
+            return (mu, logvar), q
+        return self._infer(x)
+
+    def _infer(self, x):
         B, _, T = x.shape
         d = self._dims()
         mu = torch.empty((B, d.input_dim, T), device=x.device)
