@@ -274,6 +274,15 @@ int vqhmm_decode_bwd_f32(const vqhmm_dims_t* dims, const float* const* params, c
 int vqhmm_forward_bwd_f32(const vqhmm_dims_t* dims, const float* const* params, const float* x,
                           const float* dpar, const float* dq, int64_t B, int64_t T, void* workspace,
                           size_t ws_bytes, float* grad, float* dx, void* stream);
+/* Autograd of Prior.forward (VQ_VAE_HMM_fixed.py:59-71) alone: dlog_pi (K, nullable = 0) and dlog_A
+ * (B,T,K,K) -> grad's prior.* entries (log_prior, transition_net.0/.2 weight and bias; nothing else is
+ * written) and du (nullable; CF (B, U, T) whatever u_layout).  Recomputes the MLP into the workspace
+ * (vqhmm_prior_bwd_workspace_size), then the log_softmax backwards, the hidden layer's masked data
+ * gradient, du, the two weight gradients and one fixed-order slab reduction. */
+int vqhmm_prior_bwd_workspace_size(const vqhmm_dims_t* dims, int64_t B, int64_t T, size_t* bytes);
+int vqhmm_prior_bwd_f32(const vqhmm_dims_t* dims, const float* const* params, const float* u, int u_layout,
+                        const float* dlog_pi, const float* dlog_A, int64_t B, int64_t T, void* workspace,
+                        size_t ws_bytes, float* grad, float* du, void* stream);
 
 /* ------------------------------------------- fused Prior -> Viterbi ----
  * the Viterbi path of vqhmm_viterbi_f32 over the tables vqhmm_prior_f32 would write

@@ -113,3 +113,33 @@ def test_forward_autograd_vs_oracle(use_q):
             continue
         _close(prm.grad, p[k].grad, k)
     _close(xg.grad, x64.grad, "dx")
+
+
+@pytest.mark.parametrize("B,T,K,lay,with_pi", [(16, 50, 3, 0, True), (8, 200, 4, 1, True), (5, 33, 8, 0, False)])
+def test_prior_autograd_vs_oracle(B, T, K, lay, with_pi):
+    """Prior.forward alone (:59-71) in either u layout: log_prior / transition_net gradients and du."""
+    m = _model(K=K, seed=4)
+    g = torch.Generator().manual_seed(13 * B + T)
+    u = torch.randn(B, 4, T, generator=g)
+    if lay == 1:
+        u = u.transpose(1, 2).contiguous()
+    Gpi, GA = torch.randn(K, generator=g), torch.randn(B, T, K, K, generator=g)
+    ug = u.cuda().requires_grad_(True)
+    log_pi, log_A = m.prior(ug)
+    loss = (log_A * GA.cuda()).sum() + ((log_pi * Gpi.cuda()).sum() if with_pi else 0.0)
+    loss.backward()
+    p = _p64(m)
+    u64 = u.double().requires_grad_(True)
+    rpi, rA = RM.prior_tables(p, u64, K, 4)
+    _close(log_A, rA, "log_A")
+    rl = (rA * GA.double()).sum() + ((rpi * Gpi.double()).sum() if with_pi else 0.0)
+    rl.backward()
+    for k, prm in m.named_parameters():
+        if not k.startswith("prior."):
+            assert prm.grad is None, k
+            continue
+        if k == "prior.log_prior" and not with_pi:
+            assert prm.grad is None or prm.grad.abs().max() == 0, k
+            continue
+        _close(prm.grad, p[k].grad, k)
+    _close(ug.grad, u64.grad, "du")

@@ -285,10 +285,11 @@ def test_strip_head_matches_head_launch(tmp_path, dims, bt):
 @pytest.mark.parametrize("dims,bt", [((5, 64, 3, 32, 128), (96, 150)), ((3, 64, 2, 32, 64), (40, 77)),
                                      ((5, 64, 4, 31, 128), (8, 50)), ((4, 64, 3, 29, 128), (30, 200)),
                                      ((5, 64, 3, 32, 128), (128, 200)),   # the cfg2 N = 8 shard: 249 strips of 104
-                                     ((5, 64, 3, 32, 128), (256, 150))])  # 512 strips: two per workgroup
+                                     ((5, 64, 3, 32, 128), (256, 150)),   # 512 strips: two per workgroup
+                                     ((5, 64, 3, 32, 128), (1024, 200))])  # cfg2: 206k rows, 7 rounds
 def test_strip_wgrad_fold_matches_grouped(tmp_path, dims, bt):
-    """The six weight gradients folded into the backward strip launch (strip_bwdw.hip, the default below 2^17
-    rows) against the grouped weight-gradient launch (VQHMM_STRIP_WGRAD=0): the data-gradient chain is the
+    """The six weight gradients folded into the backward strip launch (strip_bwdw.hip, the default) against the
+    grouped weight-gradient launch (VQHMM_STRIP_WGRAD=0; above 2^17 rows with the backward pair too): the data-gradient chain is the
     same code, the weight / bias gradients sum per strip workgroup instead of per row chunk, so loss and
     gradients agree within 1e-6 (and every step's gradient against the oracle: test_strong_scaling_shards_*)."""
     out = _run_both_tol(tmp_path, "VQHMM_STRIP_WGRAD", dims, bt)

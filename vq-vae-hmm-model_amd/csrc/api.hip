@@ -651,29 +651,34 @@ bool bwd_pair_fused(const ElboPlan& p, const float* const* w, const float* gscal
 
 // The backward's four data-gradient convolutions as one strip launch (strip.hip) where its shapes apply;
 // VQHMM_STRIP_BWD=0 keeps the pair launches (A/B), read once
-bool strip_bwd_on(const ElboPlan& p) {
+// the backward strip's shape / switch conditions, without the row threshold
+bool strip_bwd_shape_ok(const ElboPlan& p) {
   static const bool on = [] {
     const char* e = VQHMM_ENV("VQHMM_STRIP_BWD");
     return !e || atoi(e) != 0;
   }();
-  // measured (tools/gpu_stripab.sh): B = 128 0.124 -> 0.116 ms, 256 0.1765 -> 0.1715, 512 0.2784 -> 0.2761,
-  // cfg2 (207k rows) 0.462 -> 0.467: below 2^17 rows only, as the backward pair
-  static const int64_t max_rows = [] {  // A/B: VQHMM_STRIP_BWD_ROWS
-    const char* e = VQHMM_PROF_ENV("VQHMM_STRIP_BWD_ROWS");
-    return e ? (int64_t)atoll(e) : (int64_t)1 << 17;
-  }();
-  return on && p.R < max_rows && logits_dg_fused(p) &&
+  return on && logits_dg_fused(p) &&
          strip_bwd_supported(conv_of(p, nullptr, S_PAR_DG), conv_of(p, nullptr, S_DEC2_DG), dec1_dg_args(p, nullptr, nullptr),
                              conv_of(p, nullptr, S_ENC2_DG));
 }
 
-// The six weight gradients folded into the backward strip launch (strip_bwdw.hip): wherever the backward
-// strip runs and its packed-tap weight-gradient tiles apply (D <= 5, K <= 4); VQHMM_STRIP_WGRAD=0 keeps the
-// grouped launch
+// The six weight gradients folded into the backward strip (strip_bwdw.hip) at any row count: measured
+// (tools/gpu_ab_rows.sh) cfg2 (207k rows) 0.4483 -> 0.4352 ms against the backward pair + grouped wgrad
 bool strip_wfold_planned(const ElboPlan& p) {
-  return strip_wgrad_env() && strip_bwd_on(p) &&
+  return strip_wgrad_env() && strip_bwd_shape_ok(p) &&
          strip_bwdw_supported(conv_of(p, nullptr, S_PAR_DG), conv_of(p, nullptr, S_DEC2_DG), dec1_dg_args(p, nullptr, nullptr),
                               conv_of(p, nullptr, S_ENC2_DG), p.D);
+}
+
+bool strip_bwd_on(const ElboPlan& p) {
+  // measured (tools/gpu_stripab.sh): B = 128 0.124 -> 0.116 ms, 256 0.1765 -> 0.1715, 512 0.2784 -> 0.2761,
+  // cfg2 (207k rows) 0.462 -> 0.467: without the folded weight gradients below 2^17 rows only, as the
+  // backward pair; with them (p.wfold) at every row count
+  static const int64_t max_rows = [] {  // A/B: VQHMM_STRIP_BWD_ROWS
+    const char* e = VQHMM_PROF_ENV("VQHMM_STRIP_BWD_ROWS");
+    return e ? (int64_t)atoll(e) : (int64_t)1 << 17;
+  }();
+  return (p.R < max_rows || p.wfold) && strip_bwd_shape_ok(p);
 }
 
 // VQHMM_TAIL_FUSED=0 (grouped weight gradients): the tail without Adam, then the Adam launch (A/B; the

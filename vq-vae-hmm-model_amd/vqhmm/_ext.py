@@ -78,6 +78,9 @@ _SIGS = {
     "vqhmm_forward_f32": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(c_vp), c_vp, c_i64, c_i64, c_vp,
                                          c_vp, c_vp, c_vp, c_sz, c_vp]),
     "vqhmm_module_bwd_workspace_size": (ctypes.c_int, [ctypes.POINTER(Dims), c_i64, c_i64, ctypes.POINTER(c_sz)]),
+    "vqhmm_prior_bwd_workspace_size": (ctypes.c_int, [ctypes.POINTER(Dims), c_i64, c_i64, ctypes.POINTER(ctypes.c_size_t)]),
+    "vqhmm_prior_bwd_f32": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(c_vp), c_vp, ctypes.c_int, c_vp, c_vp,
+                                           c_i64, c_i64, c_vp, ctypes.c_size_t, c_vp, c_vp, c_vp]),
     "vqhmm_encode_bwd_f32": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(c_vp), c_vp, c_vp, c_i64, c_i64,
                                             c_vp, c_sz, c_vp, c_vp, c_vp]),
     "vqhmm_decode_bwd_f32": (ctypes.c_int, [ctypes.POINTER(Dims), ctypes.POINTER(c_vp), c_vp, c_vp, c_i64, c_i64,

@@ -42,12 +42,6 @@ def _tracks_grad(*tensors):
     return torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in tensors)
 
 
-def _no_grad_through(name, *tensors):
-    if _tracks_grad(*tensors):
-        raise RuntimeError(f"vqhmm: autograd through {name}() alone is not implemented; "
-                           "train through VAE_HMM.compute_loss (or call under torch.no_grad())")
-
-
 def _module_ws(d, B, T, device):
     nb = ctypes.c_size_t()
     _ext.check(_ext.load().vqhmm_module_bwd_workspace_size(ctypes.byref(d), B, T, ctypes.byref(nb)), "workspace")
@@ -143,6 +137,41 @@ class _ForwardFn(torch.autograd.Function):
         return (None, dx, *[grad[off[i]:off[i + 1]].view_as(p) for i, p in zip(idx, params)])
 
 
+class _PriorFn(torch.autograd.Function):
+    """Prior.forward as one autograd node (VQ_VAE_HMM_fixed.py:59-71): forward vqhmm_prior_f32, backward
+    vqhmm_prior_bwd_f32 (the two log_softmax backwards, the MLP's data and weight gradients, du)."""
+
+    @staticmethod
+    def forward(ctx, prior, u, lay, *params):
+        ctx.dims, ctx.lay = prior._dims(), lay
+        ctx.save_for_backward(u, *params)
+        return prior._infer(u, lay)
+
+    @staticmethod
+    def backward(ctx, gpi, gA):
+        u, *params = ctx.saved_tensors
+        d, lay = ctx.dims, ctx.lay
+        B = u.shape[0]
+        T = u.shape[2] if lay == 0 else u.shape[1]
+        off = param_offsets(d)
+        grad = torch.zeros(off[-1], device=u.device)
+        du = torch.empty((B, d.u_dim, T), device=u.device) if ctx.needs_input_grad[1] else None
+        lib = _ext.load()
+        nb = ctypes.c_size_t()
+        _ext.check(lib.vqhmm_prior_bwd_workspace_size(ctypes.byref(d), B, T, ctypes.byref(nb)), "workspace")
+        ws = _workspace(u.device, nb.value)
+        w = [None] * _ext.NPARAMS
+        w[6:11] = params
+        gpi = None if gpi is None else gpi.contiguous().float()
+        gA = torch.zeros((B, T, d.K, d.K), device=u.device) if gA is None else gA.contiguous().float()
+        _ext.check(lib.vqhmm_prior_bwd_f32(ctypes.byref(d), _ptr_array(w), _ext.ptr(u), lay, _ext.ptr(gpi),
+                                           _ext.ptr(gA), B, T, _ext.ptr(ws), nb.value, _ext.ptr(grad), _ext.ptr(du),
+                                           _ext.stream_ptr(u.device)), "prior backward")
+        if du is not None and lay == 1:
+            du = du.transpose(1, 2)
+        return (None, du, None, *[grad[off[6 + i]:off[7 + i]].view_as(p) for i, p in enumerate(params)])
+
+
 def _ptr_array(tensors):
     arr = _PtrArray()
     for i, t in enumerate(tensors):
@@ -226,22 +255,33 @@ class Prior(nn.Module):
             return 1
         raise RuntimeError(f"Prior: expected u of shape (B, {self.u_dim}, T) or (B, T, {self.u_dim}), got {tuple(u.shape)}")
 
+    def _dims(self):
+        lin0 = self.transition_net[0]
+        return _ext.Dims(1, 1, self.K, 1, self.u_dim, lin0.weight.shape[0])
+
+    def _params(self):
+        lin0, lin2 = self.transition_net[0], self.transition_net[2]
+        return [self.log_prior, lin0.weight, lin0.bias, lin2.weight, lin2.bias]
+
     def forward(self, u=None):
         if u is None:
             raise ValueError('u required for non-stationary transitions')
         _ext.require_device(u)
-        _no_grad_through("Prior.forward", u, self.log_prior)
         lay = self.u_layout(u)
         u = u.contiguous().float()
+        if _tracks_grad(u, *self._params()):  # differentiable: the backward runs on the HIP kernels too
+            return _PriorFn.apply(self, u, lay, *self._params())
+        return self._infer(u, lay)
+
+    def _infer(self, u, lay):
         B = u.shape[0]
         T = u.shape[2] if lay == 0 else u.shape[1]
         K = self.K
-        lin0, lin2 = self.transition_net[0], self.transition_net[2]
-        d = _ext.Dims(1, 1, K, 1, self.u_dim, lin0.weight.shape[0])
+        d = self._dims()
         log_pi = torch.empty(K, device=u.device)
         log_A = torch.empty((B, T, K, K), device=u.device)
         w = [None] * _ext.NPARAMS
-        w[6:11] = [self.log_prior, lin0.weight, lin0.bias, lin2.weight, lin2.bias]
+        w[6:11] = self._params()
         _ext.check(_ext.load().vqhmm_prior_f32(ctypes.byref(d), _ptr_array(w), _ext.ptr(u), lay, B, T,
                                                _ext.ptr(log_pi), _ext.ptr(log_A), _ext.stream_ptr(u.device)), "prior")
         return log_pi, log_A
