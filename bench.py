@@ -97,7 +97,7 @@ def stage_timings(lib, st, x, u, L, B, T, beta, nsteps):
         st.apply_adam()
     torch.cuda.synchronize()
     out = []
-    name = ctypes.create_string_buffer(64)
+    name = ctypes.create_string_buffer(256)
     fl, by, mf = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
     for s in range(n):
         us = statistics.median(ev[k][s].elapsed_time(ev[k][s + 1]) * 1e3 for k in range(nsteps))
