@@ -369,6 +369,7 @@ struct TailArgs {
   float* fin_loss;
   double* fin_accum;
   float* fin_pieces;
+  int dbg;  // profiling build only (VQHMM_TAIL_DBG): 1 skip segment reductions, 2 log_prior, 4 loss, 8 Adam
 };
 // torch.optim.Adam over the flat buffers (misc.hip adam_kernel / compose_adam_kernel)
 struct AdamArgs {

@@ -202,21 +202,39 @@ __device__ int tail_segment_block(const TailArgs& ta, float (&part)[16][64], flo
   return si;
 }
 
-// log_prior gradient (VQ_VAE_HMM_fixed.py:71,:123,:131) from the q0 slab; thread 0 writes lp.out.
-__device__ void tail_logprior_block(const TailArgs& ta, float* red, float* scratch) {
+// log_prior gradient (VQ_VAE_HMM_fixed.py:71,:123,:131) from the q0 slab, and (ADAM) its Adam update:
+// thread k < K owns element k; its log_prior value and Adam operands are loaded before the slab reduction,
+// thread 0 forms the max / sum terms from LDS in the fixed order (k ascending).
+template <bool ADAM>
+__device__ void tail_logprior_block(const TailArgs& ta, float* red, float* scratch, const AdamArgs& ad, int64_t tn,
+                                    const float* g) {
   const LogPriorGradArgs& lp = ta.lp;
-  const int K = lp.K;
-  block_reduce_cols(ta.q0slab, ta.q0chunks, K, 0, K, red, scratch);
-  if (threadIdx.x == 0) {
-    const float c = -lp.beta / loss_norm_batch(lp.norm, lp.B);
-    const float sc = lp.scale ? *lp.scale : 1.f;
+  const int K = lp.K, tid = threadIdx.x;
+  __shared__ float lsum[3];
+  const float lpk = tid < K ? lp.log_prior[tid] : 0.f;
+  AdamElem e{};
+  if (ADAM && tid < K) e = adam_load(ad, (lp.out - g) + tid, tn);
+  block_reduce_cols(ta.q0slab, ta.q0chunks, K, 0, K, red, scratch);  // ends with a barrier
+  if (tid < K) scratch[tid] = lpk;
+  __syncthreads();
+  const float c = -lp.beta / loss_norm_batch(lp.norm, lp.B);
+  if (tid == 0) {
     float m = -__builtin_inff();
-    for (int k = 0; k < K; ++k) m = fmaxf(m, lp.log_prior[k]);
+    for (int k = 0; k < K; ++k) m = fmaxf(m, scratch[k]);
     float se = 0.f;
-    for (int k = 0; k < K; ++k) se += __expf(lp.log_prior[k] - m);
+    for (int k = 0; k < K; ++k) se += __expf(scratch[k] - m);
     float tot = 0.f;
     for (int k = 0; k < K; ++k) tot += c * red[k];
-    for (int k = 0; k < K; ++k) lp.out[k] = sc * (c * red[k] - __expf(lp.log_prior[k] - m) / se * tot);
+    lsum[0] = m;
+    lsum[1] = se;
+    lsum[2] = tot;
+  }
+  __syncthreads();
+  if (tid < K) {
+    const float sc = lp.scale ? *lp.scale : 1.f;
+    const float v = sc * (c * red[tid] - __expf(lpk - lsum[0]) / lsum[1] * lsum[2]);
+    lp.out[tid] = v;
+    if constexpr (ADAM) adam_apply(ad, (lp.out - g) + tid, v, e);
   }
 }
 
@@ -319,17 +337,20 @@ __global__ __launch_bounds__(256) void tail_kernel(TailArgs ta, AdamArgs ad, con
     }
     float v = 0.f;
     int64_t col;
-    const int si = tail_segment_block(ta, part, red, scratch, &v, &col);
+    int si = 0;
+    if (ta.dbg & 1) {
+      while (si + 1 < ta.nseg && b >= ta.blk_start[si + 1]) ++si;
+      col = (b - ta.blk_start[si]) * 64 + threadIdx.x;
+    } else {
+      si = tail_segment_block(ta, part, red, scratch, &v, &col);
+    }
     const SlabSeg& sg = ta.s[si];
-    if (ADAM && threadIdx.x < 64 && col < sg.len) adam_apply(ad, (sg.out - g) + col, v, e);
+    if (ADAM && !(ta.dbg & 8) && threadIdx.x < 64 && col < sg.len) adam_apply(ad, (sg.out - g) + col, v, e);
   } else if (ta.q0slab && b == nblk) {
-    tail_logprior_block(ta, red, scratch);
-    if (ADAM && threadIdx.x == 0)
-      for (int k = 0; k < ta.lp.K; ++k) {
-        const int64_t i = (ta.lp.out - g) + k;
-        adam_apply(ad, i, ta.lp.out[k], adam_load(ad, i, tn));
-      }
+    if (ta.dbg & 2) return;
+    tail_logprior_block<ADAM>(ta, red, scratch, ad, tn, g);
   } else if (ta.fin_loss && b == finb) {
+    if (ta.dbg & 4) return;
     __shared__ double fred[5 * 256];
     finalize_loss_block(ta.fin_part, ta.fin_nblk, nullptr, ta.lp.norm, ta.fin_B, ta.fin_T, ta.fin_D, ta.lp.beta,
                         ta.fin_loss, ta.fin_accum, ta.fin_pieces, fred, ta.fin_cnt);
@@ -340,6 +361,10 @@ int launch_tail(TailArgs& ta, const AdamArgs* adam, const float* g, hipStream_t 
   if (ta.nseg > MAX_SEGS || (ta.q0slab && ta.lp.K > 256)) return VQHMM_EINVAL;
   for (int i = 0; i < ta.nseg; ++i)
     if (ta.s[i].cmpE && composed_block_cols(ta.s[i].cmpH, ta.s[i].cmpK) > 256) return VQHMM_EINVAL;
+  {
+    static const char* dbg = VQHMM_PROF_ENV("VQHMM_TAIL_DBG");
+    ta.dbg = dbg ? atoi(dbg) : 0;
+  }
   ta.blk_start[0] = 0;
   for (int i = 0; i < ta.nseg; ++i) ta.blk_start[i + 1] = ta.blk_start[i] + cdiv(ta.s[i].len, 64);
   const int64_t nb = ta.blk_start[ta.nseg] + (ta.q0slab ? 1 : 0) + (ta.fin_loss ? 1 : 0);
