@@ -1,7 +1,7 @@
 """Phase timings of the backward strip with the folded weight gradients (strip_bwdw.hip; profiling build:
 VQHMM_LIB_PATH=vqhmm/libvqhmm_prof.so VQHMM_STRIP_PROF=1): per-workgroup s_memrealtime stamps (100 MHz) of
 the first strip's phases, medians / maxima over workgroups, and the in-kernel clock (s_memtime).
-usage: VQHMM_STRIP_PROF=1 python tools/bwdw_prof.py [B ...]"""
+usage: VQHMM_STRIP_PROF=1 [VQHMM_STRIP_PROF_IT=n] python tools/bwdw_prof.py [B ...]  (strip n of each workgroup, default 0)"""
 import ctypes
 import os
 import sys
@@ -34,6 +34,10 @@ def run(B, T=200, D=5, H=64, K=3, H2=32):
     _ext.check(_ext.load().vqhmm_debug_prof(3, buf.ctypes.data_as(ctypes.c_void_p), buf.size), "debug_prof")
     t = buf.reshape(256, 16).astype(np.int64)
     t = t[t[:, 9] > 0]
+    pit = int(os.environ.get("VQHMM_STRIP_PROF_IT", "0"))
+    if pit > 0:  # a later strip (VQHMM_STRIP_PROF_IT): its phases from its own start stamp; "slabs" = the rest
+        t = t[t[:, 9] > pit]
+        t[:, 0] = t[:, 15]
     d = np.diff(t[:, :9], axis=1) * 0.01  # us
     t0 = t[:, 0].min()
     ghz = (t[:, 14] - t[:, 13]) / ((t[:, 8] - t[:, 0]) * 10.0)

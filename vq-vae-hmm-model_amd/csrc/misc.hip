@@ -323,7 +323,11 @@ __global__ __launch_bounds__(256) void tail_kernel(TailArgs ta, AdamArgs ad, con
   __shared__ float part[16][64];
   __shared__ float red[256];
   __shared__ float scratch[256];
-  const int64_t tn = ADAM ? (*ad.step & 0xffffffffll) : 0;
+  // the step count as a VECTOR load (opaque zero index): a scalar load's cache miss would hold the lgkmcnt(0)
+  // before every kernel-argument pointer use (scalar loads return out of order), i.e. every block's first loads
+  int z0 = 0;
+  asm volatile("" : "+v"(z0));
+  const int64_t tn = ADAM ? (ad.step[z0] & 0xffffffffll) : 0;
   const int64_t nblk = ta.blk_start[ta.nseg];
   const int64_t b = blockIdx.x;
   const int64_t finb = nblk + (ta.q0slab ? 1 : 0);

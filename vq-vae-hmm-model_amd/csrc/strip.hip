@@ -214,16 +214,18 @@ __device__ __forceinline__ void tail_epi(f32x4 (&acc)[NB], const TailConsts<NB>&
   }
 }
 
-// element i of a [bias (NW) | tail weight (16 x NW) | tail bias (16)] block
+// the source address of element i of a [bias (NW) | tail weight (16 x NW) | tail bias (16)] block, branch-free
+// (selects only, so a caller's loads of several entries are all in flight before one wait: a branchy form's
+// loads each ended in a vmcnt(0) at the branch join, ~10 serialized loads of staging); !ok -> the entry is 0
+// and the returned address is the (valid) bias pointer
 template <int NW>
-__device__ __forceinline__ float es_val(const float* bias, int N, const float* tW, const float* tb, int C2, int i) {
-  if (i < NW) return i < N ? bias[i] : 0.f;
-  if (i < 17 * NW) {
-    const int j = i - NW, c2 = j / NW, n = j - c2 * NW;
-    return (c2 < C2 && n < N) ? tW[(int64_t)c2 * N + n] : 0.f;
-  }
-  const int c2 = i - 17 * NW;
-  return c2 < C2 ? tb[c2] : 0.f;
+__device__ __forceinline__ const float* es_src(const float* bias, int N, const float* tW, const float* tb, int C2, int i,
+                                               bool& ok) {
+  const bool in_b = i < NW, in_w = !in_b && i < 17 * NW;
+  const int j = in_w ? i - NW : 0, c2w = j / NW, n = j - c2w * NW, c2b = (!in_b && !in_w) ? i - 17 * NW : 0;
+  ok = in_b ? i < N : in_w ? (c2w < C2 && n < N) : c2b < C2;
+  const float* p = in_b ? bias + i : in_w ? tW + ((int64_t)c2w * N + n) : tb + c2b;
+  return ok ? p : bias;
 }
 
 template <int CTRL>
@@ -334,19 +336,31 @@ __global__ __launch_bounds__(512) void strip_fwd_kernel(StripFwdArgs a, HeadArgs
   constexpr int NE = NW2 * 17 + 16, ND = 64 * 17 + 16, NC = NE + ND + 128;  // sh.Ee2 | sh.Ed2 | sh.bf
   constexpr int NCJ = (NC + 511) / 512;
   float cv[NCJ];
+  bool cvok[NCJ];
 #pragma unroll
   for (int j = 0; j < NCJ; ++j) {
     const int i = tid + 512 * j;
-    float v = 0.f;
-    if (i < NE) v = es_val<NW2>(a.b_e2, a.H2, a.tWl, a.tbl, a.K, i);
-    else if (i < NE + ND) v = es_val<64>(a.b_d2, 64, a.tWp, a.tbp, a.P, i - NE);
-    else if (i < NC) v = (i - NE - ND < 64 ? a.b_e1 : a.b_d1)[(i - NE - ND) & 63];
-    cv[j] = v;
+    bool oke, okd;
+    const float* pe = es_src<NW2>(a.b_e2, a.H2, a.tWl, a.tbl, a.K, i < NE ? i : 0, oke);
+    const float* pd = es_src<64>(a.b_d2, 64, a.tWp, a.tbp, a.P, (i >= NE && i < NE + ND) ? i - NE : 0, okd);
+    const int ib = (i >= NE + ND && i < NC) ? i - NE - ND : 0;
+    const bool inE = i < NE, inD = !inE && i < NE + ND, inB = !inE && !inD && i < NC;
+    const bool ok = inE ? oke : inD ? okd : inB;
+    const float* p = inE ? pe : inD ? pd : (ib < 64 ? a.b_e1 : a.b_d1) + (ib & 63);
+    cv[j] = *(ok ? p : a.b_e1);  // every entry's load in flight; the mask after the loop
+    cvok[j] = ok;
   }
+#pragma unroll
+  for (int j = 0; j < NCJ; ++j) cv[j] = cvok[j] ? cv[j] : 0.f;
   {
     constexpr int N1 = 3 * NW2 * ST_LDW / 4, N2 = 3 * 64 * ST_LDW / 4;  // float4s of each image
     constexpr int C1 = (N1 + 63) / 64, C2 = (N2 + 63) / 64;              // one wave instruction = 1 KB
-    for (int c = wave; c < C1 + C2; c += 8) {
+    // a fixed count per wave (the last chunk copied again where a wave has fewer: the same bytes), so the
+    // compiler counts these in vmcnt and its waits for x / the constants below leave them in flight
+    constexpr int NJ = (C1 + C2 + 7) / 8;
+#pragma unroll
+    for (int jj = 0; jj < NJ; ++jj) {
+      const int c = min(wave + 8 * jj, C1 + C2 - 1);
       const bool first = c < C1;
       const int cc = first ? c : c - C1;
       const int i = cc * 64 + lane;

@@ -37,6 +37,8 @@
 
 namespace vqhmm {
 
+__device__ float g_bwdw_one = 1.0f;  // the scale behind a null scale pointer
+
 namespace {
 constexpr int SW_LDD = 24;  // dpar rows in LDS (ldp <= 16 channels; 2 * 24 = 16 mod 32: conflict-free column reads)
 constexpr int SW_LDQ = 8;   // q / x / dlog rows in LDS
@@ -46,7 +48,7 @@ struct StripWLds {
   float RS[8 * 18 * ST_LDW];        // 10368
   float RG[ST_WIN * ST_LDW];        // 9216
   float RD[(ST_WIN + 2) * SB_LDE];  // 5200
-  float RC[3 * 4 * ST_LDW];         // 864
+  float RC[4 * 256];                // 3 * 4 * ST_LDW = 864 used; padded to four whole 1-KB DMA chunks
   float RE[ST_WIN * SW_LDQ];        // 1024
   float TW[4 * 32];                 // to_logits' weight (K <= 4, H2 <= 32), zero-padded
 };
@@ -73,6 +75,7 @@ struct SWArgs {
   float* cslab;
   int64_t* step_inc;
   int64_t nstrip;
+  int prof_it;  // profiling build: the strip index (per workgroup) whose phases are stamped
 };
 
 // c2_mfma_tile<1, 1, 4, 3, ST_LDW, 16>'s pipelined sequence on a compact image holding only output rows
@@ -207,29 +210,33 @@ __global__ __launch_bounds__(512) void strip_bwdw_kernel(SWArgs a, ConvArgs f) {
   stamp<PROF>(0);
   if constexpr (PROF > 0) { if (tid == 0 && blockIdx.x < 256) g_prof[blockIdx.x * 16 + 13] = __builtin_amdgcn_s_memtime(); }
   const int K = a.K, D = a.D;  // packed-tap gathers (k = 3, 3 C <= 16): B column j = l16 -> (tap, c)
-  // the device scalars first: a wait for them (the compiler copies them before the loop) then covers no DMA
-  const float psc = a.gscale ? *a.gscale : 1.0f;
-  const float fsc = f.scale ? *f.scale : 1.0f;
-  const float lsc = f.lb_scale ? *f.lb_scale : 1.0f;
   // ---- once: the compact composed dec_conv1 image (rows n < 4 of each tap) by LDS DMA (to_logits' weight goes
   // to LDS in the first strip's P3)
+  // to_logits' weight (K, H2) zero-padded to [4][32] (dec1_epi), through registers, its load ahead of the DMA
+  float twv = 0.f;
+  if (tid < 128) {
+    const int k = tid >> 5, c = tid & 31;
+    twv = (k < K && c < a.H2) ? f.lb_W[k * a.H2 + c] : 0.f;
+  }
   {
     constexpr int NC = 3 * 4 * ST_LDW / 4;  // float4s: tap t's rows 0..3 are 72 float4s at image row 16 t
-    for (int c = wave; c * 64 < NC; c += 8) {
-      const int i = c * 64 + lane;
-      if (i < NC) dma16(a.img_c1 + ((i / 72) * 16 * ST_LDW + (i % 72) * 4), sh.RC + c * 256);
-    }
+    static_assert(NC <= 4 * 64 && sizeof(StripWLds::RC) == 4 * 1024, "one whole-chunk DMA per wave");
+    // ONE unguarded instruction in every wave (waves 4-7 copy chunk 3 again, lanes past the image its last
+    // float4 into RC's padding: the same bytes), so no branch joins and the compiler counts it exactly
+    const int c = min(wave, 3);
+    const int i = min(c * 64 + lane, NC - 1);
+    dma16(a.img_c1 + ((i / 72) * 16 * ST_LDW + (i % 72) * 4), sh.RC + c * 256);
   }
+  if (tid < 128) sh.TW[tid] = twv;
   // the dec_conv2 image, 7 DMA instructions in every wave (54 1-KB chunks; waves 6 and 7 copy chunk 53 twice,
   // the same bytes): the first strip waits for its P1 loads with a counted vmcnt that leaves these in flight
   auto dma_d2 = [&]() __attribute__((always_inline)) {
-    constexpr int N1 = 3 * 64 * ST_LDW / 4, C1 = (N1 + 63) / 64;
-    static_assert(C1 <= 56, "7 chunks per wave");
+    constexpr int N1 = 3 * 64 * ST_LDW / 4, C1 = N1 / 64;
+    static_assert(N1 % 64 == 0 && C1 <= 56, "7 whole chunks per wave");
 #pragma unroll
-    for (int j = 0; j < 7; ++j) {
+    for (int j = 0; j < 7; ++j) {  // unguarded (no branch join: the compiler counts these exactly)
       const int c = min(wave + 8 * j, C1 - 1);
-      const int i = c * 64 + lane;
-      if (i < N1) dma16(a.img_d2 + 4 * i, sh.RW + c * 256);
+      dma16(a.img_d2 + 4 * (c * 64 + lane), sh.RW + c * 256);
     }
   };
 
@@ -314,6 +321,15 @@ __global__ __launch_bounds__(512) void strip_bwdw_kernel(SWArgs a, ConvArgs f) {
     // being hoisted out of the loop as 64-bit VGPR pairs (the accumulators need those registers)
     int tidv = tid;
     asm volatile("" : "+v"(tidv));
+    if (it == a.prof_it) stamp<PROF>(15);  // the profiled strip's start (VQHMM_STRIP_PROF_IT)
+    // the device scalars, per strip (L2-hot after the first), as VECTOR loads (opaque zero index) issued ahead
+    // of P1's loads: waited with them.  Loaded once before the loop they cost the first strip a vmcnt(0)
+    // (a register copy of the value) that also waited for the compact image's DMA
+    // (unconditional: a null pointer selects the device constant 1; a branch per load would join before the DMA)
+    const int z0 = tidv >> 10;  // 0 (tidv < 512), opaque to the compiler
+    const float psc = (a.gscale ? a.gscale : &g_bwdw_one)[z0];
+    const float fsc = (f.scale ? f.scale : &g_bwdw_one)[z0];
+    const float lsc = (f.lb_scale ? f.lb_scale : &g_bwdw_one)[z0];
     const int lane = tidv & 63, lg4 = lane >> 4, l16 = lane & 15;
     const int rm = ((lg4 & 1) << 1) | (lg4 >> 1);  // rows 2 apart in each 32-lane half: conflict-free b32 reads
     const int qtap = l16 / K, qc = l16 - qtap * K;
@@ -352,26 +368,25 @@ __global__ __launch_bounds__(512) void strip_bwdw_kernel(SWArgs a, ConvArgs f) {
       };
       const bool extra = wave == 5 || wave == 6;
       const int64_t re = wave == 5 ? s0 - 1 : s0 + 16 * 7 + 1;
-      float4 mA[4], xA, mB[4], xB = make_float4(0.f, 0.f, 0.f, 0.f);
+      // every load of this phase unconditional (clamped addresses; only the waves that need a value use it):
+      // a branch join before the image DMA below would make the compiler drain vmcnt before the front
+      float4 mA[4], xA, mB[4], xB;
       load_mask(a.g2, rb, R, lg4, l16, mA);
       xA = ld_dpar_raw(rb + l16);
-      if (extra) {
-        load_mask(a.g2, re, R, lg4, l16, mB);
-        xB = ld_dpar_raw(re + l16);
-      }
-      float4 qv = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (tidv < ST_WIN) {
-        int64_t r = s0 + tidv;
+      load_mask(a.g2, re, R, lg4, l16, mB);  // waves 5 and 6: the window's outer rows
+      xB = ld_dpar_raw(re + l16);
+      float4 qv;
+      {
+        int64_t r = s0 + (tidv & (ST_WIN - 1));
         r = r < 0 ? 0 : (r >= R ? R - 1 : r);
-        qv = *reinterpret_cast<const float4*>(a.q + r * 4);  // ld4(K) = 4
+        qv = *reinterpret_cast<const float4*>(a.q + r * 4);  // ld4(K) = 4; rows of threads < ST_WIN
       }
       asm volatile("" ::: "memory");
-      if (it == 0) dma_d2();  // after this strip's loads: B1 below waits for those, not for the image
-      if (it == 0) stamp<PROF>(10);
+      if (it == a.prof_it) stamp<PROF>(10);
       f32x4 acc[4];
       front(dpar_mask(rb + l16, xA), acc);
       if constexpr (PROF > 0) {
-        if (it == 0) {
+        if (it == a.prof_it) {
           asm volatile("s_nop 0" : : "v"(acc[3][3]));
           stamp<PROF>(11);
         }
@@ -389,11 +404,13 @@ __global__ __launch_bounds__(512) void strip_bwdw_kernel(SWArgs a, ConvArgs f) {
         *reinterpret_cast<float4*>(sh.RG + (16 * wave + l16) * ST_LDW + nb * 16 + 4 * lg4) = m1[nb];
       if (tidv < ST_WIN) *reinterpret_cast<float4*>(sh.RE + tidv * SW_LDQ) = qv;
     }
-    if (it == 0) stamp<PROF>(12);
-    if (it == 0) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");  // this strip's loads; the image DMA in flight
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // the image DMA issued in the last strip's P7
-    lds_barrier();  // B1: slots, G1, Q (and, after the first strip, the image)
-    if (it == 0) stamp<PROF>(1);
+    if (it == a.prof_it) stamp<PROF>(12);
+    // the dec_conv2 image for P2's dgrad tile (RW is free since B6 of the last strip): issued after P1 consumed
+    // its loads, the 7 youngest vmcnt events, in flight through B1 and P2's weight-gradient pass
+    dma_d2();
+    asm volatile("s_waitcnt vmcnt(7)" ::: "memory");  // (P1's loads: already consumed)
+    lds_barrier_dma();  // B1: slots, G1, Q
+    if (it == a.prof_it) stamp<PROF>(1);
     // ================= P2: dec_conv2 weight gradient (needs no image: hides the first strip's image DMA), then
     // dec_conv2 dgrad (mask g1) -> dg1 (registers)
     f32x4 mA[4];  // g2 / dpar rows again (L2), for G2 / DP in P3: in flight across this phase
@@ -411,10 +428,8 @@ __global__ __launch_bounds__(512) void strip_bwdw_kernel(SWArgs a, ConvArgs f) {
                  [&](int row) { return ya[(row >> 4) * 18 * ST_LDW + ((row & 15) + 1) * ST_LDW]; },
                  [&](int row, int t) { return xb[(row - 1 + t % 3) * ST_LDW + (t / 3) * 16]; }, accD2, bD2);
     }
-    if (it == 0) {  // every wave's share of the first image has landed
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      lds_barrier();
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's share of the image has landed
+    lds_barrier_dma();
     f32x4 d1[4];
     {
       f32x4 acc[4][1];
@@ -426,7 +441,7 @@ __global__ __launch_bounds__(512) void strip_bwdw_kernel(SWArgs a, ConvArgs f) {
       mask_epi(d1, m1, 1.0f, rb, R, T, lg4, l16, slo, shi, a.store ? a.dg1 : nullptr, nullptr, 0);
     }
     lds_barrier();  // B2: the slots, G1 and the image are read
-    if (it == 0) stamp<PROF>(2);
+    if (it == a.prof_it) stamp<PROF>(2);
     // ================= P3: D1 <- dg1, G2 <- g2, DP <- dpar; the enc_conv2 image by DMA into the G1 region;
     // P4's epilogue operands in flight
 #pragma unroll
@@ -436,10 +451,12 @@ __global__ __launch_bounds__(512) void strip_bwdw_kernel(SWArgs a, ConvArgs f) {
     }
     *reinterpret_cast<float4*>(sh.RW + RW_DP + (16 * wave + l16) * SW_LDD + 4 * lg4) = dpar_mask(rb + l16, xA);
     {
-      constexpr int N2 = 3 * 64 * SB_LDE / 4, C2 = (N2 + 63) / 64;
-      for (int c = wave; c < C2; c += 8) {
-        const int i = c * 64 + lane;
-        if (i < N2) dma16(a.img_e2 + 4 * i, sh.RG + c * 256);
+      constexpr int N2 = 3 * 64 * SB_LDE / 4, C2 = N2 / 64;
+      static_assert(N2 % 64 == 0 && C2 <= 32, "4 whole chunks per wave");
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {  // a fixed, unguarded count (the last chunk again where a wave has 3)
+        const int c = min(wave + 8 * j, C2 - 1);
+        dma16(a.img_e2 + 4 * (c * 64 + lane), sh.RG + c * 256);
       }
     }
     f32x4 qdl[3], h4[2];  // q, dqx, dlx of row rb + l16 and h2e channels 8 lg4 .. + 7 of it (dec1_epi)
@@ -452,12 +469,8 @@ __global__ __launch_bounds__(512) void strip_bwdw_kernel(SWArgs a, ConvArgs f) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) h4[j] = *reinterpret_cast<const f32x4*>(f.lb_h + r * 32 + 8 * lg4 + 4 * j);
     }
-    if (it == 0 && tidv < 128) {  // to_logits' weight (K, H2) zero-padded to [4][32] (dec1_epi)
-      const int k = tidv >> 5, c = tidv & 31;
-      sh.TW[tidv] = (k < K && c < a.H2) ? f.lb_W[k * a.H2 + c] : 0.f;
-    }
-    lds_barrier();  // B3: D1, G2, DP, TW
-    if (it == 0) stamp<PROF>(3);
+    lds_barrier_dma();  // B3: D1, G2, DP, TW (the enc_conv2 image DMA stays in flight: waited in P5)
+    if (it == a.prof_it) stamp<PROF>(3);
     // ================= P4: composed dec_conv1 dgrad + softmax backward + to_logits dgrad (dh2 -> Dh2, dlog -> DL);
     // to_params weight gradient (waves 0-3), composed dec_conv1's (waves 4-7)
     f32x4 h2v[2];  // h2e rows for P5, in flight across this phase
@@ -488,8 +501,8 @@ __global__ __launch_bounds__(512) void strip_bwdw_kernel(SWArgs a, ConvArgs f) {
     }
     float4 m2[4];  // h1e rows: H1 in P5, enc_conv2 dgrad's mask in P6
     load_mask(a.h1e, rb, R, lg4, l16, m2);
-    lds_barrier();  // B4: D1, G2, DP, Q are read; Dh2 and DL written
-    if (it == 0) stamp<PROF>(4);
+    lds_barrier_dma();  // B4: D1, G2, DP, Q are read; Dh2 and DL written
+    if (it == a.prof_it) stamp<PROF>(4);
     // ================= P5: H1 <- h1e (RW, beside DL), H2 <- h2e (RS)
 #pragma unroll
     for (int nb = 0; nb < 4; ++nb)
@@ -501,7 +514,7 @@ __global__ __launch_bounds__(512) void strip_bwdw_kernel(SWArgs a, ConvArgs f) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the enc_conv2 image DMA
     lds_barrier();  // B5
-    if (it == 0) stamp<PROF>(5);
+    if (it == a.prof_it) stamp<PROF>(5);
     // ================= P6: enc_conv2 dgrad (mask h1) -> dh1 (registers); the enc_conv2 and to_logits (waves 0-1)
     // weight gradients
     const int xsh = ld4(D) == 8 ? 1 : 0;
@@ -535,21 +548,19 @@ __global__ __launch_bounds__(512) void strip_bwdw_kernel(SWArgs a, ConvArgs f) {
                  [&](int row, int) { return xb[row * SB_LDE]; }, accS1, bS1);
     }
     lds_barrier();  // B6: H1, H2, DL, Dh2 and the enc_conv2 image are read
-    if (it == 0) stamp<PROF>(6);
+    if (it == a.prof_it) stamp<PROF>(6);
     // ================= P7: DH1 <- dh1 (RS), XX <- x (RD); the next strip's dec_conv2 image (RW)
 #pragma unroll
     for (int nb = 0; nb < 4; ++nb)
       *reinterpret_cast<f32x4*>(sh.RS + (16 * wave + l16) * ST_LDW + nb * 16 + 4 * lg4) = y[nb];
     if (tidv < (ST_WIN << xsh)) *reinterpret_cast<float4*>(sh.RD + (tidv >> xsh) * SW_LDQ + (tidv & xsh) * 4) = xv;
-    if (!last) {
-      dma_d2();
-    } else {  // after the loop: decoder.conv1's weight (64, 64, 3) for the dE share (LDS DMA, 48 chunks of 1 KB),
+    if (last) {  // after the loop: decoder.conv1's weight (64, 64, 3) for the dE share (LDS DMA, 48 chunks of 1 KB),
       // the share's dWc buffer zeroed (RG: the enc_conv2 image is read)
 #pragma unroll
       for (int j = 0; j < 6; ++j) dma16(a.cmpW + 4 * ((wave + 8 * j) * 64 + lane), sh.RW + (wave + 8 * j) * 256);
       for (int i = tidv; i < 1536; i += 512) sh.RG[i] = 0.f;
     }
-    lds_barrier();  // B7
+    lds_barrier_dma();  // B7 (the next strip's image DMA stays in flight: waited before B1)
     // ================= P8: enc_conv1 weight gradient (waves 4-7): tile (ob = wave - 4, packed taps): dY = dh1
     // (DH1), X = x (XX)
     if (wave >= 4) {
@@ -559,8 +570,8 @@ __global__ __launch_bounds__(512) void strip_bwdw_kernel(SWArgs a, ConvArgs f) {
                  [&](int row, int) { const float v = xb[(row - 1 + (xok ? xtap : 0)) * SW_LDQ]; return xok ? v : 0.f; },
                  accS1, bS1);
     }
-    lds_barrier();  // B8: DH1 and XX are read before the next strip writes the slots
-    if (it == 0) stamp<PROF>(7);
+    lds_barrier_dma();  // B8: DH1 and XX are read before the next strip writes the slots
+    if (it == a.prof_it) stamp<PROF>(7);
     ++it;
   }
 
@@ -670,6 +681,10 @@ int launch_strip_bwdw(const ConvArgs& pd, const ConvArgs& d2, const ConvArgs& f,
   a.cslab = w.cslab;
   a.step_inc = w.step_inc;
   a.nstrip = cdiv(pd.R, a.own);
+  {
+    static const int pit = prof_env("VQHMM_STRIP_PROF_IT");
+    a.prof_it = pit;
+  }
   const unsigned grid = (unsigned)strip_bwdw_grid(pd.R);
   if (prof_on()) strip_bwdw_kernel<1><<<grid, 512, sizeof(StripWLds), s>>>(a, f);
   else strip_bwdw_kernel<0><<<grid, 512, sizeof(StripWLds), s>>>(a, f);

@@ -23,6 +23,13 @@ __device__ __forceinline__ bool row_valid(int64_t r, int64_t R, int T) {
   return m >= 1u && m <= (unsigned)T;
 }
 
+// A workgroup barrier for LDS data that leaves LDS DMA (global_load_lds, counted in vmcnt) in flight:
+// lds_barrier()'s release fence makes the compiler drain vmcnt before the barrier whenever DMAs are
+// outstanding.  Here each wave's LDS writes complete (lgkmcnt(0)) before s_barrier, and the "memory"
+// clobber keeps the compiler's memory operations on their side of it; consumers of DMA'd data wait for
+// their own DMAs (vmcnt) before the barrier that publishes them.
+__device__ __forceinline__ void lds_barrier_dma() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 __device__ __forceinline__ void dma16(const float* src, float* dst) {
   __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint32_t*>(src), (__attribute__((address_space(3))) void*)dst,
                                    16, 0, 0);
