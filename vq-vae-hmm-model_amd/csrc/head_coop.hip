@@ -555,6 +555,8 @@ __global__ __launch_bounds__(256, 2) void elbo_head_coop_kernel(HeadArgs a) {
 // MLP sums run in another order, and the windows' assignment to workgroups (so the slab rows, one per
 // workgroup) differs: the tests hold both heads to the oracle at 1e-5.
 namespace {
+__device__ int64_t g_head_zero2[2] = {0, 0};  // what a null norm / count pointer reads (selected away)
+
 template <int K, int HBW>
 struct PipeLds {
   static constexpr int TH = 64 * HBW;
@@ -611,7 +613,37 @@ __global__ __launch_bounds__(768, 1) void elbo_head_pipe_kernel(HeadArgs a) {
   stamp_if(a.dbg & 16, 0);
   const int U = a.U, D = a.D;
   const int ldp = ld4(2 * D), ldx = ld4(D), ldu = ld4(U);
-  const float Bn = loss_norm_batch(a.norm, a.B);
+  // staging's global reads that nothing else waits on, issued together and first (each used to be its own
+  // round trip: a load behind a branch is waited at the join): the batch normaliser and the valid-count
+  // inputs as VECTOR loads (opaque zero index; a null pointer reads the device zeros, selected away)
+  const int z0 = tid >> 10;  // 0, opaque
+  const int64_t* normp = a.norm ? a.norm : g_head_zero2;
+  const int64_t nrm0 = normp[z0], nrm1 = normp[z0 + 1];
+  const int64_t cin = (a.cnt_in ? a.cnt_in : g_head_zero2)[z0];
+  const bool count_here = !a.norm && !a.cnt_in;
+  // the weight image's LDS DMA first: its wait (before the first barrier) then covers every staging load below
+  // in the same round trip
+  if (a.himg) {
+    constexpr int N4 = (16 * S::LDW2 + TH * 8) / 4;
+    for (int c = wave; c * 64 < N4; c += 12) {
+      const int i = c * 64 + lane;
+      if (i < N4)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint32_t*>(a.himg) + 4 * i,
+                                         (__attribute__((address_space(3))) void*)(sh.W2S + c * 256), 16, 0, 0);
+    }
+  }
+  // b2, log_prior and (row waves) window 0's u, unconditionally (clamped) so no branch joins before the DMA
+  const float b2v = a.b2[min(tid & 15, KK - 1) + z0];
+  float lpv[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) lpv[k] = a.log_prior[k + z0];
+  unsigned cpart = 0;  // this thread's share of mask.sum() (:111, :120) when the step gives no count
+  if (count_here)
+    for (int64_t b = tid; b < a.B; b += 768) {
+      const int64_t L = a.lengths[b];
+      cpart += (unsigned)(L <= 0 ? 0 : (L < a.T ? L : a.T));
+    }
+  const float Bn = a.norm ? (float)nrm1 : (float)a.B;  // loss_norm_batch
   const float cpri = -a.beta / Bn;
   const float cent = a.beta / Bn;
   const bool grad = a.need_grad != 0;
@@ -659,17 +691,8 @@ __global__ __launch_bounds__(768, 1) void elbo_head_pipe_kernel(HeadArgs a) {
   // ---- staging (as elbo_head_coop_kernel's, over 12 waves); the row waves' first rows in flight across it
   using RL = PipeRowLds<DM>;
   RL& rl = *reinterpret_cast<RL*>(reinterpret_cast<char*>(smem4) + ((sizeof(S) + 15) / 16) * 16);
-  float u0 = 0.f;
-  if (!mw && nloc > 0) u0 = load_u(0);
-  if (a.himg) {
-    constexpr int N4 = (16 * S::LDW2 + TH * 8) / 4;
-    for (int c = wave; c * 64 < N4; c += 12) {
-      const int i = c * 64 + lane;
-      if (i < N4)
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint32_t*>(a.himg) + 4 * i,
-                                         (__attribute__((address_space(3))) void*)(sh.W2S + c * 256), 16, 0, 0);
-    }
-  } else {
+  const float u0 = load_u(0);  // (row waves, nloc > 0; window 0's rows clamp into [0, R))
+  if (!a.himg) {
     for (int i = tid; i < 16 * S::LDW2; i += 768) {
       const int ij = i / S::LDW2, h = i - ij * S::LDW2;
       sh.W2S[i] = (ij < KK && h < TH) ? a.W2[ij * TH + h] : 0.f;
@@ -680,25 +703,26 @@ __global__ __launch_bounds__(768, 1) void elbo_head_pipe_kernel(HeadArgs a) {
     }
   }
   for (int i = tid; i < 2 * WR * LDL; i += 768) (&sh.dlgS[0][0])[i] = 0.f;
-  if (tid < 16) sh.b2S[tid] = tid < KK ? a.b2[tid] : 0.f;
-  if (tid == 0) sh.cnt = a.norm ? (unsigned long long)a.norm[0] : a.cnt_in ? (unsigned long long)*a.cnt_in : 0ull;
+  if (tid < 16) sh.b2S[tid] = tid < KK ? b2v : 0.f;
+  if (tid == 0) sh.cnt = a.norm ? (unsigned long long)nrm0 : a.cnt_in ? (unsigned long long)cin : 0ull;
   float lp_i = 0.f;
   {
     float m = -__builtin_inff();
-    for (int k = 0; k < K; ++k) m = fmaxf(m, a.log_prior[k]);
+#pragma unroll
+    for (int k = 0; k < K; ++k) m = fmaxf(m, lpv[k]);
     float s = 0.f;
-    for (int k = 0; k < K; ++k) s += __expf(a.log_prior[k] - m);
-    if (si < K) lp_i = a.log_prior[si] - (m + __logf(s));
+#pragma unroll
+    for (int k = 0; k < K; ++k) s += __expf(lpv[k] - m);
+    float lsi = lpv[0];
+#pragma unroll
+    for (int k = 1; k < K; ++k) lsi = si == k ? lpv[k] : lsi;
+    if (si < K) lp_i = lsi - (m + __logf(s));
   }
   if (!mw && nloc > 0) write_u(0, u0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the weight image's LDS DMA, as in elbo_head_coop_kernel
   __syncthreads();
-  if (!a.norm && !a.cnt_in) {
-    unsigned c = 0;
-    for (int64_t b = tid; b < a.B; b += 768) {
-      const int64_t L = a.lengths[b];
-      c += (unsigned)(L <= 0 ? 0 : (L < a.T ? L : a.T));
-    }
+  if (count_here) {
+    unsigned c = cpart;
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o);
     if (lane == 0) atomicAdd(&sh.cnt, (unsigned long long)c);
