@@ -732,9 +732,17 @@ __global__ __launch_bounds__(768, 1) void elbo_head_pipe_kernel(HeadArgs a) {
   stamp_if(a.dbg & 16, 1);
 
   float s_rec = 0.f, s_ent = 0.f, s_tr = 0.f, s_init = 0.f, q0acc = 0.f, db2acc = 0.f;
-  f32x4 gW2[HBW2], gW1[HBW2];
+  f32x4 gW2[HBW2];
+  // dW1' = dhid^T u' on the VALU (16 MFMAs per window as a 16-column MFMA, 11 of the 16 columns padding):
+  // lane (h = hb 16 + l16, its rows 4 lg4 + s of each row block) accumulates columns c < 5 (U <= 4 and the
+  // bias column); the four lane groups are summed once, at the slab store
+  float gw1[HBW2][5];
 #pragma unroll
-  for (int hb = 0; hb < HBW2; ++hb) gW2[hb] = gW1[hb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int hb = 0; hb < HBW2; ++hb) {
+    gW2[hb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 5; ++c) gw1[hb][c] = 0.f;
+  }
 
   // The two roles run their own copies of the window loop (one barrier per step in both, so every barrier
   // meets all 12 waves): each role's registers are then live only in its own loop.
@@ -823,7 +831,7 @@ __global__ __launch_bounds__(768, 1) void elbo_head_pipe_kernel(HeadArgs a) {
     // phase C of window j (hidden blocks wave HBW2 ..): row block rb's operands, its hidden / d-hidden
     // blocks (issued between the previous row block's weight-gradient MFMAs), then its weight-gradient MFMAs
     struct COps {
-      float ua, dla[SD], dlt[4], ubv[4];
+      float ua, dla[SD], dlt[4];
     };
     auto phase_c = [&](int j) {
       const float* uSb = sh.uS[j & 3];
@@ -840,8 +848,6 @@ __global__ __launch_bounds__(768, 1) void elbo_head_pipe_kernel(HeadArgs a) {
         for (int s = 0; s < 4; ++s) {
           const int row = rb * 16 + 4 * lg4 + s;
           o.dlt[s] = dlb[row * LDL + l16];
-          const float uvv = uSb[row * 8 + (l16 & 7)];
-          o.ubv[s] = l16 < 8 ? uvv : 0.f;
         }
       };
       auto hid = [&](const COps& o, f32x4 (&h)[HBW2], f32x4 (&dh)[HBW2]) {
@@ -877,13 +883,20 @@ __global__ __launch_bounds__(768, 1) void elbo_head_pipe_kernel(HeadArgs a) {
             hr[hl][v] = relu_f(h[hl][v]);
             dm[hl][v] = h[hl][v] > 0.f ? dh[hl][v] : 0.f;
           }
+        // u' columns 0..3 of the lane's rows 4 lg4 + s (read under the next hid MFMAs); column 4 matters only at
+        // U = 4, where it is the bias column, 1 on every row (write_u)
+        f32x4 ur4[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) ur4[s] = *reinterpret_cast<const f32x4*>(uSb + (rb * 16 + 4 * lg4 + s) * 8);
         if (rb + 1 < NRB) hid(on, h, dh);
 #pragma unroll
         for (int s = 0; s < 4; ++s)
 #pragma unroll
           for (int hl = 0; hl < HBW2; ++hl) {
             gW2[hl] = mfma16x16x4(oc.dlt[s], hr[hl][s], gW2[hl]);  // dlg^T hid
-            gW1[hl] = mfma16x16x4(dm[hl][s], oc.ubv[s], gW1[hl]);  // dhid^T u'
+#pragma unroll
+            for (int c = 0; c < 4; ++c) gw1[hl][c] = fmaf(dm[hl][s], ur4[s][c], gw1[hl][c]);  // dhid^T u'
+            gw1[hl][4] += dm[hl][s];
           }
         oc = on;
       }
@@ -1099,9 +1112,17 @@ __global__ __launch_bounds__(768, 1) void elbo_head_pipe_kernel(HeadArgs a) {
     for (int v = 0; v < 4; ++v) {
       const int ij = 4 * lg4 + v;
       if (ij < KK) sW2[ij * TH + hb * 16 + l16] = gW2[hl][v];
-      const int h = hb * 16 + 4 * lg4 + v;
-      if (l16 < U) sW1[h * U + l16] = gW1[hl][v];
-      else if (l16 == U) sb1[h] = gW1[hl][v];
+    }
+    const int h = hb * 16 + l16;  // dW1' row of this lane: the four lane groups' rows summed (fixed order)
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+      float v = gw1[hl][c];
+      v += xor16(v);
+      v += xor32(v);
+      if (lg4 == 0) {
+        if (c < U) sW1[h * U + c] = v;
+        else if (c == U) sb1[h] = v;
+      }
     }
   }
   if (a.dbg & 16) {
