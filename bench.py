@@ -101,7 +101,7 @@ def stage_timings(lib, st, x, u, L, B, T, beta, nsteps):
     fl, by, mf = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
     for s in range(n):
         us = statistics.median(ev[k][s].elapsed_time(ev[k][s + 1]) * 1e3 for k in range(nsteps))
-        lib.vqhmm_elbo_stage_info(d, B, T, s, name, 64, ctypes.byref(fl), ctypes.byref(by), ctypes.byref(mf))
+        lib.vqhmm_elbo_stage_info(d, B, T, s, name, len(name), ctypes.byref(fl), ctypes.byref(by), ctypes.byref(mf))
         out.append(dict(stage=s, name=name.value.decode(), us=us, flops=fl.value, bytes=by.value,
                         mfma=bool(mf.value)))
     return out
