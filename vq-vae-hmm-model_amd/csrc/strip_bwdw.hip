@@ -125,6 +125,28 @@ __device__ __forceinline__ void wg_pass(int lo, int nstep, int rm, FA fa, FB fb,
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = mfma16x16x4(av, bv[t], acc[t]);
   };
+  if constexpr (NT == 1) {
+    // one 32-cycle MFMA per step cannot hide an LDS read one step ahead: a ring of four operand sets
+    // (three steps' reads in flight), the same k order (so the same sums)
+    float ar[4], br[4][1];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) load(min(j, nstep - 1), ar[j], br[j]);
+    int k = 0;
+    for (; k + 4 <= nstep; k += 4) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        __builtin_amdgcn_sched_barrier(0);
+        mma(ar[j], br[j]);
+        __builtin_amdgcn_sched_barrier(0);
+        load(min(k + 4 + j, nstep - 1), ar[j], br[j]);  // reads past the last step are clamped to it (unused)
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      if (k + j < nstep) mma(ar[j], br[j]);
+    (void)a0; (void)a1; (void)b0; (void)b1;
+    return;
+  }
   load(0, a0, b0);
   int k = 0;
   for (; k + 1 < nstep; k += 2) {
