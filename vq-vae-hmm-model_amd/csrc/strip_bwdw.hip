@@ -472,14 +472,15 @@ __global__ __launch_bounds__(512) void strip_bwdw_kernel(SWArgs a, ConvArgs f) {
       *reinterpret_cast<f32x4*>(sh.RW + (16 * wave + l16) * ST_LDW + nb * 16 + 4 * lg4) = mA[nb];
     }
     *reinterpret_cast<float4*>(sh.RW + RW_DP + (16 * wave + l16) * SW_LDD + 4 * lg4) = dpar_mask(rb + l16, xA);
-    {
-      constexpr int N2 = 3 * 64 * SB_LDE / 4, C2 = N2 / 64;
-      static_assert(N2 % 64 == 0 && C2 <= 32, "4 whole chunks per wave");
+    // the enc_conv2 image (30 KB) through registers, stored to RG (free since B2) at the end of P4: an LDS DMA
+    // would be drained at P4's first LDS read (the compiler cannot tell its destination from P4's operands)
+    constexpr int N2 = 3 * 64 * SB_LDE / 4, C2 = N2 / 64;
+    static_assert(N2 % 64 == 0 && C2 <= 32, "4 whole chunks per wave");
+    f32x4 e2v[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {  // a fixed, unguarded count (the last chunk again where a wave has 3)
-        const int c = min(wave + 8 * j, C2 - 1);
-        dma16(a.img_e2 + 4 * (c * 64 + lane), sh.RG + c * 256);
-      }
+    for (int j = 0; j < 4; ++j) {  // a fixed count (the last chunk again where a wave has 3: the same bytes)
+      const int c = min(wave + 8 * j, C2 - 1);
+      e2v[j] = *reinterpret_cast<const f32x4*>(a.img_e2 + 4 * (c * 64 + lane));
     }
     f32x4 qdl[3], h4[2];  // q, dqx, dlx of row rb + l16 and h2e channels 8 lg4 .. + 7 of it (dec1_epi)
     {
@@ -523,7 +524,9 @@ __global__ __launch_bounds__(512) void strip_bwdw_kernel(SWArgs a, ConvArgs f) {
     }
     float4 m2[4];  // h1e rows: H1 in P5, enc_conv2 dgrad's mask in P6
     load_mask(a.h1e, rb, R, lg4, l16, m2);
-    lds_barrier_dma();  // B4: D1, G2, DP, Q are read; Dh2 and DL written
+#pragma unroll
+    for (int j = 0; j < 4; ++j) *reinterpret_cast<f32x4*>(sh.RG + min(wave + 8 * j, C2 - 1) * 256 + 4 * lane) = e2v[j];
+    lds_barrier_dma();  // B4: D1, G2, DP, Q are read; Dh2, DL and the enc_conv2 image written
     if (it == a.prof_it) stamp<PROF>(4);
     // ================= P5: H1 <- h1e (RW, beside DL), H2 <- h2e (RS)
 #pragma unroll
@@ -534,7 +537,6 @@ __global__ __launch_bounds__(512) void strip_bwdw_kernel(SWArgs a, ConvArgs f) {
       const int i = tidv + 512 * j;
       *reinterpret_cast<f32x4*>(sh.RS + (i >> 3) * SB_LDE + (i & 7) * 4) = h2v[j];
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the enc_conv2 image DMA
     lds_barrier();  // B5
     if (it == a.prof_it) stamp<PROF>(5);
     // ================= P6: enc_conv2 dgrad (mask h1) -> dh1 (registers); the enc_conv2 and to_logits (waves 0-1)
