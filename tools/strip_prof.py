@@ -13,7 +13,7 @@ import vqhmm  # noqa: E402
 from vqhmm import _ext  # noqa: E402
 
 NAMES = ["staging", "enc_conv1+enc_conv2+logits", "dec_conv1+dec_conv2+params", "-", "-", "-", "other strips"]
-# the backward strip (profiled when it is the step's last strip launch: the default)
+# the non-folded backward strip (VQHMM_STRIP_WGRAD=0: it is then the step's last strip launch)
 NAMES_BWD = ["DMA issue", "params+dec2 dgrad, dg1 swap", "dec1 dgrad+logits bwd", "-", "-", "-", "enc2 dgrad + rest"]
 
 
@@ -40,7 +40,10 @@ def run(B, T=200, D=5, H=64, K=3, H2=32):
     t0 = t[:, 0].min()
     print(f"B={B}: {used.sum()} workgroups, strips/wg {t[:, 8].min()}..{t[:, 8].max()}, "
           f"kernel span {(t[:, 7].max() - t0) * 0.01:.2f} us, start skew {(t[:, 0].max() - t0) * 0.01:.2f} us")
-    names = NAMES_BWD if os.environ.get("VQHMM_STRIP_BWD", "1") != "0" else NAMES
+    # buffer 0 holds the forward strip's stamps unless the non-folded backward strip ran after it
+    # (VQHMM_STRIP_WGRAD=0 with VQHMM_STRIP_BWD on)
+    bwd = os.environ.get("VQHMM_STRIP_WGRAD", "1") == "0" and os.environ.get("VQHMM_STRIP_BWD", "1") != "0"
+    names = NAMES_BWD if bwd else NAMES
     for i, n in enumerate(names):
         if n != "-":
             print(f"  {n:28s} median {np.median(d[:, i]):7.2f}  max {d[:, i].max():7.2f} us")
