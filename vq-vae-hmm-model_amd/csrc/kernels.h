@@ -436,6 +436,7 @@ struct PrologueArgs {  // step prologue: x, u -> PCL, the composed decoder conv1
   unsigned nbh;                     // set by launch_prologue
   unsigned nbx, nbu;                // set by launch_prologue
   unsigned img_blk0[MAX_WIMG + 1];  // set by launch_prologue: first block of each image
+  int dbg;  // profiling build only (VQHMM_PRO_DBG): skip block roles 1 x/u, 2 compose, 4 images, 8 head image, 16 count
 };
 int launch_prologue(PrologueArgs a, hipStream_t s);
 int launch_gather_chunks(const float* src, const int64_t* meta, int64_t B, int64_t C, int64_t Tm, float* out,

@@ -822,6 +822,11 @@ __device__ __forceinline__ void himg_slice(const PrologueArgs& a, int64_t i0) {
 __global__ __launch_bounds__(256) void prologue_kernel(PrologueArgs a) {
   extern __shared__ float cs[];
   const unsigned bx = blockIdx.x;
+  if (a.dbg) {  // timing experiment: skip the roles named by the bits
+    const unsigned e1 = a.nbx + a.nbu, e2 = e1 + (unsigned)a.H, e3 = e2 + a.img_blk0[a.nimg], e4 = e3 + a.nbh;
+    const int role = bx < e1 ? 1 : bx < e2 ? 2 : bx < e3 ? 4 : bx < e4 ? 8 : 16;
+    if (a.dbg & role) return;
+  }
   if (bx < a.nbx) {
     to_pcl_slot(a.x, a.D, a.B, a.T, a.xsc, a.xst, a.xp, (int64_t)bx * 256 + threadIdx.x);
   } else if (bx < a.nbx + a.nbu) {
@@ -852,6 +857,10 @@ __global__ __launch_bounds__(256) void prologue_kernel(PrologueArgs a) {
   }
 }
 int launch_prologue(PrologueArgs a, hipStream_t s) {
+  {
+    static const char* dbg = VQHMM_PROF_ENV("VQHMM_PRO_DBG");
+    a.dbg = dbg ? atoi(dbg) : 0;
+  }
   const int64_t R = a.B * (int64_t)(a.T + 2);
   a.nbx = (unsigned)cdiv(R * (ld4(a.D) / 4), 256);
   a.nbu = (unsigned)cdiv(R * (ld4(a.U) / 4), 256);
