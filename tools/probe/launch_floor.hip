@@ -32,6 +32,17 @@ int main() {
       one_load<<<g, 256>>>(q, p);
     }
   hipDeviceSynchronize();
+  // the same kernels replayed from a captured graph of five launches (the step's shape)
+  hipStream_t st;
+  hipStreamCreate(&st);
+  hipGraph_t gr;
+  hipGraphExec_t ge;
+  hipStreamBeginCapture(st, hipStreamCaptureModeGlobal);
+  for (int k = 0; k < 5; ++k) empty_big<<<512, 256, 0, st>>>(b);
+  hipStreamEndCapture(st, &gr);
+  hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0);
+  for (int rep = 0; rep < 50; ++rep) hipGraphLaunch(ge, st);
+  hipStreamSynchronize(st);
   printf("done\n");
   return 0;
 }
