@@ -39,6 +39,11 @@ import statistics
 import sys
 import time
 
+# The HIP runtime pre-captures a graph's kernel packets by default; on this step (5 dependent launches)
+# that replays ~0.7 us per node slower than with it off (B = 128 one-graph DP step 0.1041 -> 0.1005 ms,
+# tools/gpu_graph_ab.sh).  Read once at HIP initialisation, so it is set before torch touches the GPU.
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+
 import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -66,7 +71,11 @@ def parse():
     ap.add_argument("--scaling", default="strong", choices=("strong", "weak"),
                     help="strong: the config's global batch split over the ranks; weak: the full batch per rank")
     ap.add_argument("--batch", type=int, default=0, help="override the global batch (strong) / per-rank batch (weak)")
-    ap.add_argument("--no-graph", action="store_true", help="run the N=1 step eagerly instead of a HIP graph")
+    ap.add_argument("--launch", default="auto", choices=("auto", "graph", "eager"),
+                    help="how the step reaches the GPU: auto = eager launches for the fused single-process step "
+                         "(its 5 launches: 0.0945 vs 0.0994 ms as a graph at B = 128), one HIP graph for the "
+                         "data-parallel form (the all-reduce captured: 0.1005 vs 0.1069 ms eager)")
+    ap.add_argument("--no-graph", action="store_true", help="same as --launch eager")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--profile-steps", type=int, default=5)
@@ -378,9 +387,13 @@ def main():
         sys.exit(f"bench.py: --gpus {a.gpus} but the launcher's WORLD_SIZE is {world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # RCCL's init banner ("RCCL version : ...", NCCL_DEBUG=VERSION) goes to stdout, where rank 0's one JSON line
-    # must stand alone: warnings only (VQHMM_NCCL_DEBUG picks another level)
+    # rank 0's one JSON line must stand alone on stdout, but RCCL writes its version line and warnings there
+    # even at NCCL_DEBUG=WARN (VQHMM_NCCL_DEBUG picks another level): the JSON gets a private handle on the
+    # real stdout and file descriptor 1 goes to stderr for everything else, native libraries included
     os.environ["NCCL_DEBUG"] = os.environ.get("VQHMM_NCCL_DEBUG", "WARN")
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     if world > 1:
         # VQHMM_BENCH_BACKEND=gloo rehearses the N-rank path on a box with fewer GPUs (ranks share
         # devices round-robin; the all-reduce then goes through host memory): never a measurement
@@ -422,7 +435,10 @@ def main():
     L = torch.full((B,), T, dtype=torch.int64, device="cuda")
     beta = 1.0
 
-    use_graph = not a.no_graph  # N>1: fwd+bwd graph, RCCL all-reduce, Adam graph
+    launch = "eager" if a.no_graph else a.launch
+    if launch == "auto":
+        launch = "graph" if st.dp_form else "eager"
+    use_graph = launch == "graph"  # the DP form: fwd+bwd, RCCL all-reduce and Adam as one graph
     if use_graph:
         step = st.capture(x, u, L, beta)
     else:
@@ -508,7 +524,7 @@ def main():
         }
         if cpu:
             line["speedup_vs_cpu"] = round(value / cpu["value"], 1)
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=json_out, flush=True)
     # ordered teardown: drop the captured graphs (and with them their memory pools) while the
     # device and the communicator are alive, drain the device, then leave the process group
     del step, st, model
