@@ -554,6 +554,7 @@ void make_tail(const ElboPlan& p, const StepCtx& c, TailArgs& ta) {
     }
   } else {
     seg(wl[1].slab, wl[1].nchunks, (int64_t)wl[1].N * wl[1].C * 3, g + off[DEC2_W], nullptr);
+    if (p.wfold) { ta.s[n - 1].trO = wl[1].N; ta.s[n - 1].trC = wl[1].C; }  // the backward strip's row layout
     seg(wl[1].bslab, wl[1].nchunks, wl[1].N, g + off[DEC2_B], nullptr);
   }
   if (p.wgroup) {
@@ -566,6 +567,7 @@ void make_tail(const ElboPlan& p, const StepCtx& c, TailArgs& ta) {
   seg(wl[3].slab, wl[3].nchunks, (int64_t)wl[3].N * wl[3].C, g + off[LOGIT_W], nullptr);
   seg(wl[3].bslab, wl[3].nchunks, wl[3].N, g + off[LOGIT_B], nullptr);
   seg(wl[4].slab, wl[4].nchunks, (int64_t)wl[4].N * wl[4].C * 3, g + off[ENC2_W], nullptr);
+  if (p.wfold) { ta.s[n - 1].trO = wl[4].N; ta.s[n - 1].trC = wl[4].C; }
   seg(wl[4].bslab, wl[4].nchunks, wl[4].N, g + off[ENC2_B], nullptr);
   seg(wl[5].slab, wl[5].nchunks, (int64_t)wl[5].N * wl[5].C * 3, g + off[ENC1_W], nullptr);
   seg(wl[5].bslab, wl[5].nchunks, wl[5].N, g + off[ENC1_B], nullptr);

@@ -194,7 +194,15 @@ struct SlabSeg {
   // block reduces the dWc slab columns of its own o rows itself
   const float* cmpE;   // (K, H): the embedding as this step's forward used it
   int cmpH, cmpK;
+  // trO > 0: a conv weight (trO, trC, 3) whose rows are stored output-fastest, column (c * 3 + tap) * trO + o
+  // holding out[(o * trC + c) * 3 + tap] (the backward strip's 64-wide layers)
+  int trO, trC;
 };
+__host__ __device__ inline int64_t seg_out_index(const SlabSeg& sg, int64_t col) {
+  if (sg.trO == 0) return col;
+  const int64_t ct = col / sg.trO, c = ct / 3;
+  return ((col - ct * sg.trO) * sg.trC + c) * 3 + (ct - 3 * c);
+}
 // largest dWc column span one 64-column block of a composed segment reduces (block_reduce_cols' 256)
 __host__ __device__ inline int64_t composed_block_cols(int H, int K) { return (int64_t)(2 + 62 / (3 * H)) * 3 * K; }
 

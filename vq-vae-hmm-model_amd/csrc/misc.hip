@@ -195,7 +195,7 @@ __device__ int tail_segment_block(const TailArgs& ta, float (&part)[16][64], flo
     for (int h = 0; h < nph; h += 4)
       v += ((part[h][threadIdx.x] + part[h + 1][threadIdx.x]) + part[h + 2][threadIdx.x]) + part[h + 3][threadIdx.x];
     if (sg.scale) v *= *sg.scale;
-    sg.out[col] = v;
+    sg.out[seg_out_index(sg, col)] = v;
     *val = v;
   }
   *colp = col;
@@ -337,7 +337,7 @@ __global__ __launch_bounds__(256) void tail_kernel(TailArgs ta, AdamArgs ad, con
       int sj = 0;
       while (sj + 1 < ta.nseg && b >= ta.blk_start[sj + 1]) ++sj;
       const int64_t c = (b - ta.blk_start[sj]) * 64 + threadIdx.x;
-      if (threadIdx.x < 64 && c < ta.s[sj].len) e = adam_load(ad, (ta.s[sj].out - g) + c, tn);
+      if (threadIdx.x < 64 && c < ta.s[sj].len) e = adam_load(ad, (ta.s[sj].out - g) + seg_out_index(ta.s[sj], c), tn);
     }
     float v = 0.f;
     int64_t col;
@@ -349,7 +349,7 @@ __global__ __launch_bounds__(256) void tail_kernel(TailArgs ta, AdamArgs ad, con
       si = tail_segment_block(ta, part, red, scratch, &v, &col);
     }
     const SlabSeg& sg = ta.s[si];
-    if (ADAM && !(ta.dbg & 8) && threadIdx.x < 64 && col < sg.len) adam_apply(ad, (sg.out - g) + col, v, e);
+    if (ADAM && !(ta.dbg & 8) && threadIdx.x < 64 && col < sg.len) adam_apply(ad, (sg.out - g) + seg_out_index(sg, col), v, e);
   } else if (ta.q0slab && b == nblk) {
     if (ta.dbg & 2) return;
     tail_logprior_block<ADAM>(ta, red, scratch, ad, tn, g);

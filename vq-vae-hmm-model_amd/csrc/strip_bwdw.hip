@@ -274,16 +274,16 @@ __global__ __launch_bounds__(512) void strip_bwdw_kernel(SWArgs a, ConvArgs f) {
   const int slo = max(0, mlo), shi = min(16, mhi);
   // ---- each layer's partial gradient -> slab row blockIdx.x (tail_kernel sums the rows), after the last strip
   const int64_t ch = blockIdx.x;
+  // the two 64-wide layers' rows are stored output-fastest, [(c * 3 + tap) * O + o] (one 16-byte store per
+  // accumulator tile row instead of four scattered words; the tail maps the columns back, SlabSeg::trO)
   auto store_d2 = [&](int lg4, int l16) __attribute__((always_inline)) {  // dec_conv2 (64, 64, 3)
     float* out = a.slab[1] + ch * 64 * 64 * 3;
     const int ob = wave >> 1;
 #pragma unroll
-    for (int t = 0; t < 6; ++t)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int o = ob * 16 + 4 * lg4 + v, c = ((wave & 1) * 2 + t / 3) * 16 + l16;
-        out[(o * 64 + c) * 3 + t % 3] = accD2[t][v];
-      }
+    for (int t = 0; t < 6; ++t) {
+      const int c = ((wave & 1) * 2 + t / 3) * 16 + l16;
+      *reinterpret_cast<f32x4*>(out + (c * 3 + t % 3) * 64 + ob * 16 + 4 * lg4) = accD2[t];
+    }
     const float cb = col_sum4(bD2);
     if ((wave & 1) == 0 && lg4 == 0) a.bslab[1][ch * 64 + ob * 16 + l16] = cb;
   };
@@ -308,13 +308,18 @@ __global__ __launch_bounds__(512) void strip_bwdw_kernel(SWArgs a, ConvArgs f) {
   auto store_e2 = [&](int lg4, int l16) __attribute__((always_inline)) {  // enc_conv2 (H2, 64, 3), to_logits (K, H2)
     const int H2 = a.H2, ob = wave & 1;
     float* out = a.slab[4] + ch * H2 * 64 * 3;
+    const int c = (wave >> 1) * 16 + l16, o0 = ob * 16 + 4 * lg4;
 #pragma unroll
-    for (int t = 0; t < 3; ++t)
+    for (int t = 0; t < 3; ++t) {
+      float* dst = out + (c * 3 + t) * H2 + o0;
+      if (H2 % 4 == 0) {
+        if (o0 < H2) *reinterpret_cast<f32x4*>(dst) = accE2[t];
+      } else {
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int o = ob * 16 + 4 * lg4 + v, c = (wave >> 1) * 16 + l16;
-        if (o < H2) out[(o * 64 + c) * 3 + t] = accE2[t][v];
+        for (int v = 0; v < 4; ++v)
+          if (o0 + v < H2) dst[v] = accE2[t][v];
       }
+    }
     const float ce = col_sum4(bE2), cl = col_sum4(bS1);
     if (wave < 2 && lg4 == 0 && ob * 16 + l16 < H2) a.bslab[4][ch * H2 + ob * 16 + l16] = ce;
     if (wave < 2) {
