@@ -6,10 +6,11 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 300 python bench.py --config cfg4 --no-cpu-baseline --no-hmm --steps 30 --warmup 5 > $OUT/cfg4_b4096.json 2>>$OUT/err.log || { tail -20 $OUT/err.log; exit 1; }
 timeout -k 10 300 python bench.py --config cfg4 --batch 512 --no-cpu-baseline --no-hmm --steps 100 > $OUT/cfg4_b512.json 2>>$OUT/err.log || { tail -20 $OUT/err.log; exit 1; }
+timeout -k 10 300 python bench.py --config cfg4 --batch 512 --dp-form --no-cpu-baseline --no-hmm --steps 100 > $OUT/cfg4_b512_dpform.json 2>>$OUT/err.log || { tail -20 $OUT/err.log; exit 1; }
 timeout -k 10 400 python bench.py --config cfg3 --no-cpu-baseline --no-hmm --steps 10 --warmup 3 --profile-steps 3 > $OUT/cfg3_b2048.json 2>>$OUT/err.log || { tail -20 $OUT/err.log; exit 1; }
 python3 - <<PY
 import json
-for f in ["cfg4_b4096", "cfg4_b512", "cfg3_b2048"]:
+for f in ["cfg4_b4096", "cfg4_b512", "cfg4_b512_dpform", "cfg3_b2048"]:
     d = json.load(open("$OUT/%s.json" % f))
     print(f, d["ms_per_step"], d["value"], json.dumps(d["roofline"]))
     print("  ", {k: v for k, v in d["step_kernels_us"].items() if not k.startswith("(")})
