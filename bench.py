@@ -221,7 +221,7 @@ def hmm_kernels(lib):
             run = lambda: lib.vqhmm_fwdbwd_f32(P(log_pi), P(log_A), P(em), P(L), B, T, K, P(gamma), P(logZ),  # noqa: E731
                                                P(ws), nb, sp)
             byts = B * (4.0 * T * K * K + 4.0 * T * K + 4.0 * T * K) + 4.0 * K
-            kern = "fwdbwd_kernel<8, true, true, 2>"
+            kern = "fwdbwd_seg_kernel"
         for _ in range(3):
             run()
         s = torch.cuda.current_stream()

@@ -35,7 +35,7 @@ CASES = [
     ((7, 32, 6, 16, 3, 256), 16, 60),
     ((16, 32, 7, 16, 2, 128), 20, 45),
     ((16, 32, 8, 16, 1, 64), 12, 33),
-    ((5, 32, 3, 16, 2, 64), 24, 70),       # head_wave, U < 4
+    ((5, 32, 3, 16, 2, 64), 24, 70),       # coop, U < 4
     ((5, 32, 3, 16, 3, 128), 24, 70),
     ((5, 32, 4, 16, 5, 64), 24, 70),       # head_mfma, U = 5..7
     ((5, 32, 2, 16, 6, 128), 24, 70),

@@ -84,15 +84,18 @@ def test_viterbi_cfg5_long_sequence():
     assert np.array_equal(score.cpu().numpy(), rs)
 
 
-# K <= 8 forward-backward has two kernels: the LDS-resident one (whenever its table fits and one
-# round of workgroups covers the batch) and the streaming one (VQHMM_FB_RES=0, read per call).  The
-# streaming one forms gamma inside its chains where its LDS histories fit (T up to ~1000), else through
-# the workspace and a gamma pass (VQHMM_FB_FUSE=0 forces that form; both switches read per call).  The
-# fused form runs two sequence groups per 8-wave workgroup (VQHMM_FB_PAIR=0: one per 4-wave workgroup).
-FB_KERNELS = ["resident", "streaming", "streaming-single", "streaming-unfused"]
+# K <= 8 forward-backward has three kernels: the parallel-in-time one (hmm_seg.hip: one wave per 64-step
+# segment; by default for 5 <= K <= 8 and 128 <= T <= 1024, VQHMM_FB_SEG=1 forces it for every K <= 8 and
+# T <= 1024, =0 turns it off), the LDS-resident one (whenever its table fits and one round of workgroups
+# covers the batch) and the streaming one (VQHMM_FB_RES=0, read per call).  The streaming one forms gamma
+# inside its chains where its LDS histories fit (T up to ~1000), else through the workspace and a gamma
+# pass (VQHMM_FB_FUSE=0 forces that form; both switches read per call).  The fused form runs two sequence
+# groups per 8-wave workgroup (VQHMM_FB_PAIR=0: one per 4-wave workgroup).
+FB_KERNELS = ["segmented", "resident", "streaming", "streaming-single", "streaming-unfused"]
 
 
 def use_fb_kernel(monkeypatch, kernel):
+    monkeypatch.setenv("VQHMM_FB_SEG", "1" if kernel == "segmented" else "0")
     if kernel.startswith("streaming"):
         monkeypatch.setenv("VQHMM_FB_RES", "0")
     else:
@@ -119,6 +122,7 @@ def test_forward_backward_pair_matches_single(K, B, T, monkeypatch):
     L[0], L[1] = T, 1
     args = (*gpu(log_pi, log_A, em), torch.from_numpy(L))
     monkeypatch.setenv("VQHMM_FB_RES", "0")
+    monkeypatch.setenv("VQHMM_FB_SEG", "0")
     out = {}
     for pair in ("1", "0"):
         monkeypatch.setenv("VQHMM_FB_PAIR", pair)
@@ -241,11 +245,44 @@ def test_forward_backward_tier_fallbacks(K, spread, kernel, monkeypatch):
     assert np.all(np.abs(logZ.cpu().numpy() - rz) <= 1e-5 * np.maximum(1.0, np.abs(rz)))
 
 
+@pytest.mark.parametrize("K,B,T,L", [(8, 512, 512, "full"), (8, 300, 512, "ragged"), (5, 40, 1024, "ragged"),
+                                     (8, 17, 1000, "ragged"), (7, 9, 130, "ragged"), (8, 5, 65, "ragged"),
+                                     (6, 3, 64, "full"), (3, 33, 200, "ragged"), (1, 4, 300, "ragged")])
+def test_forward_backward_segmented(K, B, T, L, monkeypatch):
+    """The parallel-in-time kernel (hmm_seg.hip) against the fp64 oracle: the cfg4 shard shape (512 x 512,
+    K = 8), ragged lengths that end inside, at and before segment boundaries (incl. 0 and 1), T not a
+    multiple of 64, 16 segments (T = 1024), one segment (T = 64), K < 8 (padded lanes)."""
+    import vqhmm
+    monkeypatch.setenv("VQHMM_FB_SEG", "1")
+    log_pi, log_A, em = random_hmm(K * 31 + B + T, B, T, K)
+    if L == "full":
+        Ls = np.full(B, T, np.int64)
+    else:
+        Ls = np.random.default_rng(T + B).integers(0, T + 1, B).astype(np.int64)
+        Ls[0] = T
+        Ls[1 % B] = 1
+        for k, v in enumerate((64, 65, 63, 128, 0, 2)):
+            if 2 + k < B:
+                Ls[2 + k] = min(v, T)
+    gamma, logZ = vqhmm.forward_backward(*gpu(log_pi, log_A, em), torch.from_numpy(Ls))
+    sl = slice(0, B, max(1, B // 24))  # the fp64 oracle on a strided slice of the batch
+    rg, rz = hmm_ref.forward_backward_f64(log_pi, log_A[sl], em[sl], Ls[sl])
+    check_gamma(gamma.cpu().numpy()[sl], rg)
+    z = logZ.cpu().numpy()[sl]
+    live = Ls[sl] > 0
+    assert np.all(np.abs(z[live] - rz[live]) <= 1e-5 * np.maximum(1.0, np.abs(rz[live])))
+    assert np.all(np.isnan(z[~live]))
+    g = gamma.cpu().numpy()
+    past = np.arange(T)[None, :] >= Ls[:, None]
+    assert np.all(g[past] == 0)
+
+
 @pytest.mark.parametrize("K,B,T", [(8, 300, 64), (4, 1100, 40), (8, 2, 560), (2, 3, 1000)])
-def test_forward_backward_resident_boundaries(K, B, T):
+def test_forward_backward_resident_boundaries(K, B, T, monkeypatch):
     """Shapes at the resident kernel's limits: several workgroups per CU (small T), batches
     near one round, and T past the LDS table (streaming kernel)."""
     import vqhmm
+    monkeypatch.setenv("VQHMM_FB_SEG", "0")
     log_pi, log_A, em = random_hmm(K * 13 + B + T, B, T, K)
     L = np.random.default_rng(T).integers(0, T + 1, B).astype(np.int64)
     L[0] = T
@@ -378,3 +415,43 @@ def test_forward_backward_impossible_sequence(K, T, kernel, monkeypatch):
     ok = [0, 2]
     check_gamma(g[ok], rg[ok])
     assert np.all(np.abs(z[ok] - rz[ok]) <= 1e-5 * np.maximum(1.0, np.abs(rz[ok])))
+
+
+def test_forward_backward_segmented_tiers(monkeypatch):
+    """Which path the parallel-in-time kernel takes per sequence: the linear fast path leaves the workspace
+    untouched (it keeps both histories in LDS), the exact path writes the sequence's alpha / beta there.
+    Model-like tables (log_softmax of N(0,1)) must take the fast path; the extreme ones (left-to-right
+    -inf transitions, -1e3-nat emissions, 300-nat spreads, near-deterministic transitions) the exact path,
+    and both give gamma / logZ within the contract."""
+    import vqhmm
+    from vqhmm import _ext
+    monkeypatch.setenv("VQHMM_FB_SEG", "1")
+    B, T, K = 6, 300, 8
+    rng = np.random.default_rng(77)
+    log_pi, log_A, em = random_hmm(78, B, T, K, scale=1.0)
+    log_A = log_A.astype(np.float64)
+    em = em.astype(np.float64)
+    tri = np.triu(np.ones((K, K), bool))
+    la = np.where(tri, log_A[1], -np.inf)
+    log_A[1] = la - np.logaddexp.reduce(la, axis=-1, keepdims=True)   # b1: left-to-right
+    em[2] = em[2] * 50.0 - 1000.0                                      # b2: huge negative emissions
+    em[3, 100:120] *= 150.0                                            # b3: 300+ nat spread
+    log_A[4] = log_softmax(rng.standard_normal((T, K, K)) * 80.0)      # b4: near-deterministic
+    log_A, em = log_A.astype(np.float32), em.astype(np.float32)
+    L = np.array([T, T, T, T, T, 200], np.int64)
+    lp, lA, e, Lt = (*gpu(log_pi, log_A, em), torch.from_numpy(L).cuda())
+    gamma = torch.empty(B, T, K, device="cuda")
+    logZ = torch.empty(B, device="cuda")
+    lib = _ext.load()
+    nb = lib.vqhmm_fwdbwd_workspace_size(B, T, K)
+    ws = torch.full((nb // 4,), float("nan"), device="cuda")
+    _ext.check(lib.vqhmm_fwdbwd_f32(_ext.ptr(lp), _ext.ptr(lA), _ext.ptr(e), _ext.ptr(Lt), B, T, K, _ext.ptr(gamma),
+                                    _ext.ptr(logZ), _ext.ptr(ws), nb, _ext.stream_ptr()), "forward_backward")
+    al = ws[: B * T * K].view(B, T, K).cpu().numpy()
+    touched = ~np.isnan(al).all(axis=(1, 2))
+    assert list(touched) == [False, True, True, True, True, False], touched
+    with np.errstate(divide="ignore", invalid="ignore"):
+        rg, rz = hmm_ref.forward_backward_f64(log_pi, log_A, em, L)
+    check_gamma(gamma.cpu().numpy(), rg)
+    z = logZ.cpu().numpy()
+    assert np.all(np.abs(z - rz) <= 1e-5 * np.maximum(1.0, np.abs(rz)))

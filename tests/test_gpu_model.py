@@ -172,9 +172,10 @@ def test_cfg2_full_size_vs_oracle():
 
 @pytest.mark.parametrize("B", [512, 256, 128])
 def test_strong_scaling_shards_vs_oracle(B):
-    """The per-GPU shards of cfg2 under strong scaling at N = 4 and 8 (B = 512 at N = 2 too): B = 256 runs the head's 2-block
-    windows and B = 128 the 1-block ones plus the fused backward pair (conv2g_kernel), each checked
-    against the oracle, at the contract's 1e-5 normwise bound (at B = 256 this draw's
+    """The per-GPU shards of cfg2 under strong scaling at N = 4 and 8 (B = 512 at N = 2 too), each run by the
+    step's five launches (prologue, forward strip, pipelined head, the backward strip with the six weight
+    gradients folded in (strip_bwdw_kernel, owned rows sized from the row count: 104 rows / 249 strips at
+    B = 128), the tail), each checked against the oracle, at the contract's 1e-5 normwise bound (at B = 256 this draw's
     transition_net.0 gradient sits at 5.3e-6 of the fp64 oracle whatever the window size, NBW 1, 2 or
     4, i.e. fp32 summation, above the full-size test's stricter 2e-6)."""
     from test_gpu_configs import check_step_vs_oracle

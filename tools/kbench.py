@@ -102,7 +102,7 @@ def bench_fwdbwd(a):
     def fn():
         lib.vqhmm_fwdbwd_f32(P(log_pi), P(log_A), P(em), P(L), B, T, K, P(gamma), P(logZ), P(ws), nb, st)
 
-    t = time_fn(fn, iters=5, warmup=2)
+    t = time_fn(fn, iters=20, warmup=3)
     byts = B * (4 * T * K * K + 4 * T * K + 4 * T * K) + 4 * K
     print(json.dumps({"kernel": "fwdbwd", "B": B, "T": T, "K": K, "us": t * 1e6, "GBps": byts / t / 1e9,
                       "frac_hbm": byts / t / HBM_PEAK}))

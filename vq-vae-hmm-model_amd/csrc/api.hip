@@ -36,13 +36,12 @@ struct Carver {
 
 // Head choice (VQHMM_HEAD, read once): default the workgroup-cooperative head (head_coop.hip) wherever it
 // applies, pipelined (one 12-wave workgroup per CU, elbo_head_pipe_kernel) for K <= 4, TH = 128; "coop" = the
-// two-workgroups-per-CU form for K <= 4 too, "wave" = the wave-window head for K <= 4 (head_wave.hip),
-// "tile" = the tile-barrier MFMA head (head_mfma.hip) — A/B switches.
+// two-workgroups-per-CU form for K <= 4 too, "tile" = the tile-barrier MFMA head (head_mfma.hip) — A/B
+// switches.
 int head_choice() {
   static const int v = [] {
     const char* e = VQHMM_ENV("VQHMM_HEAD");
     if (e && strcmp(e, "tile") == 0) return 2;
-    if (e && strcmp(e, "wave") == 0) return 1;
     if (e && strcmp(e, "coop") == 0) return 3;
     return 0;
   }();
@@ -142,7 +141,6 @@ struct ElboPlan {
   unsigned long long* sync;  // [2] the status word (vqhmm_elbo_status_offset; reserved), [0], [1], [3] spare
   // staged head (shapes the fused heads do not cover): Prior MLP as 1x1 convs
   bool staged;
-  bool wave_head;  // head_wave.hip (K <= 4, VQHMM_HEAD=wave)
   bool coop_head;  // head_coop.hip (K <= 8, the default); else head_mfma / head.hip
   bool pipe_head;  // ... its pipelined kernel (K <= 4)
   bool dec2_split; // grouped weight gradients: dec_conv2's job as two 32-output halves (slabs [half][chunk][32]..)
@@ -191,7 +189,6 @@ ElboPlan plan_elbo(const vqhmm_dims_t* d, int64_t B, int64_t T, void* ws) {
     hc.R = R;
     p.coop_head = head_coop_supported(hc) && (head_choice() == 0 || head_choice() == 3);
     p.pipe_head = p.coop_head && head_pipe_supported(hc) && head_choice() == 0;
-    p.wave_head = !p.coop_head && head_mfma_supported(hc) && p.U <= 4 && head_choice() == 1;
   }
   {
     HeadArgs hc{};
@@ -199,7 +196,7 @@ ElboPlan plan_elbo(const vqhmm_dims_t* d, int64_t B, int64_t T, void* ws) {
     p.strip_head = p.coop_head && strip_head_on() && strip_fwd_shapes_ok(D, H, H2, K, R) && strip_head_supported(hc);
   }
   p.hgrid = p.strip_head ? strip_fwd_grid(R)
-            : p.pipe_head ? head_pipe_grid(R) : p.coop_head ? head_coop_grid(R, K) : p.wave_head ? head_wave_grid(R) : head_grid(R);
+            : p.pipe_head ? head_pipe_grid(R) : p.coop_head ? head_coop_grid(R, K) : head_grid(R);
   p.dpar = c.take<float>(R * ld4(2 * D));
   p.dqx = c.take<float>(R * ld4(K));
   p.dlx = c.take<float>(R * ld4(K));
@@ -283,7 +280,7 @@ ConvArgs conv_base(const ElboPlan& p) {
 
 extern "C" {
 
-int32_t vqhmm_abi_version(void) { return 5; }
+int32_t vqhmm_abi_version(void) { return 6; }
 
 int vqhmm_param_layout(const vqhmm_dims_t* d, int64_t off[VQHMM_NPARAMS + 1]) {
   if (!dims_ok(d) || !off) return VQHMM_EINVAL;
@@ -798,7 +795,6 @@ int run_stage(const ElboPlan& p, const StepCtx& c, int st, hipStream_t s) {
       const HeadArgs h = head_args(p, c);
       if (p.pipe_head) return launch_head_pipe(h, p.hgrid, s);
       if (p.coop_head) return launch_head_coop(h, p.hgrid, s);
-      if (p.wave_head) return launch_head_wave(h, p.hgrid, s);
       return launch_head(h, p.hgrid, s);
     }
     case S_FINAL:

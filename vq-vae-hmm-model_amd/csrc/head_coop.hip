@@ -13,7 +13,7 @@
 //   C  wave w owns hidden blocks [w HBW, (w+1) HBW): hid (rows x h), dh = dlg W2, the ReLU mask,
 //      gW2[:, its h] += dlg^T relu(hid), gW1'[its h] += dhid^T u'.
 // A wave keeps only its own hidden blocks' weight-gradient accumulators (4 KB HBW + 4 HBW floats: 16 at
-// K <= 4, 40 at K = 8, TH = 128), so there are no cross-wave sums; the slabs have head_wave.hip's
+// K <= 4, 40 at K = 8, TH = 128), so there are no cross-wave sums; the slabs have the fused heads' common
 // layout (same tail reduction).  WR = 256 / KP: 64 rows (4 row blocks) at K <= 4, 32 (2) at K <= 8.
 // Summation order differs from the reference's autograd; the tests hold it to 1e-5 relative.
 #include <stddef.h>

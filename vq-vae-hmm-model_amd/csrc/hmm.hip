@@ -1429,6 +1429,7 @@ int launch_fwdbwd(const float* log_pi, const float* log_A, const float* em, cons
   const bool w16 = aligned16(log_A) && aligned16(em);
   float* w = (float*)ws;
   if (K > 8) return launch_fwdbwd_wide(log_pi, log_A, em, lengths, B, T, K, gamma, logZ, w, s);
+  if (fwdbwd_seg_ok(B, T, K)) return launch_fwdbwd_seg(log_pi, log_A, em, lengths, B, T, K, gamma, logZ, w, s);
   if (fwdbwd_resident_ok(B, K, T)) {
     switch (K) {
       case 1: fwdbwd_res_go<1>(log_pi, log_A, em, lengths, B, T, gamma, logZ, ws, s); break;

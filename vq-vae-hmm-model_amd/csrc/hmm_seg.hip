@@ -1,0 +1,460 @@
+// Forward-backward, parallel in time.
+//
+// Semantics as hmm.hip (math.md:23-67; log_A[:, t] = t-1 -> t, VQ_VAE_HMM_fixed.py:125-127): per
+// sequence b of length L, alpha_0 = log_pi + e_0, alpha_t(j) = LSE_i(alpha_{t-1}(i) + A_t(i, j)) + e_t(j),
+// beta_{L-1} = 0, beta_{t-1}(i) = LSE_j(A_t(i, j) + e_t(j) + beta_t(j)), gamma_t = softmax(alpha_t + beta_t),
+// logZ = LSE(alpha_{L-1}).
+//
+// The streaming / resident kernels of hmm.hip run each sequence as ONE chain of L serial steps (~140
+// cycles a step): at the cfg4 shard (512 x 512, K = 8) that chain, not HBM, sets the time.  Here the
+// sequence is cut into segments of SEG = 64 steps, one wave each, one workgroup per sequence:
+//
+//   P_t(i, j) = 2^((A_t(i, j) + e_t(j) - E_t) lg e),  E_t = max_j e_t(j)   (a per-step frame; linear domain)
+//
+//   phase 1  each wave loads its segment's table ONCE into 64 VGPRs (lane (r, c) holds entry (i, j) of
+//            step t, the (i, j) <-> lane map alternating with t's parity as in hmm.hip) and forms the
+//            segment's transfer matrix M_s = prod_t P_t (lane (r, c) holds M(r, c); per step the row r of
+//            M and column c of P come through LDS, 8 FMAs, the row rescaled by a power of two).
+//   phase 2  one wave chains the S segment matrices forward for the alpha vector at every segment
+//            boundary, another backward for beta (log2 domain, max-shifted LSE; S steps, not T).
+//   phase 3  each wave reruns its segment's alpha and beta vector chains from those boundary vectors
+//            on the tables still in its registers (the two chains interleaved, rescaled every 8 steps),
+//            keeps both histories in LDS and writes gamma_t = alpha_t beta_t / sum for its 64 steps.
+//
+// HBM sees log_A and em once and gamma once (the algorithmic bytes); the serial chain is 64 matrix
+// steps + S + 64 vector steps instead of L.  Range: a value that leaves [2^-96, 2^96] anywhere (a
+// matrix entry relative to its row's last scale, a chain value relative to its last rescale) means
+// something nearly vanished or exploded in fp32, as do -inf / NaN inputs (an exact 0 table entry, an
+// all -inf emission row).  Then the whole sequence is recomputed by the exact path below (max-shifted
+// natural-log recursions, renormalised every step, offsets in fp64, the workspace holding both
+// directions): the tier fallback of hmm.hip, per sequence.
+#include "hmm_lanes.h"
+
+namespace vqhmm {
+
+constexpr int FBS_SEG = 64;       // time steps per segment (= per wave)
+constexpr int FBS_MAXW = 16;      // segments per workgroup: T <= 1024
+constexpr int FBS_WAVE_F = 1152;  // LDS floats per wave: es/hist_a [64][8] | hist_b [64][8] | M [8][8] | P' [8][8]
+constexpr float FBS_LOG2E = 1.44269504088896341f;
+constexpr double FBS_LN2 = 0.69314718055994531;
+
+// LDS of one workgroup of nw waves: the waves' regions, then the segment matrices (log2) [16][8][8], the
+// boundary vectors alpha [17][8] and beta [17][8] (log2), the segments' frame sums (fp64) and flags.
+__host__ __device__ constexpr size_t fbs_lds_bytes(int nw) {
+  return (size_t)nw * FBS_WAVE_F * 4 + (1024 + 136 + 136) * 4 + FBS_MAXW * 8 + FBS_MAXW * 4;
+}
+
+__device__ __forceinline__ float fbs_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ __forceinline__ float fbs_log2(float x) { return __builtin_amdgcn_logf(x); }
+// a value the linear forms may carry: within [2^-96, 2^96] (false for 0, inf, NaN)
+__device__ __forceinline__ bool fbs_in_range(float lo, float hi) { return lo >= 0x1p-96f && hi <= 0x1p96f; }
+// c ? a : b with a computed unconditionally: left to itself the compiler turns the select into a branch
+// around a's computation and sinks the step's table load into it, draining vmcnt there
+__device__ __forceinline__ float fbs_pick(bool c, float a, float b) {
+  asm volatile("" : "+v"(a));
+  return c ? a : b;
+}
+__device__ __forceinline__ int fbs_bits(float x) { return __builtin_bit_cast(int, x); }
+// a wave-uniform int in a VGPR: comparisons against it stay v_cmp / v_cndmask selects instead of
+// scalar branches (which let the compiler sink a step's table load into a branch and drain vmcnt there)
+__device__ __forceinline__ int fbs_vgpr(int x) {
+  int v;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "s"(x));
+  return v;
+}
+
+// One workgroup per sequence, one wave per 64-step segment.  Steps that are not transitions of the
+// sequence (t = 0, t >= L) carry the identity matrix, so every phase runs branch-free over its 64 steps:
+// alpha / beta pass such a step unchanged and the product ignores it.
+__global__ __launch_bounds__(1024) void fwdbwd_seg_kernel(const float* __restrict__ log_pi,
+                                                          const float* __restrict__ log_A,
+                                                          const float* __restrict__ em,
+                                                          const int64_t* __restrict__ lengths, int64_t B, int T,
+                                                          int K, float* __restrict__ gamma,
+                                                          float* __restrict__ logZ, float* __restrict__ ws,
+                                                          unsigned long long* __restrict__ prof) {
+  constexpr int SEG = FBS_SEG;
+  extern __shared__ float4 smem_fbs4[];
+  float* sm = reinterpret_cast<float*>(smem_fbs4);
+  const int nw = (int)(blockDim.x >> 6);
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int lane = (int)(threadIdx.x & 63), ra = lane >> 3, cb = lane & 7;
+  const int64_t b = blockIdx.x;
+  const int64_t Lr = lengths[b];
+  const int L = (int)(Lr <= 0 ? 0 : (Lr < T ? Lr : T));
+  const int ts = w * SEG;  // first time step of this wave's segment (even: a step's parity is u's)
+  float* gq = gamma + b * (int64_t)T * K;
+  // profiling build only (VQHMM_FB_PROF=1, fast path): per wave s_memtime at the phase ends, [b][w][8]
+  auto stamp = [&](int k) {
+    if (prof && lane == 0) {
+      const unsigned long long v = k == 0 ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime();
+      prof[((int64_t)b * FBS_MAXW + w) * 8 + k] = v;
+      if (k == 7) prof[((int64_t)b * FBS_MAXW + w) * 8 + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+  };
+  if (prof && lane == 0) prof[((int64_t)b * FBS_MAXW + w) * 8 + 2] = __builtin_amdgcn_s_memtime();
+  stamp(0);
+
+  if (L == 0) {  // gamma = 0, logZ = NaN (hmm.hip's convention)
+    for (int idx = (int)threadIdx.x; idx < T * K; idx += (int)blockDim.x) gq[idx] = 0.f;
+    if (threadIdx.x == 0) logZ[b] = __builtin_bit_cast(float, 0x7fc00000u);
+    return;
+  }
+
+  float* es = sm + w * FBS_WAVE_F;  // [64][8]: e_t(j) - E_t (natural); phase 3: alpha history
+  float* hb = es + 512;             // [64][8]: beta history
+  float* mb = es + 1024;            // [8][8]: M
+  float* pb = es + 1088;            // [8][8]: P transposed (column c at pb[c*8 ..])
+  float* g_mlog = sm + nw * FBS_WAVE_F;  // [16][8][8] log2 M_s (row scale folded in)
+  float* g_va = g_mlog + 1024;           // [17][8] alpha at segment boundaries (log2, framed)
+  float* g_wb = g_va + 136;              // [17][8] beta at segment ends (log2)
+  double* g_esum = reinterpret_cast<double*>(g_wb + 136);
+  int* g_flag = reinterpret_cast<int*>(g_esum + FBS_MAXW);
+
+  const float* Ab = log_A + b * (int64_t)T * K * K;
+  const float* Eb = em + b * (int64_t)T * K;
+  const int Kv = fbs_vgpr(K);
+  const bool real = ra < Kv && cb < Kv;
+  // the sequence's tables as buffers: loads past their end return 0 (steps past T are identity steps)
+  const int stride = __builtin_amdgcn_readfirstlane(K * K * 4);  // bytes per step of log_A
+  const __amdgpu_buffer_rsrc_t rA =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Ab, (short)0, __builtin_amdgcn_readfirstlane(T * K * K * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rE =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Eb, (short)0, __builtin_amdgcn_readfirstlane(T * K * 4), 0x00020000);
+  // lane's entry of a step: (i, j) = (ra, cb) on even t, (cb, ra) on odd t
+  const int voff0 = real ? (ra * K + cb) * 4 : 0, voff1 = real ? (cb * K + ra) * 4 : 0;
+  auto tab_ld = [&](int u) -> float {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rA, (u & 1) ? voff1 : voff0,
+                                                                         (ts + u) * stride, 0));
+  };
+
+  // ---------------------------------------------------------------- loads: em rows, then the table
+  // lane l: the emission row of step ts + l
+  const int tl = ts + lane;
+  float er[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) er[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rE, tl * K * 4 + j * 4, 0, 0));
+  float tab[SEG];
+  static_for<48>([&](auto ui) {  // 8 + 48 loads in flight (vmcnt counts to 63)
+    constexpr int u = decltype(ui)::value;
+    tab[u] = tab_ld(u);
+  });
+  float E = NEG_INF;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) E = j < Kv ? fmaxf(E, er[j]) : E;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) es[lane * 8 + j] = er[j] - E;
+  // the frames of the sequence's steps in this segment (logZ = sum_t E_t + lg of the framed sums)
+  const double esum = wave_sum_dpp((double)(tl < L ? E : 0.f));
+  stamp(3);
+
+  // ---------------------------------------------------------------- phase 1: M_s = prod_t P_t
+  // Lane (ra, cb) holds M(ra, cb); row ra's scale 2^cx.  Step t: M'(r, c) = sum_k M(r, k) P_t(k, c), the row
+  // M(r, :) and the column P_t(:, c) read from LDS (the wave's own buffers: LDS ops retire in order).
+  float m = (ra == cb && ra < Kv) ? 1.f : 0.f;
+  const float ident = m;
+  float cx = 0.f;  // (a float sum: integer adds get reassociated into a tree holding every step's exponent)
+  int lob = fbs_bits(1.f), hib = fbs_bits(1.f);  // range of the real entries (bit patterns, as rmax)
+  const int ua = fbs_vgpr(max(0, min(SEG, L - ts)));  // steps u < ua are the sequence's (t < L)
+  const int u_first = fbs_vgpr(w == 0 ? 1 : 0);      // (t = 0 is no transition)
+  static_for<SEG>([&](auto ui) {
+    constexpr int u = decltype(ui)::value, p = u & 1;
+    const int i = p ? cb : ra, j = p ? ra : cb;
+    float P = fbs_exp2((tab[u] + es[u * 8 + j]) * FBS_LOG2E);
+    const bool trans = (u < ua) & (u >= u_first);
+    P = fbs_pick(real & trans, P, ident);  // not a transition: identity
+    tab[u] = P;
+    if constexpr (u < 16) tab[u + 48] = tab_ld(u + 48);
+    pb[j * 8 + i] = P;
+    mb[lane] = m;
+    const float4 r0 = *reinterpret_cast<const float4*>(mb + ra * 8);
+    const float4 r1 = *reinterpret_cast<const float4*>(mb + ra * 8 + 4);
+    const float4 c0 = *reinterpret_cast<const float4*>(pb + cb * 8);
+    const float4 c1 = *reinterpret_cast<const float4*>(pb + cb * 8 + 4);
+    // row max on the bit patterns (M >= 0: integer order = float order; a NaN wins, and flags below)
+    const int rmax = max(max(max(fbs_bits(r0.x), fbs_bits(r0.y)), max(fbs_bits(r0.z), fbs_bits(r0.w))),
+                         max(max(fbs_bits(r1.x), fbs_bits(r1.y)), max(fbs_bits(r1.z), fbs_bits(r1.w))));
+    const int e = __builtin_amdgcn_frexp_expf(__builtin_bit_cast(float, rmax));
+    float s0 = r0.x * c0.x;
+    s0 = fmaf(r0.y, c0.y, s0);
+    s0 = fmaf(r0.z, c0.z, s0);
+    s0 = fmaf(r0.w, c0.w, s0);
+    float s1 = r1.x * c1.x;
+    s1 = fmaf(r1.y, c1.y, s1);
+    s1 = fmaf(r1.z, c1.z, s1);
+    s1 = fmaf(r1.w, c1.w, s1);
+    m = __builtin_amdgcn_ldexpf(s0 + s1, -e);
+    cx += (float)e;
+    const int mc = (real & trans) ? fbs_bits(m) : fbs_bits(1.f);
+    lob = min(lob, mc);
+    hib = max(hib, mc);
+  });
+  float lo = __builtin_bit_cast(float, lob), hi = __builtin_bit_cast(float, hib);
+  {
+    // the rows' scales relative to the largest (exact small integers): lg M stays O(10) in fp32, the
+    // common scale c0 goes to the fp64 frame sum
+    const float c0 = allred<8, false>(ra < Kv ? cx : NEG_INF, OpMax{});
+    const float ml = m > 0.f ? fbs_log2(m) + (cx - c0) : NEG_INF;
+    g_mlog[w * 64 + lane] = real ? ml : NEG_INF;
+    const bool bad = real && !fbs_in_range(lo, hi);
+    const int anybad = __builtin_amdgcn_ballot_w64(bad) != 0;
+    if (lane == 0) {
+      g_flag[w] = anybad;
+      g_esum[w] = esum + FBS_LN2 * (double)c0;
+    }
+  }
+  stamp(4);
+  __syncthreads();
+  int flagged = 0;
+  for (int s = 0; s < nw; ++s) flagged |= g_flag[s];
+
+  // ---------------------------------------------------------------- phase 2: boundary vectors
+  // Every segment's chain starts "at step -1" of the segment: segment 0 from alpha_0 (its step 0 is an
+  // identity step), segment s from alpha at step 64 s - 1; beta from step 64 s + 63 (= beta_{L-1} past L).
+  if (!flagged) {
+    if (w == 0) {
+      // V_0(j) = lg alpha_0 (framed by E_0); V_{s+1}(c) = LSE_r(V_s(r) + lg M_s(r, c))
+      const float v0 = cb < K ? (log_pi[cb] + sm[cb]) * FBS_LOG2E : NEG_INF;  // sm = wave 0's es row 0
+      if (lane < 8) g_va[lane] = v0;
+      // each V renormalised to max 0 (the offsets summed in fp64): V of a late segment would otherwise be
+      // ~-1e3 and its fp32 ulp a 1e-5 relative error in 2^V
+      float vn = v0;
+      double off = 0.0;
+      for (int s = 0; s < nw; ++s) {
+        const float x = g_va[s * 8 + ra] + g_mlog[s * 64 + lane];
+        const float mx = allred<8, false>(x, OpMax{});
+        const float ex = mx == NEG_INF ? 0.f : fbs_exp2(x - mx);
+        const float su = allred<8, false>(ex, OpAdd{});
+        vn = mx == NEG_INF ? NEG_INF : mx + fbs_log2(su);
+        const float vm = allred<8, true>(cb < K ? vn : NEG_INF, OpMax{});
+        if (vm != NEG_INF) {
+          vn -= vm;
+          off += (double)vm;
+        }
+        if (lane < 8) g_va[(s + 1) * 8 + lane] = vn;
+      }
+      // logZ = ln 2 * (lg sum_j 2^V_S(j) + the offsets) + the frames
+      const float vx = cb < K ? vn : NEG_INF;
+      const float mx = allred<8, true>(vx, OpMax{});
+      const float su = allred<8, true>(mx == NEG_INF ? 0.f : fbs_exp2(vx - mx), OpAdd{});
+      double fr = 0.0;
+      for (int s = 0; s < nw; ++s) fr += g_esum[s];
+      if (lane == 0) logZ[b] = (float)(FBS_LN2 * ((double)mx + (double)fbs_log2(su) + off) + fr);
+    }
+    if (w == (nw > 1 ? 1 : 0)) {
+      // W_{S-1} = 0; W_{s-1}(r) = LSE_c(lg M_s(r, c) + W_s(c)) = beta at step 64 s - 1
+      if (lane < 8) g_wb[(nw - 1) * 8 + lane] = lane < K ? 0.f : NEG_INF;
+      for (int s = nw - 1; s >= 1; --s) {
+        const float x = g_mlog[s * 64 + lane] + g_wb[s * 8 + cb];
+        const float mx = allred<8, true>(x, OpMax{});
+        const float ex = mx == NEG_INF ? 0.f : fbs_exp2(x - mx);
+        const float su = allred<8, true>(ex, OpAdd{});
+        float wn = mx == NEG_INF ? NEG_INF : mx + fbs_log2(su);
+        const float wm = allred<8, false>(ra < K ? wn : NEG_INF, OpMax{});  // (beta's scale cancels)
+        wn = wm == NEG_INF ? wn : wn - wm;
+        if (cb == 0) g_wb[(s - 1) * 8 + ra] = wn;
+      }
+    }
+  }
+  __syncthreads();
+  stamp(5);
+
+  // ---------------------------------------------------------------- phase 3: the segment's chains + gamma
+  if (!flagged) {
+    float* ha = es;  // alpha history (the emission rows are no longer needed)
+    const int ub = fbs_vgpr(max(0, min(SEG, L - ts)));  // (a fresh copy: phase 1's compares are not kept)
+    const int uf = fbs_vgpr(w == 0 ? 1 : 0);
+    lo = 1.f;
+    hi = 1.f;
+    // alpha starts on step 0's i axis (ra), beta on step 63's j axis (odd: ra)
+    float xa, xb;
+    {
+      const float va = g_va[w * 8 + ra];
+      const float ma = allred<8, false>(va, OpMax{});
+      xa = ma == NEG_INF ? 0.f : fbs_exp2(va - ma);
+      const float vb = g_wb[w * 8 + ra];
+      const float mbx = allred<8, false>(vb, OpMax{});
+      xb = mbx == NEG_INF ? 0.f : fbs_exp2(vb - mbx);
+      hb[(SEG - 1) * 8 + ra] = xb;
+    }
+    static_for<SEG>([&](auto ki) {
+      constexpr int k = decltype(ki)::value;
+      {  // alpha step u = k: reduce over i (even: ra, odd: cb); the result sits on the j axis
+        constexpr int u = k, p = u & 1;
+        const float v = xa * tab[u];
+        float y = allred<8, p == 1>(v, OpAdd{});
+        if constexpr (u % 8 == 4) {
+          const int sx = __builtin_amdgcn_frexp_expf(allred<8, p == 1>(xa, OpMax{}));
+          y = __builtin_amdgcn_ldexpf(y, -sx);
+        }
+        const int jc = p ? ra : cb;
+        const bool chk = (jc < Kv) & (u < ub) & (u >= uf);  // transitions only
+        lo = chk ? fminf(lo, y) : lo;
+        hi = chk ? fmaxf(hi, y) : hi;
+        xa = y;
+        ha[u * 8 + jc] = y;
+      }
+      {  // beta step u = 63 - k: reduce over j (even: cb, odd: ra); the result sits on the i axis
+        constexpr int u = SEG - 1 - k, p = u & 1;
+        const float v = tab[u] * xb;
+        float y = allred<8, p == 0>(v, OpAdd{});
+        if constexpr (u % 8 == 4) {
+          const int sx = __builtin_amdgcn_frexp_expf(allred<8, p == 0>(xb, OpMax{}));
+          y = __builtin_amdgcn_ldexpf(y, -sx);
+        }
+        const int ic = p ? cb : ra;
+        const bool chk = (ic < Kv) & (u < ub) & (u >= uf);
+        lo = chk ? fminf(lo, y) : lo;
+        hi = chk ? fmaxf(hi, y) : hi;
+        xb = y;
+        if constexpr (u >= 1) hb[(u - 1) * 8 + ic] = y;
+      }
+    });
+    const int anybad = __builtin_amdgcn_ballot_w64(!fbs_in_range(lo, hi)) != 0;
+    stamp(6);
+    // gamma of the segment's steps: lane (ra, cb) = step 8 r + ra, state cb
+#pragma unroll
+    for (int r = 0; r < SEG / 8; ++r) {
+      const int u = r * 8 + ra, t = ts + u;
+      if (t < T) {
+        float gv = 0.f;
+        if (t < L) {
+          const float pr = cb < K ? ha[u * 8 + cb] * hb[u * 8 + cb] : 0.f;
+          const float su = allred<8, true>(pr, OpAdd{});
+          gv = pr * __builtin_amdgcn_rcpf(su);
+        }
+        if (cb < K) gq[(int64_t)t * K + cb] = gv;
+      }
+    }
+    if (lane == 0) g_flag[w] = anybad;
+    stamp(7);
+    __syncthreads();
+    for (int s = 0; s < nw; ++s) flagged |= g_flag[s];
+    if (!flagged) return;
+  }
+
+  // ---------------------------------------------------------------- exact path (rare): natural log,
+  // max-shifted LSE, both directions renormalised every step (offsets in fp64), the workspace holding
+  // alpha [B][T][K] and beta [B][T][K]; then gamma over the whole sequence.  Overwrites phase 3's gamma.
+  float* wal = ws + b * (int64_t)T * K;
+  float* wbe = ws + B * (int64_t)T * K + b * (int64_t)T * K;
+  if (w == 0) {
+    double S = 0.0;
+    // emissions enter framed by their step's max (e - E_t; E_t into the fp64 offset): e of about -1e3
+    // nats would otherwise cost the recursion's values their low bits
+    float a;
+    {
+      const float e0 = cb < K ? Eb[cb] : NEG_INF;
+      const float E0 = allred<8, true>(e0, OpMax{});
+      a = (cb < K && e0 != NEG_INF) ? log_pi[cb] + (e0 - E0) : NEG_INF;  // state on the inner axis (step 1 odd)
+      S += (double)E0;
+    }
+    {
+      const float mx = allred<8, true>(a, OpMax{});
+      if (mx == NEG_INF) S = -__builtin_inf();
+      else {
+        a -= mx;
+        S += mx;
+      }
+      if (ra == 0 && cb < K) wal[cb] = a;
+    }
+    for (int t = 1; t < L; ++t) {
+      const int p = t & 1;
+      const int i = p ? cb : ra, j = p ? ra : cb;
+      const float A = (i < K && j < K) ? Ab[(int64_t)t * K * K + i * K + j] : NEG_INF;
+      const float e = j < K ? Eb[(int64_t)t * K + j] : NEG_INF;
+      const float Et = p ? allred<8, false>(e, OpMax{}) : allred<8, true>(e, OpMax{});  // over the j axis
+      S += (double)Et;
+      const float v = a + A;
+      const float mx = p ? allred<8, true>(v, OpMax{}) : allred<8, false>(v, OpMax{});
+      const float ex = mx == NEG_INF ? 0.f : expf(v - mx);
+      const float su = p ? allred<8, true>(ex, OpAdd{}) : allred<8, false>(ex, OpAdd{});
+      float na = (mx == NEG_INF || e == NEG_INF) ? NEG_INF : (mx + logf(su)) + (e - Et);
+      const float nm = p ? allred<8, false>(na, OpMax{}) : allred<8, true>(na, OpMax{});
+      if (nm == NEG_INF) S = -__builtin_inf();
+      else {
+        na -= nm;
+        S += nm;
+      }
+      a = na;
+      if ((p ? cb : ra) == 0 && j < K) wal[(int64_t)t * K + j] = a;
+    }
+    // alpha_{L-1}'s state axis: inner for even L-1 (incl. L = 1), outer for odd
+    const bool inner = ((L - 1) & 1) == 0;
+    const int st = inner ? cb : ra;
+    const float x0 = st < K ? a : NEG_INF;
+    const float mx = inner ? allred<8, true>(x0, OpMax{}) : allred<8, false>(x0, OpMax{});
+    const float ex = mx == NEG_INF ? 0.f : expf(x0 - mx);
+    const float su = inner ? allred<8, true>(ex, OpAdd{}) : allred<8, false>(ex, OpAdd{});
+    if (lane == 0) logZ[b] = mx == NEG_INF ? NEG_INF : (float)(S + (double)mx + (double)logf(su));
+  }
+  if (w == (nw > 1 ? 1 : 0)) {
+    // beta_{L-1} = 0 on the j axis of step L-1's parity
+    const int p0 = (L - 1) & 1;
+    float be = ((p0 ? ra : cb) < K) ? 0.f : NEG_INF;
+    if ((p0 ? cb : ra) == 0 && (p0 ? ra : cb) < K) wbe[(int64_t)(L - 1) * K + (p0 ? ra : cb)] = 0.f;
+    for (int t = L - 1; t >= 1; --t) {
+      const int p = t & 1;
+      const int i = p ? cb : ra, j = p ? ra : cb;
+      const float A = (i < K && j < K) ? Ab[(int64_t)t * K * K + i * K + j] : NEG_INF;
+      const float e = j < K ? Eb[(int64_t)t * K + j] : NEG_INF;
+      const float Et = p ? allred<8, false>(e, OpMax{}) : allred<8, true>(e, OpMax{});  // over the j axis
+      const float v = (A + (e == NEG_INF ? NEG_INF : e - Et)) + be;
+      const float mx = p ? allred<8, false>(v, OpMax{}) : allred<8, true>(v, OpMax{});
+      const float ex = mx == NEG_INF ? 0.f : expf(v - mx);
+      const float su = p ? allred<8, false>(ex, OpAdd{}) : allred<8, true>(ex, OpAdd{});
+      float nb = mx == NEG_INF ? NEG_INF : mx + logf(su);
+      const float nm = p ? allred<8, true>(nb, OpMax{}) : allred<8, false>(nb, OpMax{});
+      if (nm != NEG_INF) nb -= nm;
+      be = nb;
+      if ((p ? ra : cb) == 0 && i < K) wbe[(int64_t)(t - 1) * K + i] = be;
+    }
+  }
+  __syncthreads();
+  for (int t = (int)threadIdx.x; t < T; t += (int)blockDim.x) {
+    float* gt = gq + (int64_t)t * K;
+    if (t >= L) {
+      for (int j = 0; j < K; ++j) gt[j] = 0.f;
+      continue;
+    }
+    float xs[8];
+    float mx = NEG_INF;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      xs[j] = j < K ? wal[(int64_t)t * K + j] + wbe[(int64_t)t * K + j] : NEG_INF;
+      mx = fmaxf(mx, xs[j]);
+    }
+    float su = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      xs[j] = (mx == NEG_INF || j >= K) ? 0.f : expf(xs[j] - mx);
+      su += xs[j];
+    }
+    for (int j = 0; j < 8; ++j)
+      if (j < K) gt[j] = mx == NEG_INF ? __builtin_nanf("") : xs[j] / su;
+  }
+}
+
+// VQHMM_FB_SEG=0: never the segmented kernel (a test switch read per call, like VQHMM_FB_RES)
+bool fwdbwd_seg_ok(int64_t B, int64_t T, int64_t K) {
+  const char* env = VQHMM_ENV("VQHMM_FB_SEG");
+  if (env && env[0] == '0') return false;
+  const bool force = env && env[0] == '1';  // tests: every K <= 8, every T <= 1024
+  if (B < 1 || K < 1 || K > 8 || T > (int64_t)FBS_SEG * FBS_MAXW || B > 0x7fffffff) return false;
+  return force || (K >= 5 && T >= 2 * FBS_SEG);
+}
+
+int launch_fwdbwd_seg(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths, int64_t B,
+                      int64_t T, int64_t K, float* gamma, float* logZ, float* ws, hipStream_t s) {
+  const int nw = (int)cdiv(T, FBS_SEG);
+  static const bool prof = [] {  // profiling build: phase stamps into the workspace (tools/fbseg_prof.py)
+    const char* e = VQHMM_PROF_ENV("VQHMM_FB_PROF");
+    return e && e[0] == '1';
+  }();
+  fwdbwd_seg_kernel<<<dim3((unsigned)B), dim3(64 * nw), fbs_lds_bytes(nw), s>>>(
+      log_pi, log_A, em, lengths, B, (int)T, (int)K, gamma, logZ, ws, prof ? (unsigned long long*)ws : nullptr);
+  VQHMM_LAUNCH_CHECK();
+  return VQHMM_OK;
+}
+
+}  // namespace vqhmm

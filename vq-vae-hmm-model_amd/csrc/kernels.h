@@ -131,8 +131,8 @@ struct WgradArgs {
 };
 
 struct HeadArgs {
-  int dbg;               // head_wave profiling switch (VQHMM_HEAD_DBG bits: 1 no A, 2 no B, 4 no C, 8 no
-                         // window loop); results then invalid.  0 in every product launch
+  int dbg;               // head profiling switch (profiling build, VQHMM_HEAD_DBG bits; 16: phase stamps);
+                         // 0 in every product launch
   int64_t B;
   int T;
   int64_t R;
@@ -330,9 +330,6 @@ bool fused_head_supported(const HeadArgs& a);
 int launch_staged_head(const StagedHeadArgs& a, int l2grid, hipStream_t s);
 
 int head_grid(int64_t R);
-// wave-window head (head_wave.hip), same support as head_mfma; its grid / slab count
-int head_wave_grid(int64_t R);
-int launch_head_wave(const HeadArgs& a, int grid, hipStream_t s);
 bool head_mfma_supported(const HeadArgs& a);
 int launch_head_mfma(const HeadArgs& a, int grid, hipStream_t s);
 // workgroup-cooperative MFMA head (head_coop.hip): K <= 8, U <= 4, TH in {64, 128, 256}, D <= 16; its
@@ -467,6 +464,10 @@ int launch_viterbi_wide(const float* log_pi, const float* log_A, const float* em
 int launch_fwdbwd_wide(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths, int64_t B,
                        int64_t T, int64_t K, float* gamma, float* logZ, float* ws, hipStream_t s);
 size_t fwdbwd_ws_bytes(int64_t B, int64_t T, int64_t K);
+// K <= 8, T <= 1024: parallel in time, one wave per 64-step segment (hmm_seg.hip)
+bool fwdbwd_seg_ok(int64_t B, int64_t T, int64_t K);
+int launch_fwdbwd_seg(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths, int64_t B,
+                      int64_t T, int64_t K, float* gamma, float* logZ, float* ws, hipStream_t s);
 int launch_viterbi(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths, int64_t B,
                    int64_t T, int64_t K, int32_t* path, float* score, void* ws, size_t ws_bytes, hipStream_t s);
 int launch_fwdbwd(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths, int64_t B,

@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # VQHMM_LIB_PATH: load another build of the same library (kernel A/B experiments only)
 LIB_PATH = os.environ.get("VQHMM_LIB_PATH") or os.path.join(_HERE, "libvqhmm.so")
 NPARAMS = 18
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 EUNSUPPORTED = -4
 _ERRORS = {-1: "invalid argument", -2: "kernel launch failed", -3: "workspace too small",
@@ -100,8 +100,9 @@ _SIGS = {
     "vqhmm_debug_prof": (ctypes.c_int, [ctypes.c_int, c_vp, c_i64]),
 }
 
-# bits of the step's device status word (include/vqhmm.h VQHMM_STATUS_*)
-STATUS_BITS = {1: "the backward tail's in-launch wait for the reduced decoder-conv1 gradient timed out"}
+# bits of the step's device status word (include/vqhmm.h VQHMM_STATUS_*): bit 1 is reserved and no kernel
+# sets it since the backward tail lost its in-launch wait (round 4)
+STATUS_BITS = {1: "reserved (no kernel sets it)"}
 
 
 def load():
@@ -111,12 +112,18 @@ def load():
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"vqhmm: native library not built ({LIB_PATH}); run `make -C {os.path.dirname(_HERE)}`")
         lib = ctypes.CDLL(LIB_PATH)
+        # the version first: a stale library lacks newer symbols and would fail below with a bare
+        # "undefined symbol" instead
+        ver = getattr(lib, "vqhmm_abi_version", None)
+        if ver is None:
+            raise RuntimeError(f"vqhmm: {LIB_PATH} exports no vqhmm_abi_version; rebuild the library")
+        ver.restype, ver.argtypes = c_i32, []
+        if ver() != ABI_VERSION:
+            raise RuntimeError(f"vqhmm: ABI version mismatch (library {ver()}, package {ABI_VERSION}); rebuild the library")
         for name, (res, args) in _SIGS.items():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.vqhmm_abi_version() != ABI_VERSION:
-            raise RuntimeError("vqhmm: ABI version mismatch; rebuild the library")
         _lib = lib
     return _lib
 
