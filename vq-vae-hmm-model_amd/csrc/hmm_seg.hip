@@ -63,6 +63,62 @@ __device__ __forceinline__ int fbs_vgpr(int x) {
   return v;
 }
 
+// 8-lane all-reduces for the linear chains (values >= 0), as hmm_lanes.h's allred but (a) the max on bit
+// patterns (v_max_i32: no NaN canonicalisation ops), (b) DPP without an "old" operand (folds into the add /
+// max) and (c) the permlane swaps as plain asm, which the scheduler may interleave with another chain's
+// (asm volatile pins every swap in program order: two chains in one wave then serialise)
+__device__ __forceinline__ float2 fbs_pair16(float x) {
+  float a = x, b = x;
+  asm("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+  return make_float2(a, b);
+}
+__device__ __forceinline__ float2 fbs_pair32(float x) {
+  float a = x, b = x;
+  asm("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+  return make_float2(a, b);
+}
+template <int CTRL>
+__device__ __forceinline__ float fbs_mdpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+template <bool INNER>
+__device__ __forceinline__ float fbs_sum8(float v) {
+  if constexpr (INNER) {
+    v += fbs_mdpp<DPP_XOR1>(v);
+    v += fbs_mdpp<DPP_XOR2>(v);
+    v += fbs_mdpp<DPP_HALF_MIRROR>(v);
+  } else {
+    v += fbs_mdpp<DPP_ROR8>(v);
+    const float2 a = fbs_pair16(v);
+    v = a.x + a.y;
+    const float2 c = fbs_pair32(v);
+    v = c.x + c.y;
+  }
+  return v;
+}
+template <bool INNER>
+__device__ __forceinline__ int fbs_maxb8(int v) {  // max of non-negative floats, on their bit patterns
+  auto mx = [](int a, float b) { return max(a, __builtin_bit_cast(int, b)); };
+  const float f = __builtin_bit_cast(float, v);
+  if constexpr (INNER) {
+    v = mx(v, fbs_mdpp<DPP_XOR1>(f));
+    v = mx(v, fbs_mdpp<DPP_XOR2>(__builtin_bit_cast(float, v)));
+    v = mx(v, fbs_mdpp<DPP_HALF_MIRROR>(__builtin_bit_cast(float, v)));
+  } else {
+    v = mx(v, fbs_mdpp<DPP_ROR8>(f));
+    const float2 a = fbs_pair16(__builtin_bit_cast(float, v));
+    v = max(__builtin_bit_cast(int, a.x), __builtin_bit_cast(int, a.y));
+    const float2 c = fbs_pair32(__builtin_bit_cast(float, v));
+    v = max(__builtin_bit_cast(int, c.x), __builtin_bit_cast(int, c.y));
+  }
+  return v;
+}
+// frexp exponent of the 8-lane max of x >= 0
+template <bool INNER>
+__device__ __forceinline__ int fbs_exp8(float x) {
+  return __builtin_amdgcn_frexp_expf(__builtin_bit_cast(float, fbs_maxb8<INNER>(__builtin_bit_cast(int, x))));
+}
+
 // One workgroup per sequence, one wave per 64-step segment.  Steps that are not transitions of the
 // sequence (t = 0, t >= L) carry the identity matrix, so every phase runs branch-free over its 64 steps:
 // alpha / beta pass such a step unchanged and the product ignores it.
@@ -282,9 +338,9 @@ __global__ __launch_bounds__(1024) void fwdbwd_seg_kernel(const float* __restric
       {  // alpha step u = k: reduce over i (even: ra, odd: cb); the result sits on the j axis
         constexpr int u = k, p = u & 1;
         const float v = xa * tab[u];
-        float y = allred<8, p == 1>(v, OpAdd{});
+        float y = fbs_sum8<p == 1>(v);
         if constexpr (u % 8 == 4) {
-          const int sx = __builtin_amdgcn_frexp_expf(allred<8, p == 1>(xa, OpMax{}));
+          const int sx = fbs_exp8<p == 1>(xa);
           y = __builtin_amdgcn_ldexpf(y, -sx);
         }
         const int jc = p ? ra : cb;
@@ -297,9 +353,9 @@ __global__ __launch_bounds__(1024) void fwdbwd_seg_kernel(const float* __restric
       {  // beta step u = 63 - k: reduce over j (even: cb, odd: ra); the result sits on the i axis
         constexpr int u = SEG - 1 - k, p = u & 1;
         const float v = tab[u] * xb;
-        float y = allred<8, p == 0>(v, OpAdd{});
+        float y = fbs_sum8<p == 0>(v);
         if constexpr (u % 8 == 4) {
-          const int sx = __builtin_amdgcn_frexp_expf(allred<8, p == 0>(xb, OpMax{}));
+          const int sx = fbs_exp8<p == 0>(xb);
           y = __builtin_amdgcn_ldexpf(y, -sx);
         }
         const int ic = p ? cb : ra;
