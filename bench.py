@@ -132,12 +132,26 @@ def traffic_for(kernel_name, cfg, batch=None):
         return None
 
 
-def traffic_checked(traffic, avg_us):
+def traffic_checked(traffic, avg_us, where=""):
     """A PMC byte count is kept only if it is physically possible for the launch it is quoted with
-    (traffic / duration <= the 8 TB/s HBM peak); otherwise null."""
+    (traffic / duration <= the 8 TB/s HBM peak); otherwise null, with the rejected figure reported by
+    traffic_rejected() and on stderr (a stale profiles/pmc_traffic.json or a wrong kernel match: regenerate
+    it with tools/gpu_pmc_r6.sh), so 'rejected' is not mistaken for 'not profiled'."""
     if traffic is None or avg_us is None or avg_us <= 0:
         return traffic
-    return traffic if traffic / (avg_us * 1e-6) <= HBM_PEAK_GBPS * 1e9 else None
+    if traffic / (avg_us * 1e-6) <= HBM_PEAK_GBPS * 1e9:
+        return traffic
+    print(f"bench.py: PMC traffic {traffic} B for {where or 'a launch'} implies "
+          f"{traffic / (avg_us * 1e-6) / 1e9:.0f} GB/s at {avg_us:.2f} us (> peak): reported as null",
+          file=sys.stderr)
+    return None
+
+
+def traffic_rejected(traffic, avg_us):
+    """The raw figure traffic_checked() nulled (bytes and the implied GB/s), or None."""
+    if traffic is None or avg_us is None or avg_us <= 0 or traffic / (avg_us * 1e-6) <= HBM_PEAK_GBPS * 1e9:
+        return None
+    return {"bytes": traffic, "implied_GBps": round(traffic / (avg_us * 1e-6) / 1e9, 1)}
 
 
 def vq_cfg3(lib):
@@ -164,7 +178,8 @@ def vq_cfg3(lib):
     gbps = byts / (us * 1e-6) / 1e9
     out = {"kernel": "vq_rows_kernel (vqhmm_vq_argmin_f32)", "bound": "hbm", "avg_us": round(us, 2),
            "achieved": round(gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(gbps / HBM_PEAK_GBPS, 4),
-           "traffic": traffic_checked(traffic_for("vq_argmin", "vq_cfg3"), us), "shape": "B2048 Dv64 T200 K32"}
+           "traffic": traffic_checked(traffic_for("vq_argmin", "vq_cfg3"), us, "vq_cfg3"),
+           "shape": "B2048 Dv64 T200 K32"}
     # the fused quantize (pseudocode.txt:12-18): argmin + z_q gather + straight-through value written +
     # squared-error partials, then the fixed-order partial sum: z read once, z_q_st and idx written
     zq = torch.empty_like(z)
@@ -235,7 +250,7 @@ def hmm_kernels(lib):
         gbps = byts / (us * 1e-6) / 1e9
         out[name] = {"kernel": kern, "bound": "hbm", "avg_us": round(us, 2), "achieved": round(gbps, 1),
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(gbps / HBM_PEAK_GBPS, 4),
-                     "traffic": traffic_checked(traffic_for(name, name), us), "shape": f"B{B} T{T} K{K}"}
+                     "traffic": traffic_checked(traffic_for(name, name), us, name), "shape": f"B{B} T{T} K{K}"}
         del log_A, em, ws
     # the fused Prior-MLP -> Viterbi at the same cfg5 shard: log_A is built on the chip
     # from u, so the kernel is bound by the MLP on the f32 MFMA: 2 (U + K^2) TH flops per position
@@ -479,9 +494,14 @@ def main():
             ach = dom["bytes"] / dur / 1e9
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBPS, 4)}
-        roof.update({"traffic": traffic_checked(traffic_for(dom["name"], a.config, B), dom["us"]),
+        raw = traffic_for(dom["name"], a.config, B)
+        roof.update({"traffic": traffic_checked(raw, dom["us"], dom["name"]),
                      "kernel": dom["name"], "avg_us": round(dom["us"], 2)})
-        kernels = {s["name"]: round(s["us"], 2) for s in stages}
+        if traffic_rejected(raw, dom["us"]):
+            roof["traffic_rejected"] = traffic_rejected(raw, dom["us"])
+        # per launch only: the stages that launch nothing of their own (named "(... in ...)": their work
+        # rides in a neighbour's launch) are left out; they would read ~5 us of event overhead each
+        kernels = {s["name"]: round(s["us"], 2) for s in stages if not s["name"].startswith("(")}
         # every launch's own roofline (SURVEY 8d asks for the H->H convs' MFMA fraction, not only the
         # dominant stage's): algorithmic flops (MFMA-bound) or bytes (HBM-bound) over the event-timed
         # stage duration (which includes ~5 us of event overhead: an empty stage reads ~5 us)
@@ -516,11 +536,19 @@ def main():
                        "global_batch": Bglob, "per_gpu_batch": B, "seq_len": T, "K": K, "input_dim": D,
                        "hidden_dim": H, "hidden_dim2": H2, "u_dim": U, "trans_hidden": TH,
                        "parallelism": f"dp{world}" if world > 1 else "single", "hip_graph": use_graph,
+                       # HIP runtime settings this process ran with (bench.py sets the graph packet-capture
+                       # switch before HIP starts; it changes only the DP form's graph replay, ~0.7 us/node)
+                       "hip_env": {k: os.environ[k] for k in ("DEBUG_CLR_GRAPH_PACKET_CAPTURE",
+                                                              "HIP_FORCE_DEV_KERNARG") if k in os.environ},
                        "step_form": _step_form(st, use_graph),
                        "collective": ({"backend": _backend_name(), "ranks": torch.distributed.get_world_size()}
                                       if torch.distributed.is_initialized() else None)},
             "roofline": roof, "cpu_baseline": cpu,
-            "step_kernels_us": kernels, "stage_roofline": stage_roof, "vq_cfg3": vq, **hmm,
+            "step_kernels_us": kernels,
+            "step_kernels_note": ("HIP-event time of each launch of the step run stage by stage (the forward "
+                                  "finalizing its own loss: need_grad=1, one launch the timed step does not "
+                                  "have); each includes ~5 us of event overhead"),
+            "stage_roofline": stage_roof, "vq_cfg3": vq, **hmm,
         }
         if cpu:
             line["speedup_vs_cpu"] = round(value / cpu["value"], 1)

@@ -78,7 +78,7 @@ def test_status_word_inside_workspace(dims, B, T):
 # the A/B switches the release library may read (common.h VQHMM_ENV): each selects between launch paths the
 # GPU tests prove bit-identical (VQHMM_STRIP_HEAD / VQHMM_HEAD: equal within their stated tolerance)
 RELEASE_SWITCHES = {"VQHMM_CONV_FUSE", "VQHMM_TAIL_FUSED", "VQHMM_STRIP", "VQHMM_STRIP_BWD", "VQHMM_STRIP_WGRAD", "VQHMM_STRIP_HEAD",
-                    "VQHMM_FB_RES", "VQHMM_FB_FUSE", "VQHMM_FB_PAIR", "VQHMM_HEAD"}
+                    "VQHMM_FB_RES", "VQHMM_FB_FUSE", "VQHMM_FB_PAIR", "VQHMM_FB_SEG", "VQHMM_HEAD"}
 
 
 def test_release_library_reads_no_profiling_knobs():

@@ -143,3 +143,53 @@ def test_prior_autograd_vs_oracle(B, T, K, lay, with_pi):
             continue
         _close(prm.grad, p[k].grad, k)
     _close(ug.grad, u64.grad, "du")
+
+
+@pytest.mark.parametrize("D,H,K,H2", [(16, 64, 8, 32), (64, 256, 32, 128)])
+def test_forward_autograd_wide_dims(D, H, K, H2):
+    """the module backward at cfg4 dims (D = 16, K = 8) and cfg3 dims (D = 64, H = 256, K = 32),
+    where other kernels run than at cfg2 (convbig / wgradbig past 64 channels, the channels-first dgrad
+    outputs): every encoder / decoder gradient, dx and dq against the fp64 oracle, small B and T."""
+    m = _model(D=D, H=H, K=K, H2=H2, seed=5)
+    B, T = 4, 40
+    g = torch.Generator().manual_seed(D + K)
+    x = torch.randn(B, D, T, generator=g)
+    G1, G2, G3 = (torch.randn(B, c, T, generator=g) for c in (D, D, K))
+    xg = x.cuda().requires_grad_(True)
+    (mu, logvar), q = m(xg)
+    ((mu * G1.cuda()).sum() + (logvar * G2.cuda()).sum() + (q * G3.cuda()).sum()).backward()
+    p = _p64(m)
+    x64 = x.double().requires_grad_(True)
+    rq = torch.softmax(RM.encoder_logits(p, x64), 1)
+    rmu, rlv = RM.decoder_params(p, rq)
+    _close(q, rq, "q")
+    _close(mu, rmu, "mu")
+    _close(logvar, rlv, "logvar")
+    ((rmu * G1.double()).sum() + (rlv * G2.double()).sum() + (rq * G3.double()).sum()).backward()
+    for k, prm in m.named_parameters():
+        if k.startswith("prior."):
+            assert prm.grad is None, k
+            continue
+        _close(prm.grad, p[k].grad, k)
+    _close(xg.grad, x64.grad, "dx")
+
+
+@pytest.mark.parametrize("D,H,K,H2", [(16, 64, 8, 32), (64, 256, 32, 128)])
+def test_decode_autograd_wide_dims(D, H, K, H2):
+    """decode alone at cfg4 / cfg3 dims: the decoder gradients and dq against the fp64 oracle."""
+    m = _model(D=D, H=H, K=K, H2=H2, seed=6)
+    B, T = 3, 33
+    g = torch.Generator().manual_seed(3 * D + K)
+    q = torch.softmax(torch.randn(B, K, T, generator=g), 1)
+    G1, G2 = torch.randn(B, D, T, generator=g), torch.randn(B, D, T, generator=g)
+    qg = q.cuda().requires_grad_(True)
+    mu, logvar = m.decode(qg)
+    ((mu * G1.cuda()).sum() + (logvar * G2.cuda()).sum()).backward()
+    p = _p64(m)
+    q64 = q.double().requires_grad_(True)
+    rmu, rlv = RM.decoder_params(p, q64)
+    ((rmu * G1.double()).sum() + (rlv * G2.double()).sum()).backward()
+    for k in ("decoder.embeddings.weight", "decoder.conv1.weight", "decoder.conv1.bias", "decoder.conv2.weight",
+              "decoder.conv2.bias", "decoder.to_params.weight", "decoder.to_params.bias"):
+        _close(dict(m.named_parameters())[k].grad, p[k].grad, k)
+    _close(qg.grad, q64.grad, "dq")

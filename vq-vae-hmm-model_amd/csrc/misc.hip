@@ -361,7 +361,9 @@ __global__ __launch_bounds__(256) void tail_kernel(TailArgs ta, AdamArgs ad, con
   }
 }
 
+static void prof_empties(const char* name, hipStream_t s);
 int launch_tail(TailArgs& ta, const AdamArgs* adam, const float* g, hipStream_t s) {
+  prof_empties("VQHMM_TAIL_EMPTY", s);
   if (ta.nseg > MAX_SEGS || (ta.q0slab && ta.lp.K > 256)) return VQHMM_EINVAL;
   for (int i = 0; i < ta.nseg; ++i)
     if (ta.s[i].cmpE && composed_block_cols(ta.s[i].cmpH, ta.s[i].cmpK) > 256) return VQHMM_EINVAL;
@@ -856,7 +858,20 @@ __global__ __launch_bounds__(256) void prologue_kernel(PrologueArgs a) {
     if (threadIdx.x == 0) *a.cnt = (int64_t)cred[0];
   }
 }
+// profiling build only (VQHMM_PRO_EMPTY / VQHMM_TAIL_EMPTY = n): n empty launches (256 workgroups, no LDS)
+// right before the prologue / the tail, to attribute what a launch costs after the one before it
+// (tools/gpu_launch_attr.sh)
+__global__ __launch_bounds__(256) void prof_empty_kernel(int* p) {
+  if (p && threadIdx.x == 0 && blockIdx.x == 0x7fffffff) p[0] = 1;
+}
+static void prof_empties(const char* name, hipStream_t s) {
+  const char* e = VQHMM_PROF_ENV(name);
+  const int n = e ? atoi(e) : 0;
+  for (int k = 0; k < n; ++k) prof_empty_kernel<<<256, 256, 0, s>>>(nullptr);
+}
+
 int launch_prologue(PrologueArgs a, hipStream_t s) {
+  prof_empties("VQHMM_PRO_EMPTY", s);
   {
     static const char* dbg = VQHMM_PROF_ENV("VQHMM_PRO_DBG");
     a.dbg = dbg ? atoi(dbg) : 0;
