@@ -34,9 +34,10 @@ namespace vqhmm {
 
 constexpr int FBS_SEG = 64;       // time steps per segment (= per wave)
 constexpr int FBS_MAXW = 16;      // segments per workgroup: T <= 1024
-constexpr int FBS_WAVE_F = 1152;  // LDS floats per wave: es/hist_a [64][8] | hist_b [64][8] | M [8][8] | P' [8][8]
+constexpr int FBS_WAVE_F = 1536;  // LDS floats per wave: es/hist_a [64][8] | hist_b [64][8] | P^T [2][4][8][8]
 constexpr float FBS_LOG2E = 1.44269504088896341f;
 constexpr double FBS_LN2 = 0.69314718055994531;
+typedef float fbs_f4 __attribute__((ext_vector_type(4)));
 
 // LDS of one workgroup of nw waves: the waves' regions, then the segment matrices (log2) [16][8][8], the
 // boundary vectors alpha [17][8] and beta [17][8] (log2), the segments' frame sums (fp64) and flags.
@@ -159,8 +160,6 @@ __global__ __launch_bounds__(1024) void fwdbwd_seg_kernel(const float* __restric
 
   float* es = sm + w * FBS_WAVE_F;  // [64][8]: e_t(j) - E_t (natural); phase 3: alpha history
   float* hb = es + 512;             // [64][8]: beta history
-  float* mb = es + 1024;            // [8][8]: M
-  float* pb = es + 1088;            // [8][8]: P transposed (column c at pb[c*8 ..])
   float* g_mlog = sm + nw * FBS_WAVE_F;  // [16][8][8] log2 M_s (row scale folded in)
   float* g_va = g_mlog + 1024;           // [17][8] alpha at segment boundaries (log2, framed)
   float* g_wb = g_va + 136;              // [17][8] beta at segment ends (log2)
@@ -191,68 +190,149 @@ __global__ __launch_bounds__(1024) void fwdbwd_seg_kernel(const float* __restric
 #pragma unroll
   for (int j = 0; j < 8; ++j) er[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rE, tl * K * 4 + j * 4, 0, 0));
   float tab[SEG];
-  static_for<48>([&](auto ui) {  // 8 + 48 loads in flight (vmcnt counts to 63)
-    constexpr int u = decltype(ui)::value;
+  // in phase 1's order (step s of the four chains: u = s, 16 + s, 32 + s, 48 + s); 8 + 48 loads in flight
+  // (vmcnt counts to 63), the last 16 issued by phase 1's first four steps
+  static_for<48>([&](auto ni) {
+    constexpr int n = decltype(ni)::value, u = (n & 3) * 16 + (n >> 2);
     tab[u] = tab_ld(u);
   });
   float E = NEG_INF;
 #pragma unroll
   for (int j = 0; j < 8; ++j) E = j < Kv ? fmaxf(E, er[j]) : E;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) es[lane * 8 + j] = er[j] - E;
+  for (int j = 0; j < 8; ++j) es[lane * 8 + j] = (er[j] - E) * FBS_LOG2E;  // (log2)
   // the frames of the sequence's steps in this segment (logZ = sum_t E_t + lg of the framed sums)
   const double esum = wave_sum_dpp((double)(tl < L ? E : 0.f));
   stamp(3);
 
-  // ---------------------------------------------------------------- phase 1: M_s = prod_t P_t
-  // Lane (ra, cb) holds M(ra, cb); row ra's scale 2^cx.  Step t: M'(r, c) = sum_k M(r, k) P_t(k, c), the row
-  // M(r, :) and the column P_t(:, c) read from LDS (the wave's own buffers: LDS ops retire in order).
-  float m = (ra == cb && ra < Kv) ? 1.f : 0.f;
-  const float ident = m;
+  // ---------------------------------------------------------------- phase 1: M_s = prod_t P_t (matrix pipe)
+  // Four chains per wave, chain q over the steps u = 16 q + s (s = 0..15), then (M_0 M_1)(M_2 M_3).  A chain
+  // step is 8 v_mfma_f32_4x4x1f32 (16 blocks of 4 x 4 x 1): lane l = 16 q + 8 I + 4 J + x is row / column x
+  // of block (q, I, J), and accumulator register i holds M(4 J + x, 4 I + i).  (M P) = sum_k M(:, k) P(k, :)
+  // blockwise: MFMA n contracts k = n ^ 4 I (each block its own order), A = P(k, 4 I + x) from the chain's
+  // P^T rows in LDS (written by the lanes of the table layout), B = M(4 J + x, k) = the lane's own register n
+  // (n < 4) or its I-partner's (lane ^ 8, DPP row_ror:8) register n - 4.  Each step rescales every row by the
+  // power of two of its max (row r's scale 2^cx on the two lanes holding it).
+  const int q = lane >> 4, bI = (lane >> 3) & 1, bJ = (lane >> 2) & 1, bx = lane & 3;
+  const int row = 4 * bJ + bx;
+  const bool rowreal = row < Kv;
+  fbs_f4 acc;
+  int padm[4];  // or-masks: an entry outside K x K reads as 1.0 in the range checks
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int col = 4 * bI + i;
+    acc[i] = (row == col && rowreal) ? 1.f : 0.f;
+    padm[i] = (rowreal && col < Kv) ? 0 : fbs_bits(1.f);
+  }
+  const float ident = (ra == cb && ra < Kv) ? 1.f : 0.f;  // the table layout's identity entry
   float cx = 0.f;  // (a float sum: integer adds get reassociated into a tree holding every step's exponent)
-  int lob = fbs_bits(1.f), hib = fbs_bits(1.f);  // range of the real entries (bit patterns, as rmax)
+  int lob = fbs_bits(1.f), hib = fbs_bits(1.f);  // range of the checked entries (bit patterns)
   const int ua = fbs_vgpr(max(0, min(SEG, L - ts)));  // steps u < ua are the sequence's (t < L)
   const int u_first = fbs_vgpr(w == 0 ? 1 : 0);      // (t = 0 is no transition)
-  static_for<SEG>([&](auto ui) {
-    constexpr int u = decltype(ui)::value, p = u & 1;
-    const int i = p ? cb : ra, j = p ? ra : cb;
-    float P = fbs_exp2((tab[u] + es[u * 8 + j]) * FBS_LOG2E);
-    const bool trans = (u < ua) & (u >= u_first);
-    P = fbs_pick(real & trans, P, ident);  // not a transition: identity
-    tab[u] = P;
-    if constexpr (u < 16) tab[u + 48] = tab_ld(u + 48);
-    pb[j * 8 + i] = P;
-    mb[lane] = m;
-    const float4 r0 = *reinterpret_cast<const float4*>(mb + ra * 8);
-    const float4 r1 = *reinterpret_cast<const float4*>(mb + ra * 8 + 4);
-    const float4 c0 = *reinterpret_cast<const float4*>(pb + cb * 8);
-    const float4 c1 = *reinterpret_cast<const float4*>(pb + cb * 8 + 4);
-    // row max on the bit patterns (M >= 0: integer order = float order; a NaN wins, and flags below)
-    const int rmax = max(max(max(fbs_bits(r0.x), fbs_bits(r0.y)), max(fbs_bits(r0.z), fbs_bits(r0.w))),
-                         max(max(fbs_bits(r1.x), fbs_bits(r1.y)), max(fbs_bits(r1.z), fbs_bits(r1.w))));
-    const int e = __builtin_amdgcn_frexp_expf(__builtin_bit_cast(float, rmax));
-    float s0 = r0.x * c0.x;
-    s0 = fmaf(r0.y, c0.y, s0);
-    s0 = fmaf(r0.z, c0.z, s0);
-    s0 = fmaf(r0.w, c0.w, s0);
-    float s1 = r1.x * c1.x;
-    s1 = fmaf(r1.y, c1.y, s1);
-    s1 = fmaf(r1.z, c1.z, s1);
-    s1 = fmaf(r1.w, c1.w, s1);
-    m = __builtin_amdgcn_ldexpf(s0 + s1, -e);
+  float* pbuf = es + 1024;                            // [2][4][8][8] the chains' P^T, double-buffered
+  auto trans_of = [&](int u) { return (u < ua) & (u >= u_first); };
+  auto rescale = [&]() {  // row max on the bit patterns (M >= 0: integer order = float order)
+    const int m4 = max(max(fbs_bits(acc[0]), fbs_bits(acc[1])), max(fbs_bits(acc[2]), fbs_bits(acc[3])));
+    const int m8 = max(m4, fbs_bits(fbs_mdpp<DPP_ROR8>(__builtin_bit_cast(float, m4))));
+    const int e = __builtin_amdgcn_frexp_expf(__builtin_bit_cast(float, m8));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = __builtin_amdgcn_ldexpf(acc[i], -e);
     cx += (float)e;
-    const int mc = (real & trans) ? fbs_bits(m) : fbs_bits(1.f);
-    lob = min(lob, mc);
-    hib = max(hib, mc);
+  };
+  auto checked = [&](int i, bool on) { return fbs_bits(acc[i]) | padm[i] | (on ? 0 : fbs_bits(1.f)); };
+  auto check_lo = [&](bool on) {  // (a NaN or inf persists to the final check's hi)
+    lob = min(lob, min(min(checked(0, on), checked(1, on)), min(checked(2, on), checked(3, on))));
+    asm volatile("" : "+v"(lob));  // min is associative: unpinned, the 16 steps' values become a tree held to the end
+  };
+  auto check_lohi = [&](bool on) {
+    check_lo(on);
+    hib = max(hib, max(max(checked(0, on), checked(1, on)), max(checked(2, on), checked(3, on))));
+  };
+  auto mstep = [&](const float* pq) {  // pq[c * 8 + k] = P(k, c) of this lane's chain
+    const float* pa = pq + (4 * bI + bx) * 8;
+    const float4 a0 = *reinterpret_cast<const float4*>(pa + 4 * bI);
+    const float4 a1 = *reinterpret_cast<const float4*>(pa + 4 - 4 * bI);
+    float d[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) d[i] = fbs_mdpp<DPP_ROR8>(acc[i]);
+    fbs_f4 c = {0.f, 0.f, 0.f, 0.f};
+    c = __builtin_amdgcn_mfma_f32_4x4x1f32(a0.x, acc[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_4x4x1f32(a0.y, acc[1], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_4x4x1f32(a0.z, acc[2], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_4x4x1f32(a0.w, acc[3], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_4x4x1f32(a1.x, d[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_4x4x1f32(a1.y, d[1], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_4x4x1f32(a1.z, d[2], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_4x4x1f32(a1.w, d[3], c, 0, 0, 0);
+    acc = c;
+  };
+  static_for<SEG / 4>([&](auto si) {
+    constexpr int s = decltype(si)::value, p = s & 1;
+    const int i = p ? cb : ra, j = p ? ra : cb;
+    float* pw = pbuf + (s & 1) * 256;
+    static_for<4>([&](auto qi) {
+      constexpr int qq = decltype(qi)::value, u = 16 * qq + s;
+      const float P = fbs_exp2(fmaf(tab[u], FBS_LOG2E, es[u * 8 + j]));
+      tab[u] = fbs_pick(real & trans_of(u), P, ident);  // not a transition: identity
+      pw[qq * 64 + j * 8 + i] = tab[u];
+    });
+    if constexpr (s < 4) {
+      static_for<4>([&](auto qi) {
+        constexpr int u = 16 * decltype(qi)::value + 12 + s;
+        tab[u] = tab_ld(u);
+      });
+    }
+    if constexpr (s > 0) {
+      rescale();
+      check_lo(trans_of(16 * q + s - 1));
+    }
+    mstep(pw + q * 64);
   });
-  float lo = __builtin_bit_cast(float, lob), hi = __builtin_bit_cast(float, hib);
+  rescale();
+  check_lohi(trans_of(16 * q + 15));
+  // combine: chain q + 1's matrix enters chain q's step as "P" = 2^(cx - cxm) M~ (cxm its largest real row
+  // scale, added to chain q's rows); a product is checked when both factors hold a transition
+  auto chain_max = [&](float v) {  // over the 16 lanes of a chain (rows: x and J; I repeats them)
+    v = fmaxf(v, fbs_mdpp<DPP_XOR1>(v));
+    v = fmaxf(v, fbs_mdpp<DPP_XOR2>(v));
+    return fmaxf(v, fbs_mdpp<DPP_ROR4>(v));
+  };
+  auto has_t = [&](int qq) { return ua > max(16 * qq, u_first); };
+  auto feed = [&](float* pq, float cxm) {  // this chain's matrix as the "P" at pq (P^T layout)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pq[(4 * bI + i) * 8 + row] = __builtin_amdgcn_ldexpf(acc[i], (int)(cx - cxm));
+  };
+  {
+    const float cxm = chain_max(rowreal ? cx : NEG_INF);
+    if (q & 1) feed(pbuf + (q - 1) * 64, cxm);
+    const float c1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cxm), 16));
+    const float c3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cxm), 48));
+    cx += q == 0 ? c1 : (q == 2 ? c3 : 0.f);
+    mstep(pbuf + q * 64);
+    rescale();
+    check_lohi(((q & 1) == 0) & has_t(q) & has_t(q + 1));
+  }
+  {
+    const float cxm = chain_max(rowreal ? cx : NEG_INF);
+    if (q == 2) feed(pbuf + 256, cxm);
+    cx += q == 0 ? __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cxm), 32)) : 0.f;
+    mstep(pbuf + 256 + q * 64);
+    rescale();
+    check_lohi((q == 0) & (has_t(0) | has_t(1)) & (has_t(2) | has_t(3)));
+  }
   {
     // the rows' scales relative to the largest (exact small integers): lg M stays O(10) in fp32, the
     // common scale c0 goes to the fp64 frame sum
-    const float c0 = allred<8, false>(ra < Kv ? cx : NEG_INF, OpMax{});
-    const float ml = m > 0.f ? fbs_log2(m) + (cx - c0) : NEG_INF;
-    g_mlog[w * 64 + lane] = real ? ml : NEG_INF;
-    const bool bad = real && !fbs_in_range(lo, hi);
+    const float c0 = chain_max(rowreal ? cx : NEG_INF);
+    if (q == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int col = 4 * bI + i;
+        const float ml = acc[i] > 0.f ? fbs_log2(acc[i]) + (cx - c0) : NEG_INF;
+        g_mlog[w * 64 + row * 8 + col] = (rowreal && col < Kv) ? ml : NEG_INF;
+      }
+    }
+    const bool bad = (lob < fbs_bits(0x1p-96f)) | (hib > fbs_bits(0x1p96f));
     const int anybad = __builtin_amdgcn_ballot_w64(bad) != 0;
     if (lane == 0) {
       g_flag[w] = anybad;
@@ -270,7 +350,7 @@ __global__ __launch_bounds__(1024) void fwdbwd_seg_kernel(const float* __restric
   if (!flagged) {
     if (w == 0) {
       // V_0(j) = lg alpha_0 (framed by E_0); V_{s+1}(c) = LSE_r(V_s(r) + lg M_s(r, c))
-      const float v0 = cb < K ? (log_pi[cb] + sm[cb]) * FBS_LOG2E : NEG_INF;  // sm = wave 0's es row 0
+      const float v0 = cb < K ? fmaf(log_pi[cb], FBS_LOG2E, sm[cb]) : NEG_INF;  // sm = wave 0's es row 0
       if (lane < 8) g_va[lane] = v0;
       // each V renormalised to max 0 (the offsets summed in fp64): V of a late segment would otherwise be
       // ~-1e3 and its fp32 ulp a 1e-5 relative error in 2^V
@@ -320,8 +400,8 @@ __global__ __launch_bounds__(1024) void fwdbwd_seg_kernel(const float* __restric
     float* ha = es;  // alpha history (the emission rows are no longer needed)
     const int ub = fbs_vgpr(max(0, min(SEG, L - ts)));  // (a fresh copy: phase 1's compares are not kept)
     const int uf = fbs_vgpr(w == 0 ? 1 : 0);
-    lo = 1.f;
-    hi = 1.f;
+    float lo = 1.f;
+    float hi = 1.f;
     // alpha starts on step 0's i axis (ra), beta on step 63's j axis (odd: ra)
     float xa, xb;
     {
