@@ -28,6 +28,8 @@
 // all -inf emission row).  Then the whole sequence is recomputed by the exact path below (max-shifted
 // natural-log recursions, renormalised every step, offsets in fp64, the workspace holding both
 // directions): the tier fallback of hmm.hip, per sequence.
+#include <type_traits>
+
 #include "hmm_lanes.h"
 
 namespace vqhmm {
@@ -348,47 +350,61 @@ __global__ __launch_bounds__(1024) void fwdbwd_seg_kernel(const float* __restric
   // Every segment's chain starts "at step -1" of the segment: segment 0 from alpha_0 (its step 0 is an
   // identity step), segment s from alpha at step 64 s - 1; beta from step 64 s + 63 (= beta_{L-1} past L).
   if (!flagged) {
+    // The vectors alternate axes step by step (V on ra's axis, lanes (r, *) holding V(r), before an even
+    // step; on cb's before an odd one), so each step reduces over the axis its input sits on and no LDS
+    // round trip sits in the chain.  Each result is shifted by the max of its column maxima (reduced beside
+    // the sum): V stays within [0, 3] at its max (a late segment's V would otherwise be ~-1e3 and its fp32
+    // ulp a 1e-5 relative error in 2^V); the forward shifts are summed in fp64, beta's cancel.
+    auto lse_step = [&](auto oddc, float v, float ml, float& sh) {  // LSE over the axis v sits on
+      constexpr bool ODD = decltype(oddc)::value;
+      const float x = v + ml;
+      const float mx = allred<8, ODD>(x, OpMax{});
+      const float ex = mx == NEG_INF ? 0.f : fbs_exp2(x - mx);
+      sh = allred<8, !ODD>(mx, OpMax{});
+      const float su = allred<8, ODD>(ex, OpAdd{});
+      const float vn = mx == NEG_INF ? NEG_INF : mx + fbs_log2(su);
+      return sh == NEG_INF ? vn : vn - sh;
+    };
     if (w == 0) {
       // V_0(j) = lg alpha_0 (framed by E_0); V_{s+1}(c) = LSE_r(V_s(r) + lg M_s(r, c))
       const float v0 = cb < K ? fmaf(log_pi[cb], FBS_LOG2E, sm[cb]) : NEG_INF;  // sm = wave 0's es row 0
       if (lane < 8) g_va[lane] = v0;
-      // each V renormalised to max 0 (the offsets summed in fp64): V of a late segment would otherwise be
-      // ~-1e3 and its fp32 ulp a 1e-5 relative error in 2^V
-      float vn = v0;
+      float v = ra < K ? fmaf(log_pi[ra], FBS_LOG2E, sm[ra]) : NEG_INF;  // V_0 on the ra axis
       double off = 0.0;
-      for (int s = 0; s < nw; ++s) {
-        const float x = g_va[s * 8 + ra] + g_mlog[s * 64 + lane];
-        const float mx = allred<8, false>(x, OpMax{});
-        const float ex = mx == NEG_INF ? 0.f : fbs_exp2(x - mx);
-        const float su = allred<8, false>(ex, OpAdd{});
-        vn = mx == NEG_INF ? NEG_INF : mx + fbs_log2(su);
-        const float vm = allred<8, true>(cb < K ? vn : NEG_INF, OpMax{});
-        if (vm != NEG_INF) {
-          vn -= vm;
-          off += (double)vm;
-        }
-        if (lane < 8) g_va[(s + 1) * 8 + lane] = vn;
+      auto fwd = [&](auto oddc, int s) {
+        constexpr bool ODD = decltype(oddc)::value;
+        float sh;
+        v = lse_step(oddc, v, g_mlog[s * 64 + (ODD ? cb * 8 + ra : lane)], sh);  // M_s(r, c), r on v's axis
+        off += sh == NEG_INF ? 0.0 : (double)sh;
+        if ((ODD ? cb : ra) == 0) g_va[(s + 1) * 8 + (ODD ? ra : cb)] = v;
+      };
+      for (int s = 0; s < nw; s += 2) {
+        fwd(std::false_type{}, s);
+        if (s + 1 < nw) fwd(std::true_type{}, s + 1);
       }
-      // logZ = ln 2 * (lg sum_j 2^V_S(j) + the offsets) + the frames
-      const float vx = cb < K ? vn : NEG_INF;
-      const float mx = allred<8, true>(vx, OpMax{});
-      const float su = allred<8, true>(mx == NEG_INF ? 0.f : fbs_exp2(vx - mx), OpAdd{});
+      // logZ = ln 2 * (lg sum_j 2^V_S(j) + the offsets) + the frames; V_S on cb's axis for odd S
+      const bool on_cb = nw & 1;
+      const float vx = (on_cb ? cb : ra) < K ? v : NEG_INF;
+      const float mx = on_cb ? allred<8, true>(vx, OpMax{}) : allred<8, false>(vx, OpMax{});
+      const float ex = mx == NEG_INF ? 0.f : fbs_exp2(vx - mx);
+      const float su = on_cb ? allred<8, true>(ex, OpAdd{}) : allred<8, false>(ex, OpAdd{});
       double fr = 0.0;
       for (int s = 0; s < nw; ++s) fr += g_esum[s];
       if (lane == 0) logZ[b] = (float)(FBS_LN2 * ((double)mx + (double)fbs_log2(su) + off) + fr);
     }
     if (w == (nw > 1 ? 1 : 0)) {
-      // W_{S-1} = 0; W_{s-1}(r) = LSE_c(lg M_s(r, c) + W_s(c)) = beta at step 64 s - 1
-      if (lane < 8) g_wb[(nw - 1) * 8 + lane] = lane < K ? 0.f : NEG_INF;
-      for (int s = nw - 1; s >= 1; --s) {
-        const float x = g_mlog[s * 64 + lane] + g_wb[s * 8 + cb];
-        const float mx = allred<8, true>(x, OpMax{});
-        const float ex = mx == NEG_INF ? 0.f : fbs_exp2(x - mx);
-        const float su = allred<8, true>(ex, OpAdd{});
-        float wn = mx == NEG_INF ? NEG_INF : mx + fbs_log2(su);
-        const float wm = allred<8, false>(ra < K ? wn : NEG_INF, OpMax{});  // (beta's scale cancels)
-        wn = wm == NEG_INF ? wn : wn - wm;
-        if (cb == 0) g_wb[(s - 1) * 8 + ra] = wn;
+      // W_{S-1} = 0; W_{s-1}(r) = LSE_c(lg M_s(r, c) + W_s(c)) = beta at step 64 s - 1; W_{S-1} on cb's axis
+      float v = cb < K ? 0.f : NEG_INF;
+      if (lane < 8) g_wb[(nw - 1) * 8 + lane] = v;
+      auto bwd = [&](auto oddc, int s) {
+        constexpr bool ODD = decltype(oddc)::value;  // even: x(r = ra, c = cb), reduced over cb
+        float sh;
+        v = lse_step(std::integral_constant<bool, !ODD>{}, v, g_mlog[s * 64 + (ODD ? cb * 8 + ra : lane)], sh);
+        if ((ODD ? ra : cb) == 0) g_wb[(s - 1) * 8 + (ODD ? cb : ra)] = v;
+      };
+      for (int s = nw - 1; s >= 1; s -= 2) {
+        bwd(std::false_type{}, s);
+        if (s - 1 >= 1) bwd(std::true_type{}, s - 1);
       }
     }
   }
@@ -398,10 +414,19 @@ __global__ __launch_bounds__(1024) void fwdbwd_seg_kernel(const float* __restric
   // ---------------------------------------------------------------- phase 3: the segment's chains + gamma
   if (!flagged) {
     float* ha = es;  // alpha history (the emission rows are no longer needed)
-    const int ub = fbs_vgpr(max(0, min(SEG, L - ts)));  // (a fresh copy: phase 1's compares are not kept)
-    const int uf = fbs_vgpr(w == 0 ? 1 : 0);
-    float lo = 1.f;
-    float hi = 1.f;
+    // range checks on the bit patterns (values >= 0): an entry off the K axis or a step that is no
+    // transition reads as 1.0 (or-mask), the min / max pinned per step (associative: left alone they become
+    // a tree holding all 128 values)
+    const int ubs = __builtin_amdgcn_readfirstlane(max(0, min(SEG, L - ts)));
+    const int ufs = w == 0 ? 1 : 0;
+    const int pm_ra = ra < Kv ? 0 : fbs_bits(1.f), pm_cb = cb < Kv ? 0 : fbs_bits(1.f);
+    int lob = fbs_bits(1.f), hib = fbs_bits(1.f);
+    auto check = [&](float y, int pm, int u) {
+      const int t = fbs_bits(y) | pm | (((u < ubs) & (u >= ufs)) ? 0 : fbs_bits(1.f));
+      lob = min(lob, t);
+      hib = max(hib, t);
+      asm volatile("" : "+v"(lob), "+v"(hib));
+    };
     // alpha starts on step 0's i axis (ra), beta on step 63's j axis (odd: ra)
     float xa, xb;
     {
@@ -424,9 +449,7 @@ __global__ __launch_bounds__(1024) void fwdbwd_seg_kernel(const float* __restric
           y = __builtin_amdgcn_ldexpf(y, -sx);
         }
         const int jc = p ? ra : cb;
-        const bool chk = (jc < Kv) & (u < ub) & (u >= uf);  // transitions only
-        lo = chk ? fminf(lo, y) : lo;
-        hi = chk ? fmaxf(hi, y) : hi;
+        check(y, p ? pm_ra : pm_cb, u);  // transitions only
         xa = y;
         ha[u * 8 + jc] = y;
       }
@@ -439,14 +462,13 @@ __global__ __launch_bounds__(1024) void fwdbwd_seg_kernel(const float* __restric
           y = __builtin_amdgcn_ldexpf(y, -sx);
         }
         const int ic = p ? cb : ra;
-        const bool chk = (ic < Kv) & (u < ub) & (u >= uf);
-        lo = chk ? fminf(lo, y) : lo;
-        hi = chk ? fmaxf(hi, y) : hi;
+        check(y, p ? pm_cb : pm_ra, u);
         xb = y;
         if constexpr (u >= 1) hb[(u - 1) * 8 + ic] = y;
       }
     });
-    const int anybad = __builtin_amdgcn_ballot_w64(!fbs_in_range(lo, hi)) != 0;
+    const int anybad =
+        __builtin_amdgcn_ballot_w64((lob < fbs_bits(0x1p-96f)) | (hib > fbs_bits(0x1p96f))) != 0;
     stamp(6);
     // gamma of the segment's steps: lane (ra, cb) = step 8 r + ra, state cb
 #pragma unroll
