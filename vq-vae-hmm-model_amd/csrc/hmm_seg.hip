@@ -99,6 +99,20 @@ __device__ __forceinline__ float fbs_sum8(float v) {
   }
   return v;
 }
+// two 8-lane sums over the outer axis at once (alpha's and beta's on even k): after the row_ror:8 adds, one
+// 16-swap leaves a's row-pair sums in rows 0 / 2 and b's in 1 / 3, a 32-swap completes both, a last 16-swap
+// spreads each over all rows (3 swaps for the two, 4 apart)
+__device__ __forceinline__ void fbs_sum8_outer2(float a, float b, float& ya, float& yb) {
+  a += fbs_mdpp<DPP_ROR8>(a);
+  b += fbs_mdpp<DPP_ROR8>(b);
+  asm("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));  // a = [a0 b0 a2 b2], b = [a1 b1 a3 b3]
+  float c = a + b, d = c;
+  asm("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(c), "+v"(d));  // c = [c0 c1 c0 c1], d = [c2 c3 c2 c3]
+  float e = c + d, f = e;                                                 // [A B A B]
+  asm("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(e), "+v"(f));  // e = [A A A A], f = [B B B B]
+  ya = e;
+  yb = f;
+}
 template <bool INNER>
 __device__ __forceinline__ int fbs_maxb8(int v) {  // max of non-negative floats, on their bit patterns
   auto mx = [](int a, float b) { return max(a, __builtin_bit_cast(int, b)); };
@@ -440,10 +454,20 @@ __global__ __launch_bounds__(1024) void fwdbwd_seg_kernel(const float* __restric
     }
     static_for<SEG>([&](auto ki) {
       constexpr int k = decltype(ki)::value;
-      {  // alpha step u = k: reduce over i (even: ra, odd: cb); the result sits on the j axis
+      // alpha step u = k reduces over i (even: ra, odd: cb), the result on the j axis; beta step 63 - k over
+      // j (odd: ra, even: cb), the result on the i axis.  On even k both reduce over ra: one set of swaps
+      float ya, yb;
+      {
+        const float va = xa * tab[k], vb = tab[SEG - 1 - k] * xb;
+        if constexpr ((k & 1) == 0) fbs_sum8_outer2(va, vb, ya, yb);
+        else {
+          ya = fbs_sum8<true>(va);
+          yb = fbs_sum8<true>(vb);
+        }
+      }
+      {
         constexpr int u = k, p = u & 1;
-        const float v = xa * tab[u];
-        float y = fbs_sum8<p == 1>(v);
+        float y = ya;
         if constexpr (u % 8 == 4) {
           const int sx = fbs_exp8<p == 1>(xa);
           y = __builtin_amdgcn_ldexpf(y, -sx);
@@ -453,10 +477,9 @@ __global__ __launch_bounds__(1024) void fwdbwd_seg_kernel(const float* __restric
         xa = y;
         ha[u * 8 + jc] = y;
       }
-      {  // beta step u = 63 - k: reduce over j (even: cb, odd: ra); the result sits on the i axis
+      {
         constexpr int u = SEG - 1 - k, p = u & 1;
-        const float v = tab[u] * xb;
-        float y = fbs_sum8<p == 0>(v);
+        float y = yb;
         if constexpr (u % 8 == 4) {
           const int sx = fbs_exp8<p == 0>(xb);
           y = __builtin_amdgcn_ldexpf(y, -sx);
