@@ -435,10 +435,12 @@ __global__ __launch_bounds__(1024) void fwdbwd_seg_kernel(const float* __restric
     const int ufs = w == 0 ? 1 : 0;
     const int pm_ra = ra < Kv ? 0 : fbs_bits(1.f), pm_cb = cb < Kv ? 0 : fbs_bits(1.f);
     int lob = fbs_bits(1.f), hib = fbs_bits(1.f);
-    auto check = [&](float y, int pm, int u) {
-      const int t = fbs_bits(y) | pm | (((u < ubs) & (u >= ufs)) ? 0 : fbs_bits(1.f));
-      lob = min(lob, t);
-      hib = max(hib, t);
+    auto masked = [&](float y, int pm, int u) {
+      return fbs_bits(y) | pm | (((u < ubs) & (u >= ufs)) ? 0 : fbs_bits(1.f));
+    };
+    auto check2 = [&](int ta, int tb) {  // alpha's and beta's values of one k (v_min3 / v_max3)
+      lob = min(lob, min(ta, tb));
+      hib = max(hib, max(ta, tb));
       asm volatile("" : "+v"(lob), "+v"(hib));
     };
     // alpha starts on step 0's i axis (ra), beta on step 63's j axis (odd: ra)
@@ -457,8 +459,11 @@ __global__ __launch_bounds__(1024) void fwdbwd_seg_kernel(const float* __restric
       // alpha step u = k reduces over i (even: ra, odd: cb), the result on the j axis; beta step 63 - k over
       // j (odd: ra, even: cb), the result on the i axis.  On even k both reduce over ra: one set of swaps
       float ya, yb;
+      int ta;
       {
-        const float va = xa * tab[k], vb = tab[SEG - 1 - k] * xb;
+        float va = xa * tab[k], vb = tab[SEG - 1 - k] * xb;
+        asm("" : "+v"(va), "+v"(vb));  // (else the product is folded into the first reduction step as an
+                                        // fma, recomputing it beside a DPP move: 3 instructions for 2)
         if constexpr ((k & 1) == 0) fbs_sum8_outer2(va, vb, ya, yb);
         else {
           ya = fbs_sum8<true>(va);
@@ -473,7 +478,7 @@ __global__ __launch_bounds__(1024) void fwdbwd_seg_kernel(const float* __restric
           y = __builtin_amdgcn_ldexpf(y, -sx);
         }
         const int jc = p ? ra : cb;
-        check(y, p ? pm_ra : pm_cb, u);  // transitions only
+        ta = masked(y, p ? pm_ra : pm_cb, u);  // transitions only
         xa = y;
         ha[u * 8 + jc] = y;
       }
@@ -485,7 +490,7 @@ __global__ __launch_bounds__(1024) void fwdbwd_seg_kernel(const float* __restric
           y = __builtin_amdgcn_ldexpf(y, -sx);
         }
         const int ic = p ? cb : ra;
-        check(y, p ? pm_cb : pm_ra, u);
+        check2(ta, masked(y, p ? pm_cb : pm_ra, u));
         xb = y;
         if constexpr (u >= 1) hb[(u - 1) * 8 + ic] = y;
       }
