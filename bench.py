@@ -43,6 +43,9 @@ import time
 # that replays ~0.7 us per node slower than with it off (B = 128 one-graph DP step 0.1041 -> 0.1005 ms,
 # tools/gpu_graph_ab.sh).  Read once at HIP initialisation, so it is set before torch touches the GPU.
 os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+# Kernel arguments in device memory (vqhmm sets the same default on import; here it must precede torch's
+# first GPU call): B = 128 0.1082 -> 0.0939 ms, cfg2 0.4342 -> 0.4199 ms (tools/gpu_kernarg_ab.sh).
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
 
 import torch
 

@@ -379,6 +379,9 @@ __global__ __launch_bounds__(1024) void fwdbwd_seg_kernel(const float* __restric
       const float vn = mx == NEG_INF ? NEG_INF : mx + fbs_log2(su);
       return sh == NEG_INF ? vn : vn - sh;
     };
+    // the two serial chains run while the workgroup's other waves wait at the barrier: raised priority,
+    // so the co-resident workgroup's waves on the same SIMDs do not take their issue slots
+    if (w <= 1) __builtin_amdgcn_s_setprio(3);
     if (w == 0) {
       // V_0(j) = lg alpha_0 (framed by E_0); V_{s+1}(c) = LSE_r(V_s(r) + lg M_s(r, c))
       const float v0 = cb < K ? fmaf(log_pi[cb], FBS_LOG2E, sm[cb]) : NEG_INF;  // sm = wave 0's es row 0
@@ -422,6 +425,7 @@ __global__ __launch_bounds__(1024) void fwdbwd_seg_kernel(const float* __restric
       }
     }
   }
+  __builtin_amdgcn_s_setprio(0);
   __syncthreads();
   stamp(5);
 

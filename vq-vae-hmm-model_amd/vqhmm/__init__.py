@@ -6,13 +6,21 @@ train_model, RandomChunkDataset, collate_fn — plus the hard-regime kernels
 vq_argmin / forward_backward / viterbi.  All compute runs in hand-written HIP
 kernels in libvqhmm.so; there is no CPU fallback.
 """
-from . import _ext  # noqa: F401
-from .checkpoint import load_checkpoint, load_encoder, save_checkpoint, save_encoder  # noqa: F401
-from .data import DeviceChunkLoader, RandomChunkDataset, collate_fn  # noqa: F401
-from .hmm import forward_backward, quantize, regime_argmax, viterbi, vq_argmin  # noqa: F401
-from .infer import hard_regimes, infer, prior_viterbi, viterbi_regimes  # noqa: F401
-from .model import PARAM_ORDER, VAE_HMM, Decoder, Encoder, Prior  # noqa: F401
-from .train import Trainer, TrainState, train_model  # noqa: F401
+import os as _os
+
+# Kernel arguments in device memory instead of host memory: a dispatch's argument fetch then does not cross
+# PCIe, which is most of a short launch's fixed cost here (tools/gpu_kernarg_ab.sh, alternating on one box:
+# B = 128 step 0.1082 -> 0.0939 ms, its DP form 0.1149 -> 0.0995, cfg2 0.4342 -> 0.4199).  Read when the HIP
+# runtime initialises, i.e. effective when this package is imported before the process's first GPU call.
+_os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+
+from . import _ext  # noqa: E402,F401
+from .checkpoint import load_checkpoint, load_encoder, save_checkpoint, save_encoder  # noqa: E402,F401
+from .data import DeviceChunkLoader, RandomChunkDataset, collate_fn  # noqa: E402,F401
+from .hmm import forward_backward, quantize, regime_argmax, viterbi, vq_argmin  # noqa: E402,F401
+from .infer import hard_regimes, infer, prior_viterbi, viterbi_regimes  # noqa: E402,F401
+from .model import PARAM_ORDER, VAE_HMM, Decoder, Encoder, Prior  # noqa: E402,F401
+from .train import Trainer, TrainState, train_model  # noqa: E402,F401
 
 __all__ = ["VAE_HMM", "Encoder", "Prior", "Decoder", "train_model", "Trainer", "TrainState", "RandomChunkDataset",
            "collate_fn", "DeviceChunkLoader", "vq_argmin", "quantize", "regime_argmax", "viterbi", "forward_backward", "PARAM_ORDER",
