@@ -13,15 +13,16 @@
 //
 //   phase 1  each wave loads its segment's table ONCE into 64 VGPRs (lane (r, c) holds entry (i, j) of
 //            step t, the (i, j) <-> lane map alternating with t's parity as in hmm.hip) and forms the
-//            segment's transfer matrix M_s = prod_t P_t (lane (r, c) holds M(r, c); per step the row r of
-//            M and column c of P come through LDS, 8 FMAs, the row rescaled by a power of two).
+//            segment's transfer matrix M_s = prod_t P_t on the matrix pipe: four 16-step chains per wave
+//            as 16 blocks of v_mfma_f32_4x4x1f32, combined (M_0 M_1)(M_2 M_3) (layout at the code).
 //   phase 2  one wave chains the S segment matrices forward for the alpha vector at every segment
-//            boundary, another backward for beta (log2 domain, max-shifted LSE; S steps, not T).
+//            boundary, another backward for beta (log2 domain, max-shifted LSE; S steps, not T; the vector
+//            alternates lane axes step by step, so no LDS round trip sits in the chain).
 //   phase 3  each wave reruns its segment's alpha and beta vector chains from those boundary vectors
 //            on the tables still in its registers (the two chains interleaved, rescaled every 8 steps),
 //            keeps both histories in LDS and writes gamma_t = alpha_t beta_t / sum for its 64 steps.
 //
-// HBM sees log_A and em once and gamma once (the algorithmic bytes); the serial chain is 64 matrix
+// HBM sees log_A and em once and gamma once (the algorithmic bytes); the serial chain is 16 + 2 matrix
 // steps + S + 64 vector steps instead of L.  Range: a value that leaves [2^-96, 2^96] anywhere (a
 // matrix entry relative to its row's last scale, a chain value relative to its last rescale) means
 // something nearly vanished or exploded in fp32, as do -inf / NaN inputs (an exact 0 table entry, an
@@ -49,8 +50,6 @@ __host__ __device__ constexpr size_t fbs_lds_bytes(int nw) {
 
 __device__ __forceinline__ float fbs_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 __device__ __forceinline__ float fbs_log2(float x) { return __builtin_amdgcn_logf(x); }
-// a value the linear forms may carry: within [2^-96, 2^96] (false for 0, inf, NaN)
-__device__ __forceinline__ bool fbs_in_range(float lo, float hi) { return lo >= 0x1p-96f && hi <= 0x1p96f; }
 // c ? a : b with a computed unconditionally: left to itself the compiler turns the select into a branch
 // around a's computation and sinks the step's table load into it, draining vmcnt there
 __device__ __forceinline__ float fbs_pick(bool c, float a, float b) {
@@ -313,7 +312,7 @@ __global__ __launch_bounds__(1024) void fwdbwd_seg_kernel(const float* __restric
     v = fmaxf(v, fbs_mdpp<DPP_XOR2>(v));
     return fmaxf(v, fbs_mdpp<DPP_ROR4>(v));
   };
-  auto has_t = [&](int qq) { return ua > max(16 * qq, u_first); };
+  auto has_t = [&](int qq) -> int { return ua > max(16 * qq, u_first); };
   auto feed = [&](float* pq, float cxm) {  // this chain's matrix as the "P" at pq (P^T layout)
 #pragma unroll
     for (int i = 0; i < 4; ++i) pq[(4 * bI + i) * 8 + row] = __builtin_amdgcn_ldexpf(acc[i], (int)(cx - cxm));
@@ -326,7 +325,7 @@ __global__ __launch_bounds__(1024) void fwdbwd_seg_kernel(const float* __restric
     cx += q == 0 ? c1 : (q == 2 ? c3 : 0.f);
     mstep(pbuf + q * 64);
     rescale();
-    check_lohi(((q & 1) == 0) & has_t(q) & has_t(q + 1));
+    check_lohi((int)((q & 1) == 0) & has_t(q) & has_t(q + 1));
   }
   {
     const float cxm = chain_max(rowreal ? cx : NEG_INF);
@@ -334,7 +333,7 @@ __global__ __launch_bounds__(1024) void fwdbwd_seg_kernel(const float* __restric
     cx += q == 0 ? __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cxm), 32)) : 0.f;
     mstep(pbuf + 256 + q * 64);
     rescale();
-    check_lohi((q == 0) & (has_t(0) | has_t(1)) & (has_t(2) | has_t(3)));
+    check_lohi((int)(q == 0) & (has_t(0) | has_t(1)) & (has_t(2) | has_t(3)));
   }
   {
     // the rows' scales relative to the largest (exact small integers): lg M stays O(10) in fp32, the
@@ -348,7 +347,7 @@ __global__ __launch_bounds__(1024) void fwdbwd_seg_kernel(const float* __restric
         g_mlog[w * 64 + row * 8 + col] = (rowreal && col < Kv) ? ml : NEG_INF;
       }
     }
-    const bool bad = (lob < fbs_bits(0x1p-96f)) | (hib > fbs_bits(0x1p96f));
+    const bool bad = (int)(lob < fbs_bits(0x1p-96f)) | (int)(hib > fbs_bits(0x1p96f));
     const int anybad = __builtin_amdgcn_ballot_w64(bad) != 0;
     if (lane == 0) {
       g_flag[w] = anybad;
@@ -500,7 +499,7 @@ __global__ __launch_bounds__(1024) void fwdbwd_seg_kernel(const float* __restric
       }
     });
     const int anybad =
-        __builtin_amdgcn_ballot_w64((lob < fbs_bits(0x1p-96f)) | (hib > fbs_bits(0x1p96f))) != 0;
+        __builtin_amdgcn_ballot_w64((int)(lob < fbs_bits(0x1p-96f)) | (int)(hib > fbs_bits(0x1p96f))) != 0;
     stamp(6);
     // gamma of the segment's steps: lane (ra, cb) = step 8 r + ra, state cb
 #pragma unroll
