@@ -116,7 +116,11 @@ int vqhmm_viterbi_f32(const float* log_pi, const float* log_A, const float* em, 
  * Posterior marginals: same inputs as Viterbi ->
  * gamma (B,T,K) fp32 (0 at t >= length), logZ (B) fp32 (NaN if length 0).
  * Base-2 log-space alpha/beta with per-step shifts; a chunk whose fast step
- * leaves float range is recomputed with the max-shifted log-sum-exp.
+ * leaves float range is recomputed with the max-shifted log-sum-exp.  For
+ * 2 <= K <= 8 and 128 <= T <= 1024 (K = 4: T > 256) the kernel is parallel in
+ * time (64-step segments' transfer matrices on the matrix cores, a boundary
+ * pass, then per-segment chains; hmm_seg.hip); a sequence that leaves the
+ * linear range there is recomputed exactly in the same launch.
  * Workspace: vqhmm_fwdbwd_workspace_size(B, T, K) = 2 * B * T * K * 4 bytes.
  * Accuracy target vs the fp64 oracle: |gamma| abs 1e-5, logZ rel 1e-5.  K <= 4096 (as Viterbi). */
 size_t vqhmm_fwdbwd_workspace_size(int64_t B, int64_t T, int64_t K);

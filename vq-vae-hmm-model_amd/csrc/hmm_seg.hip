@@ -630,7 +630,10 @@ bool fwdbwd_seg_ok(int64_t B, int64_t T, int64_t K) {
   if (env && env[0] == '0') return false;
   const bool force = env && env[0] == '1';  // tests: every K <= 8, every T <= 1024
   if (B < 1 || K < 1 || K > 8 || T > (int64_t)FBS_SEG * FBS_MAXW || B > 0x7fffffff) return false;
-  return force || (K >= 5 && T >= 2 * FBS_SEG);
+  // measured against hmm.hip's kernels (tools/kbench.py, profiles/r06/fwdbwd/kbench_smallk.txt): faster at every
+  // K >= 2 for T >= 128 except K = 4 at T <= 256, where hmm.hip's 4-lane groups win (B = 1024, T = 200: 25.6 vs
+  // 28.2 us)
+  return force || (K >= 2 && T >= 2 * FBS_SEG && (K != 4 || T > 4 * FBS_SEG));
 }
 
 int launch_fwdbwd_seg(const float* log_pi, const float* log_A, const float* em, const int64_t* lengths, int64_t B,
