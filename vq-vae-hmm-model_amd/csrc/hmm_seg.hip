@@ -501,18 +501,30 @@ __global__ __launch_bounds__(1024) void fwdbwd_seg_kernel(const float* __restric
     const int anybad =
         __builtin_amdgcn_ballot_w64((int)(lob < fbs_bits(0x1p-96f)) | (int)(hib > fbs_bits(0x1p96f))) != 0;
     stamp(6);
-    // gamma of the segment's steps: lane (ra, cb) = step 8 r + ra, state cb
-#pragma unroll
-    for (int r = 0; r < SEG / 8; ++r) {
-      const int u = r * 8 + ra, t = ts + u;
+    // gamma of the segment's steps: lane u = step ts + u with its whole state row (two float4s of each
+    // history), one pass and no cross-lane reduction (was 8 passes of lane = (step, state) with an 8-lane sum)
+    {
+      const int u = lane, t = ts + u;
       if (t < T) {
-        float gv = 0.f;
-        if (t < L) {
-          const float pr = cb < K ? ha[u * 8 + cb] * hb[u * 8 + cb] : 0.f;
-          const float su = allred<8, true>(pr, OpAdd{});
-          gv = pr * __builtin_amdgcn_rcpf(su);
+        const float4 a0 = *reinterpret_cast<const float4*>(ha + u * 8), a1 = *reinterpret_cast<const float4*>(ha + u * 8 + 4);
+        const float4 h0 = *reinterpret_cast<const float4*>(hb + u * 8), h1 = *reinterpret_cast<const float4*>(hb + u * 8 + 4);
+        float gv[8] = {a0.x * h0.x, a0.y * h0.y, a0.z * h0.z, a0.w * h0.w, a1.x * h1.x, a1.y * h1.y, a1.z * h1.z, a1.w * h1.w};
+        float su = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) su += j < Kv ? gv[j] : 0.f;
+        const float rs = __builtin_amdgcn_rcpf(su);
+        const bool live = t < L;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) gv[j] = live ? gv[j] * rs : 0.f;
+        float* gr = gq + (int64_t)t * K;
+        if (K == 8) {
+          *reinterpret_cast<float4*>(gr) = make_float4(gv[0], gv[1], gv[2], gv[3]);
+          *reinterpret_cast<float4*>(gr + 4) = make_float4(gv[4], gv[5], gv[6], gv[7]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (j < K) gr[j] = gv[j];
         }
-        if (cb < K) gq[(int64_t)t * K + cb] = gv;
       }
     }
     if (lane == 0) g_flag[w] = anybad;
