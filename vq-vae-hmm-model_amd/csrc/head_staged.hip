@@ -218,17 +218,25 @@ __device__ __forceinline__ float wave_max_dpp(float v) {
   return fmaxf(r.x, r.y);
 }
 
-__global__ __launch_bounds__(256) void head_l2_kernel(StagedHeadArgs a) {
-  __shared__ double red[4][256];
+// 16 waves per workgroup, RPW rows per wave per iteration (rows r0, r0 + nw, ...): the grid is capped at
+// head_grid(R) workgroups (one loss partial each), so the memory-level parallelism has to come from inside
+// the workgroup; cfg3 head_l2 (A/B on one box, rocprofv3 averages): one row per 4-wave workgroup
+// 0.62 ms; 4 rows x 4 waves 0.39-0.42 (173 VGPRs); with the row math on the scalar unit (81 VGPRs)
+// 256 x 4 / 1024 x 2 / 1024 x 4 / 512 x 4 / 1024 x 8 = 0.416 / 0.279 / 0.258 / 0.264 / 0.300 ms
+constexpr int L2_NT = 1024, RPW = 4;
+
+__global__ __launch_bounds__(L2_NT) void head_l2_kernel(StagedHeadArgs a) {
+  __shared__ double red[4][L2_NT];
   __shared__ unsigned long long cnt;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // wave index in an SGPR: the row index math and the per-row lengths / trw loads then run on the scalar unit
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int K = a.K, D = a.D, LQ = ld4(K), LP = ld4(2 * D), LX = ld4(D);
   if (tid == 0) cnt = a.norm ? (unsigned long long)a.norm[0] : 0ull;
   __syncthreads();
   {  // valid positions (the recon normaliser mask.sum() * C, VQ_VAE_HMM_fixed.py:120)
     unsigned long long c = 0;
 #pragma unroll 8  // independent load -> store iterations: keep 8 loads in flight
-    for (int64_t b = tid; !a.norm && b < a.B; b += 256) {
+    for (int64_t b = tid; !a.norm && b < a.B; b += L2_NT) {
       const int64_t L = a.lengths[b];
       c += (unsigned long long)(L <= 0 ? 0 : (L < a.T ? L : a.T));
     }
@@ -239,55 +247,98 @@ __global__ __launch_bounds__(256) void head_l2_kernel(StagedHeadArgs a) {
   const float cpri = -a.beta / loss_norm_batch(a.norm, a.B), cent = a.beta / loss_norm_batch(a.norm, a.B);
   const float lpk = lane < K ? a.log_pi[lane] : 0.f;
   float s_rec = 0.f, s_init = 0.f, s_tr = 0.f, s_ent = 0.f;
-  const int64_t nw = (int64_t)gridDim.x * 4;
-  for (int64_t r = (int64_t)blockIdx.x * 4 + wave; r < a.R; r += nw) {
-    int64_t b;
-    int t;
-    const bool valid = row_bt(r, a.R, a.T, b, t);
-    const int64_t L = valid ? a.lengths[b] : 0;
-    const bool m = valid && t < L;
+  // every load of a row group issued before any of its arithmetic and none gated on the lengths load: one row
+  // per wave left ~200 dependent load -> reduce -> store rounds per wave at cfg3 (0.62 ms, latency-bound);
+  // masked rows load but do not compute, as before
+  const int64_t nw = (int64_t)gridDim.x * (L2_NT / 64);
+  const bool small_r = a.R < (int64_t(1) << 32);
+  const uint32_t Tp32 = (uint32_t)a.T + 2u;
+  for (int64_t r0 = (int64_t)blockIdx.x * (L2_NT / 64) + wave; r0 < a.R; r0 += nw * RPW) {
+    int64_t rr[RPW], L[RPW];
+    int tt[RPW];
+    bool ok[RPW], valid[RPW];
+    float lg[RPW], qk[RPW], dqc[RPW], nxv[RPW], trw[RPW];
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+      const int64_t r = r0 + i * nw;
+      int64_t b = 0;
+      int t = 0;
+      rr[i] = r;
+      ok[i] = r < a.R;
+      if (small_r) {  // 32-bit division for R < 2^32 (row_bt's 64-bit one otherwise)
+        const uint32_t bq = (uint32_t)r / Tp32;
+        b = bq;
+        t = (int)((uint32_t)r - bq * Tp32) - 1;
+        valid[i] = r < a.R && t >= 0 && t < a.T;
+      } else {
+        valid[i] = row_bt(r, a.R, a.T, b, t);
+      }
+      tt[i] = t;
+      L[i] = valid[i] ? a.lengths[b] : 0;
+      const bool vk = valid[i] && lane < K;
+      lg[i] = ok[i] && lane < K ? a.logits[r * LQ + lane] : -__builtin_inff();
+      qk[i] = ok[i] && lane < K ? a.q[r * LQ + lane] : 0.f;
+      dqc[i] = vk ? a.dqc[r * LQ + lane] : 0.f;
+      nxv[i] = vk ? a.nx[(r + 1) * LQ + lane] : 0.f;
+      trw[i] = valid[i] ? a.trw[r] : 0.f;
+    }
     // recon NLL, lane c = channel (c, c + 64, ...)
     for (int c = lane; c < D; c += 64) {
-      float dmu = 0.f, dlv = 0.f;
-      if (m) {
-        const float mu = a.par[r * LP + c], lv = a.par[r * LP + D + c], xv = a.x[r * LX + c];
-        const float ev = __expf(lv);
-        const float var = (ev < 1e-8f ? 1e-8f : ev)  /* clamp(min=1e-8), NaN stays NaN */;
-        const float df = mu - xv;
-        const float r2 = df * df / var;
-        s_rec += 0.5f * (__logf(6.2831855f * var) + r2);
-        dmu = df / var * inv_n;
-        dlv = (ev >= 1e-8f) ? 0.5f * (1.f - r2) * inv_n : 0.f;
+      float mu[RPW], lv[RPW], xv[RPW];
+#pragma unroll
+      for (int i = 0; i < RPW; ++i) {
+        const int64_t r = rr[i];
+        mu[i] = valid[i] ? a.par[r * LP + c] : 0.f;
+        lv[i] = valid[i] ? a.par[r * LP + D + c] : 0.f;
+        xv[i] = valid[i] ? a.x[r * LX + c] : 0.f;
       }
-      if (a.need_grad) {
-        a.dpar[r * LP + c] = dmu;
-        a.dpar[r * LP + D + c] = dlv;
-      }
-    }
-    if (a.need_grad)
-      for (int c = 2 * D + lane; c < LP; c += 64) a.dpar[r * LP + c] = 0.f;  // pad channels
-    // entropy of q = softmax(logits) and its logits gradient, lane k = state
-    const float lg = lane < K ? a.logits[r * LQ + lane] : -__builtin_inff();
-    const float qk = lane < K ? a.q[r * LQ + lane] : 0.f;
-    const float mx = wave_max_dpp(lg);
-    const float lse = mx + __logf(wave_sum_dpp(lane < K ? __expf(lg - mx) : 0.f));
-    const float f = wave_sum_dpp(lane < K ? qk * (lg - lse) : 0.f);
-    if (m && lane == 0) s_ent -= f;
-    if (valid && lane == 0) s_tr += a.trw[r];
-    const float wn = (valid && t + 1 < L) ? 1.f : 0.f;  // weight of the t -> t+1 transition
-    if (lane < LQ) {
-      float dl = 0.f, dq = 0.f;
-      if (valid && lane < K) {
-        if (m) dl = cent * qk * ((lg - lse) - f);
-        dq = cpri * (a.dqc[r * LQ + lane] + wn * a.nx[(r + 1) * LQ + lane]);  // dqc already carries w_t
-        if (t == 0) {
-          dq = fmaf(cpri, lpk, dq);
-          s_init = fmaf(qk, lpk, s_init);
+#pragma unroll
+      for (int i = 0; i < RPW; ++i) {
+        float dmu = 0.f, dlv = 0.f;
+        if (valid[i] && tt[i] < L[i]) {
+          const float ev = __expf(lv[i]);
+          const float var = (ev < 1e-8f ? 1e-8f : ev)  /* clamp(min=1e-8), NaN stays NaN */;
+          const float df = mu[i] - xv[i];
+          const float r2 = df * df / var;
+          s_rec += 0.5f * (__logf(6.2831855f * var) + r2);
+          dmu = df / var * inv_n;
+          dlv = (ev >= 1e-8f) ? 0.5f * (1.f - r2) * inv_n : 0.f;
+        }
+        if (a.need_grad && ok[i]) {
+          a.dpar[rr[i] * LP + c] = dmu;
+          a.dpar[rr[i] * LP + D + c] = dlv;
         }
       }
-      if (a.need_grad) {
-        a.dlx[r * LQ + lane] = dl;
-        a.dqx[r * LQ + lane] = dq;
+    }
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+      if (!ok[i]) continue;
+      const int64_t r = rr[i];
+      const int t = tt[i];
+      const bool m = valid[i] && t < L[i];
+      if (a.need_grad)
+        for (int c = 2 * D + lane; c < LP; c += 64) a.dpar[r * LP + c] = 0.f;  // pad channels
+      // entropy of q = softmax(logits) and its logits gradient, lane k = state
+      const float mx = wave_max_dpp(lg[i]);
+      const float lse = mx + __logf(wave_sum_dpp(lane < K ? __expf(lg[i] - mx) : 0.f));
+      const float f = wave_sum_dpp(lane < K ? qk[i] * (lg[i] - lse) : 0.f);
+      if (m && lane == 0) s_ent -= f;
+      if (valid[i] && lane == 0) s_tr += trw[i];
+      const float wn = (valid[i] && t + 1 < L[i]) ? 1.f : 0.f;  // weight of the t -> t+1 transition
+      if (lane < LQ) {
+        float dl = 0.f, dq = 0.f;
+        if (valid[i] && lane < K) {
+          if (m) dl = cent * qk[i] * ((lg[i] - lse) - f);
+          dq = cpri * (dqc[i] + wn * nxv[i]);  // dqc already carries w_t
+          if (t == 0) {
+            dq = fmaf(cpri, lpk, dq);
+            s_init = fmaf(qk[i], lpk, s_init);
+          }
+        }
+        if (a.need_grad) {
+          a.dlx[r * LQ + lane] = dl;
+          a.dqx[r * LQ + lane] = dq;
+        }
       }
     }
   }
@@ -296,7 +347,7 @@ __global__ __launch_bounds__(256) void head_l2_kernel(StagedHeadArgs a) {
   red[2][tid] = s_tr;
   red[3][tid] = s_ent;
   __syncthreads();
-  for (int st = 128; st > 0; st >>= 1) {
+  for (int st = L2_NT / 2; st > 0; st >>= 1) {
     if (tid < st)
       for (int i = 0; i < 4; ++i) red[i][tid] += red[i][tid + st];
     __syncthreads();
@@ -346,7 +397,7 @@ int launch_staged_head(const StagedHeadArgs& a, int l2grid, hipStream_t s) {
   else if (a.K <= 32) head_l1_wide_kernel<false><<<g1, 256, 0, s>>>(a);
   else head_l1_kernel<64><<<g1, 256, 0, s>>>(a);
   VQHMM_LAUNCH_CHECK();
-  head_l2_kernel<<<l2grid, 256, 0, s>>>(a);
+  head_l2_kernel<<<l2grid, L2_NT, 0, s>>>(a);
   VQHMM_LAUNCH_CHECK();
   if (a.need_grad) {
     head_q0_kernel<<<1, 256, 0, s>>>(a.q, a.B, a.T, a.K, a.q0);
