@@ -97,26 +97,48 @@ __global__ __launch_bounds__(256) void head_l1_kernel(StagedHeadArgs a) {
   }
 }
 
-// One wave per row, lane = channel (D <= 64 recon channels, K <= 64 states): every load and store is a whole
-// contiguous row (the thread-per-row form read each row's channels 16 B apart per lane: 3.2 ms at cfg3); the
-// row's log-sum-exp and <q, log q> are wave reductions (DPP + permlane, a fixed order).
+// Sum over the 32 lanes of one parity (lane & 1) on the VALU: DPP xor 2 / row_ror:4 / row_ror:8 keep the
+// parity, then the permlane swaps; no LDS round trip (ds_bpermute was 5 per value, 16 values per row).
+__device__ __forceinline__ float parity_sum_dpp(float v) {
+  v += __builtin_bit_cast(float, dpp_u32<0x4E>(__builtin_bit_cast(uint32_t, v)));   // quad_perm [2,3,0,1]
+  v += __builtin_bit_cast(float, dpp_u32<0x124>(__builtin_bit_cast(uint32_t, v)));  // row_ror:4
+  v += __builtin_bit_cast(float, dpp_u32<0x128>(__builtin_bit_cast(uint32_t, v)));  // row_ror:8
+  float2 r = pair16(v);
+  v = r.x + r.y;
+  r = pair32(v);
+  return r.x + r.y;
+}
+__device__ __forceinline__ float xor1_dpp(float v) {
+  return __builtin_bit_cast(float, dpp_u32<0xB1>(__builtin_bit_cast(uint32_t, v)));  // quad_perm [1,0,3,2]
+}
+
 // head_l1 for 8 < K <= 32, one wave per row with every load and store a whole contiguous row: lane (i, h) =
 // (l >> 1, l & 1) holds log_A_t[i][16 h .. 16 h + 15] (the old lane-per-i form walked each i row with a
 // K-float stride per lane: 2.6 ms at cfg3).  Row reductions pair lanes (xor 1); the column sums dqc_j =
-// sum_i q_{t-1,i} log_A[i][j] run over the 32 lanes of a half (xor 2 .. 32, a fixed tree).  V4: K % 4 == 0
+// sum_i q_{t-1,i} log_A[i][j] run over the 32 lanes of a half (parity_sum_dpp).  V4: K % 4 == 0
 // (float4 rows).
 template <bool V4>
 __global__ __launch_bounds__(256) void head_l1_wide_kernel(StagedHeadArgs a) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // row math on SALU
   const int K = a.K, KK = K * K, LDA = ld4(KK), LQ = ld4(K);
   const int i = lane >> 1, h = lane & 1, j0 = 16 * h;
   const bool irow = i < K;
   const float cpri = -a.beta / loss_norm_batch(a.norm, a.B);
   const int64_t nw = (int64_t)gridDim.x * 4;
+  const bool small_r = a.R < (int64_t(1) << 32);
+  const uint32_t Tp32 = (uint32_t)a.T + 2u;
   for (int64_t r = (int64_t)blockIdx.x * 4 + wave; r < a.R; r += nw) {
     int64_t b;
     int t;
-    const bool valid = row_bt(r, a.R, a.T, b, t);
+    bool valid;
+    if (small_r) {  // 32-bit division for R < 2^32 (row_bt's 64-bit one otherwise)
+      const uint32_t bq = (uint32_t)r / Tp32;
+      b = bq;
+      t = (int)((uint32_t)r - bq * Tp32) - 1;
+      valid = t >= 0 && t < a.T;
+    } else {
+      valid = row_bt(r, a.R, a.T, b, t);
+    }
     float* row = a.lgA + r * LDA;
     if (!valid) {  // pad rows: zero gradient rows (the wgrad / dgrad sums run over all rows)
       for (int e = lane; e < LDA; e += 64) row[e] = 0.f;
@@ -150,12 +172,12 @@ __global__ __launch_bounds__(256) void head_l1_wide_kernel(StagedHeadArgs a) {
 #pragma unroll
     for (int jj = 0; jj < 16; ++jj)
       if (j0 + jj < K) m = fmaxf(m, la[jj]);
-    m = fmaxf(m, __shfl_xor(m, 1));
+    m = fmaxf(m, xor1_dpp(m));
     float se = 0.f;
 #pragma unroll
     for (int jj = 0; jj < 16; ++jj)
       if (j0 + jj < K) se += __expf(la[jj] - m);
-    se += __shfl_xor(se, 1);
+    se += xor1_dpp(se);
     const float ls = m + __logf(se);
     const float qp = irow ? a.q[(r - 1) * LQ + i] : 0.f;  // row r - 1 is a zero pad row at t = 0
     float nxi = 0.f, sq = 0.f;
@@ -167,12 +189,10 @@ __global__ __launch_bounds__(256) void head_l1_wide_kernel(StagedHeadArgs a) {
         sq += qc[jj];
       }
     }
-    nxi += __shfl_xor(nxi, 1);
-    sq += __shfl_xor(sq, 1);
+    nxi += xor1_dpp(nxi);
+    sq += xor1_dpp(sq);
     // transition term sum_i q_{t-1,i} nx_i (each i counted once: h = 0 lanes)
-    float tri = (irow && h == 0) ? qp * nxi : 0.f;
-#pragma unroll
-    for (int o = 2; o < 64; o <<= 1) tri += __shfl_xor(tri, o);
+    const float tri = parity_sum_dpp((irow && h == 0) ? qp * nxi : 0.f);
     if (h == 0 && i < LQ) a.nx[r * LQ + i] = irow ? nxi : 0.f;
     if (lane == 0) a.trw[r] = w * tri;  // lane 0 (h = 0) holds the sum over every i
     // dqc_j = w sum_i q_{t-1,i} log_A[i][j]: over the 32 lanes of this half
@@ -180,9 +200,7 @@ __global__ __launch_bounds__(256) void head_l1_wide_kernel(StagedHeadArgs a) {
 #pragma unroll
     for (int jj = 0; jj < 16; ++jj) d[jj] = irow ? qp * la[jj] : 0.f;
 #pragma unroll
-    for (int o = 2; o < 64; o <<= 1)
-#pragma unroll
-      for (int jj = 0; jj < 16; ++jj) d[jj] += __shfl_xor(d[jj], o);
+    for (int jj = 0; jj < 16; ++jj) d[jj] = parity_sum_dpp(d[jj]);
     if (i == 0) {
 #pragma unroll
       for (int jj = 0; jj < 16; ++jj)
@@ -218,6 +236,9 @@ __device__ __forceinline__ float wave_max_dpp(float v) {
   return fmaxf(r.x, r.y);
 }
 
+// head_l2: one wave per row, lane = channel (D <= 64 recon channels, K <= 64 states): every load and store is a whole
+// contiguous row (the thread-per-row form read each row's channels 16 B apart per lane: 3.2 ms at cfg3); the
+// row's log-sum-exp and <q, log q> are wave reductions (DPP + permlane, a fixed order).
 // 16 waves per workgroup, RPW rows per wave per iteration (rows r0, r0 + nw, ...): the grid is capped at
 // head_grid(R) workgroups (one loss partial each), so the memory-level parallelism has to come from inside
 // the workgroup; cfg3 head_l2 (A/B on one box, rocprofv3 averages): one row per 4-wave workgroup
