@@ -3,7 +3,7 @@
   head_coop.hip  elbo_head_pipe_kernel: K <= 4, U <= 4, TH = 128, D <= 16   (cfg1 / cfg2; the default there)
                  elbo_head_coop_kernel: K <= 8, U <= 4, TH in {64, 128, 256}, D <= 16 otherwise (cfg4)
   head_mfma.hip  K <= 4, U in 5..7, TH in {64, 128}
-  staged         everything else (cfg3: K = 32)
+  staged         everything else (cfg3: K = 32); head_l1 by K: pow2 (16, 32), wide (other K <= 32), lane per row
 
 Both head_coop kernels keep a wave's window-invariant phase-A operands in registers where their
 workgroup runs two or more windows (coop: more than 512 windows of 63 rows at K <= 4, 31 at K <= 8;
@@ -40,6 +40,11 @@ CASES = [
     ((5, 32, 4, 16, 5, 64), 24, 70),       # head_mfma, U = 5..7
     ((5, 32, 2, 16, 6, 128), 24, 70),
     ((5, 32, 3, 16, 7, 64), 24, 70),
+    ((8, 32, 16, 16, 4, 64), 24, 70),      # staged, head_l1_pow2 K = 16
+    ((8, 32, 32, 16, 3, 128), 40, 90),     # staged, head_l1_pow2 K = 32
+    ((8, 32, 12, 16, 4, 64), 24, 70),      # staged, head_l1_wide (float4 rows)
+    ((8, 32, 10, 16, 2, 64), 20, 45),      # staged, head_l1_wide (scalar rows)
+    ((8, 32, 40, 16, 4, 64), 12, 33),      # staged, head_l1 lane per row (K > 32)
 ]
 
 

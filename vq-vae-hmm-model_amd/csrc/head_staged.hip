@@ -225,6 +225,119 @@ __global__ __launch_bounds__(256) void head_l1_wide_kernel(StagedHeadArgs a) {
   }
 }
 
+// head_l1 for K = 16 / 32 with every wave-instruction on log_A a contiguous 1 KiB: lane l holds float4 number
+// 64 g + l of the row-major K x K block (g < K^2 / 256), i.e. row i = (64 g + l) / (K / 4), columns
+// 4 (l % (K / 4)) .. + 3.  A row's K / 4 lanes are adjacent (DPP quad / half-mirror sums); the column sums
+// dqc_j run over the lanes with the same l % (K / 4) (row_ror + permlane swaps).  head_l1_wide's lane (i, h)
+// form touched 64 separate 64-B segments per wave-instruction (0.94 ms at cfg3 for 3.57 GB, 3.8 TB/s).
+template <int LPR>
+__device__ __forceinline__ float row_sum_dpp(float v) {  // over the LPR (4 or 8) adjacent lanes of a row
+  v += xor1_dpp(v);
+  v += __builtin_bit_cast(float, dpp_u32<0x4E>(__builtin_bit_cast(uint32_t, v)));     // quad_perm [2,3,0,1]
+  if constexpr (LPR == 8)
+    v += __builtin_bit_cast(float, dpp_u32<0x141>(__builtin_bit_cast(uint32_t, v)));  // row_half_mirror
+  return v;
+}
+template <int LPR>
+__device__ __forceinline__ float row_max_dpp(float v) {
+  v = fmaxf(v, xor1_dpp(v));
+  v = fmaxf(v, __builtin_bit_cast(float, dpp_u32<0x4E>(__builtin_bit_cast(uint32_t, v))));
+  if constexpr (LPR == 8) v = fmaxf(v, __builtin_bit_cast(float, dpp_u32<0x141>(__builtin_bit_cast(uint32_t, v))));
+  return v;
+}
+template <int LPR>
+__device__ __forceinline__ float col_sum_dpp(float v) {  // over the 64 / LPR lanes with the same lane % LPR
+  if constexpr (LPR == 4)
+    v += __builtin_bit_cast(float, dpp_u32<0x124>(__builtin_bit_cast(uint32_t, v)));  // row_ror:4
+  v += __builtin_bit_cast(float, dpp_u32<0x128>(__builtin_bit_cast(uint32_t, v)));    // row_ror:8
+  float2 r = pair16(v);
+  v = r.x + r.y;
+  r = pair32(v);
+  return r.x + r.y;
+}
+
+template <int KP>
+__global__ __launch_bounds__(256) void head_l1_pow2_kernel(StagedHeadArgs a) {
+  constexpr int LPR = KP / 4, G = KP * KP / 256, KK = KP * KP;  // LDA = KK, LQ = KP
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // row math on SALU
+  const int c0 = 4 * (lane % LPR);
+  const bool lead = lane % LPR == 0;
+  const float cpri = -a.beta / loss_norm_batch(a.norm, a.B);
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  const bool small_r = a.R < (int64_t(1) << 32);
+  const uint32_t Tp32 = (uint32_t)a.T + 2u;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + wave; r < a.R; r += nw) {
+    int64_t b;
+    int t;
+    bool valid;
+    if (small_r) {  // 32-bit division for R < 2^32 (row_bt's 64-bit one otherwise)
+      const uint32_t bq = (uint32_t)r / Tp32;
+      b = bq;
+      t = (int)((uint32_t)r - bq * Tp32) - 1;
+      valid = t >= 0 && t < a.T;
+    } else {
+      valid = row_bt(r, a.R, a.T, b, t);
+    }
+    float* row = a.lgA + r * KK;
+    if (!valid) {  // pad rows: zero gradient rows (the wgrad / dgrad sums run over all rows)
+#pragma unroll
+      for (int g = 0; g < G; ++g) *reinterpret_cast<float4*>(row + 256 * g + 4 * lane) = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (lane < LPR) {
+        *reinterpret_cast<float4*>(a.nx + r * KP + 4 * lane) = make_float4(0.f, 0.f, 0.f, 0.f);
+        *reinterpret_cast<float4*>(a.dqc + r * KP + 4 * lane) = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      if (lane == 0) a.trw[r] = 0.f;
+      continue;
+    }
+    float4 v[G];
+    float qp[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) v[g] = *reinterpret_cast<const float4*>(row + 256 * g + 4 * lane);
+    const float4 c = *reinterpret_cast<const float4*>(a.q + r * KP + c0);
+#pragma unroll
+    for (int g = 0; g < G; ++g) qp[g] = a.q[(r - 1) * KP + (64 * g + lane) / LPR];  // row r - 1: zero pad at t = 0
+    const int64_t L = a.lengths[b];
+    const float w = (t >= 1 && t < L) ? 1.f : 0.f;
+    const float qc[4] = {c.x, c.y, c.z, c.w};
+    const float sq = row_sum_dpp<LPR>((qc[0] + qc[1]) + (qc[2] + qc[3]));  // sum_j q_{t,j}
+    float tri = 0.f, d[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      float la[4] = {v[g].x, v[g].y, v[g].z, v[g].w};
+      const float m = row_max_dpp<LPR>(fmaxf(fmaxf(la[0], la[1]), fmaxf(la[2], la[3])));
+      float se = 0.f;
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc) se += __expf(la[cc] - m);
+      const float ls = m + __logf(row_sum_dpp<LPR>(se));
+      float nxi = 0.f;
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc) {
+        la[cc] -= ls;
+        nxi = fmaf(la[cc], qc[cc], nxi);
+        d[cc] = fmaf(qp[g], la[cc], d[cc]);
+      }
+      nxi = row_sum_dpp<LPR>(nxi);
+      const int i = (64 * g + lane) / LPR;
+      if (lead) {
+        a.nx[r * KP + i] = nxi;
+        tri = fmaf(qp[g], nxi, tri);  // transition term sum_i q_{t-1,i} nx_i, each i once
+      }
+      // log_softmax backward of d tr / d log_A = cpri w q_{t-1,i} q_{t,j}, in place over the row
+      const float ci = cpri * w * qp[g], rs = ci * sq;
+      *reinterpret_cast<float4*>(row + 256 * g + 4 * lane) =
+          make_float4(ci * qc[0] - __expf(la[0]) * rs, ci * qc[1] - __expf(la[1]) * rs,
+                      ci * qc[2] - __expf(la[2]) * rs, ci * qc[3] - __expf(la[3]) * rs);
+    }
+    tri = wave_sum_dpp(tri);
+    if (lane == 0) a.trw[r] = w * tri;
+    // dqc_j = w sum_i q_{t-1,i} log_A[i][j]
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc) d[cc] = col_sum_dpp<LPR>(d[cc]);
+    if (lane < LPR)
+      *reinterpret_cast<float4*>(a.dqc + r * KP + c0) = make_float4(w * d[0], w * d[1], w * d[2], w * d[3]);
+  }
+}
+
 __device__ __forceinline__ float wave_max_dpp(float v) {
   v = fmaxf(v, __builtin_bit_cast(float, dpp_u32<0xB1>(__builtin_bit_cast(uint32_t, v))));
   v = fmaxf(v, __builtin_bit_cast(float, dpp_u32<0x4E>(__builtin_bit_cast(uint32_t, v))));
@@ -414,6 +527,8 @@ int launch_staged_head(const StagedHeadArgs& a, int l2grid, hipStream_t s) {
   VQHMM_LAUNCH_CHECK();
   const unsigned g1 = (unsigned)std::min<int64_t>(cdiv(a.R, 4), 2048);
   if (a.K <= 8) head_l1_kernel<16><<<g1, 256, 0, s>>>(a);
+  else if (a.K == 32) head_l1_pow2_kernel<32><<<g1, 256, 0, s>>>(a);
+  else if (a.K == 16) head_l1_pow2_kernel<16><<<g1, 256, 0, s>>>(a);
   else if (a.K <= 32 && a.K % 4 == 0) head_l1_wide_kernel<true><<<g1, 256, 0, s>>>(a);
   else if (a.K <= 32) head_l1_wide_kernel<false><<<g1, 256, 0, s>>>(a);
   else head_l1_kernel<64><<<g1, 256, 0, s>>>(a);
