@@ -62,6 +62,18 @@ __device__ __forceinline__ bool row_bt(int64_t r, int64_t R, int T, int64_t& b, 
   t = (int)(r - b * Tp) - 1;
   return t >= 0 && t < T;
 }
+// row_bt with a 32-bit division when R < 2^32 (a launch-uniform branch): the 64-bit division is several times
+// the instructions, which shows in per-row epilogues of short-reduction kernels (convbig at Kc = 128, k = 1).
+__device__ __forceinline__ bool row_bt_fast(int64_t r, int64_t R, int T, int64_t& b, int& t) {
+  if (R < (int64_t(1) << 32)) {
+    if (r < 0 || r >= R) return false;
+    const uint32_t Tp = (uint32_t)T + 2u, bq = (uint32_t)r / Tp;
+    b = bq;
+    t = (int)((uint32_t)r - bq * Tp) - 1;
+    return t >= 0 && t < T;
+  }
+  return row_bt(r, R, T, b, t);
+}
 
 // Lane exchange x[lane ^ 16] / x[lane ^ 32] on the VALU (gfx950 v_permlane16/32_swap:
 // vdst's odd 16-lane rows (upper half) trade places with src's even rows (lower

@@ -63,6 +63,67 @@ __device__ __forceinline__ const float* cb_wsrc(const ConvArgs& a, int n0, int c
   return a.W + ((int64_t)(c0 + c) * a.N + n0) * ks + 4 * f;
 }
 
+// Epilogue shared by the k = 3 / k = 1 kernels: lane (lg, l16), register v -> row wm*64 + i*16 + 4 lg + v,
+// column wn*BN/2 + j*16 + l16; Xs is reused as the SOFTMAX staging buffer.
+template <int BN, bool SOFTMAX>
+__device__ __forceinline__ void cb_epilogue(const ConvArgs& a, f32x4 (&acc)[4][BN / 32], float* Xs, int64_t m0, int n0) {
+  constexpr int WN = BN / 32;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lg = lane >> 4, l16 = lane & 15;
+  const int wm = wave & 1, wn = wave >> 1;
+  const float sc = a.scale ? *a.scale : 1.f;
+  const int ldn = a.N;  // N % 4 == 0: no pad channels
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int row = wm * 64 + i * 16 + 4 * lg + v;
+      const int64_t r = m0 + row;
+      int64_t b;
+      int t;
+      const bool valid = row_bt_fast(r, a.R, a.T, b, t);
+#pragma unroll
+      for (int j = 0; j < WN; ++j) {
+        const int n = n0 + wn * (BN / 2) + j * 16 + l16;
+        float y = acc[i][j][v] * sc;
+        if (a.bias && n < a.N) y += a.bias[n];
+        if (a.act == 1) y = relu_f(y);
+        else if (a.act == 2 && r < a.R && n < a.N) y = a.aux[r * ldn + n] > 0.f ? y : 0.f;
+        y = valid ? y : 0.f;
+        acc[i][j][v] = y;
+        if (a.out && r < a.R && n < a.N) a.out[r * ldn + n] = y;
+      }
+    }
+  }
+  if constexpr (SOFTMAX) {  // q = softmax over the row's N <= BN / 2 channels (all in the wn = 0 waves)
+    __syncthreads();
+    float* Ys = Xs;  // [BM][BN / 2 + 1]
+    constexpr int LY = BN / 2 + 1;
+    if (wn == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+#pragma unroll
+          for (int j = 0; j < WN; ++j) Ys[(wm * 64 + i * 16 + 4 * lg + v) * LY + j * 16 + l16] = acc[i][j][v];
+    }
+    __syncthreads();
+    if (tid < CB_BM) {
+      const int64_t r = m0 + tid;
+      int64_t b;
+      int t;
+      const bool valid = row_bt_fast(r, a.R, a.T, b, t);
+      const float* y = Ys + tid * LY;
+      float mx = -__builtin_inff();
+      for (int n = 0; n < a.N; ++n) mx = fmaxf(mx, y[n]);
+      float se = 0.f;
+      for (int n = 0; n < a.N; ++n) se += __expf(y[n] - mx);
+      if (r < a.R)
+        for (int n = 0; n < a.N; ++n) a.q_out[r * ldn + n] = valid ? __expf(y[n] - mx) / se : 0.f;
+    }
+  }
+}
+
 template <int BN, bool SOFTMAX>
 __global__ __launch_bounds__(256) void convbig_kernel(ConvArgs a) {
   using C = ConvBigCfg<BN>;
@@ -152,58 +213,115 @@ __global__ __launch_bounds__(256) void convbig_kernel(ConvArgs a) {
     }
   }
 
-  // ---- epilogue: lane (lg, l16), register v -> row wm*64 + i*16 + 4 lg + v, column wn*BN/2 + j*16 + l16
-  const float sc = a.scale ? *a.scale : 1.f;
-  const int ldn = a.N;  // N % 4 == 0: no pad channels
+  cb_epilogue<BN, SOFTMAX>(a, acc, Xs, m0, n0);
+}
+
+// k = 1 with Kc % 32 == 0: two 16-channel slices per LDS stage, no halo rows.  One slice per stage left a k = 1
+// workgroup 64 MFMAs per wave between a slice's loads and their use, under the load latency: the Prior MLP's
+// 1x1 layers (K^2 = 1024 logits and their data gradient) and the 1x1 data gradients ran at 0.21-0.37 of the
+// MFMA peak at cfg3.  Same slices in the same order as convbig_kernel: the same fmaf chain, bit for bit.
+template <int BN>
+struct ConvBig1Cfg {
+  static constexpr int SPS = 2;                         // slices per stage
+  static constexpr int X4 = CB_BM * 4, W4 = BN * 4;     // float4s of one slice's X rows / weight rows
+  static constexpr int PX = X4 / 256, PW = (W4 + 255) / 256;
+  static constexpr int XS = CB_BM * CB_LD, WS = BN * CB_LD;
+  static constexpr int LDS_FLOATS = SPS * (XS + WS);
+};
+
+template <int BN, bool SOFTMAX>
+__global__ __launch_bounds__(256) void convbig1_kernel(ConvArgs a) {
+  using C = ConvBig1Cfg<BN>;
+  constexpr int WN = BN / 32, SPS = C::SPS;
+  extern __shared__ float4 smem4[];
+  float* Xs = reinterpret_cast<float*>(smem4);  // [SPS][BM][LD]
+  float* Ws = Xs + SPS * C::XS;                 // [SPS][BN][LD]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lg = lane >> 4, l16 = lane & 15;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int64_t m0 = (int64_t)blockIdx.x * CB_BM;
+  const int n0 = blockIdx.y * BN;
+  const int ldx = a.Kc, nstage = a.Kc / (CB_KC * SPS);
+
+  float4 px[SPS][C::PX], pw[SPS][C::PW];
+  auto load = [&](int c0) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+    for (int h = 0; h < SPS; ++h) {
 #pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int row = wm * 64 + i * 16 + 4 * lg + v;
-      const int64_t r = m0 + row;
-      int64_t b;
-      int t;
-      const bool valid = row_bt(r, a.R, a.T, b, t);
+      for (int k = 0; k < C::PX; ++k) {
+        const int i = tid + 256 * k, row = i >> 2, c4 = (i & 3) * 4;
+        const int64_t r = m0 + row;
+        px[h][k] = r < a.R ? *reinterpret_cast<const float4*>(a.src + r * ldx + c0 + CB_KC * h + c4)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
 #pragma unroll
-      for (int j = 0; j < WN; ++j) {
-        const int n = n0 + wn * (BN / 2) + j * 16 + l16;
-        float y = acc[i][j][v] * sc;
-        if (a.bias && n < a.N) y += a.bias[n];
-        if (a.act == 1) y = relu_f(y);
-        else if (a.act == 2 && r < a.R && n < a.N) y = a.aux[r * ldn + n] > 0.f ? y : 0.f;
-        y = valid ? y : 0.f;
-        acc[i][j][v] = y;
-        if (a.out && r < a.R && n < a.N) a.out[r * ldn + n] = y;
+      for (int k = 0; k < C::PW; ++k) {
+        const int q = tid + 256 * k;
+        int dst[4];
+        const float* src = q < C::W4 ? cb_wsrc<BN>(a, n0, c0 + CB_KC * h, q, dst) : nullptr;
+        pw[h][k] = src ? *reinterpret_cast<const float4*>(src) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
     }
-  }
-  if constexpr (SOFTMAX) {  // q = softmax over the row's N <= BN / 2 channels (all in the wn = 0 waves)
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int h = 0; h < SPS; ++h) {
+#pragma unroll
+      for (int k = 0; k < C::PX; ++k) {
+        const int i = tid + 256 * k;
+        *reinterpret_cast<float4*>(Xs + h * C::XS + (i >> 2) * CB_LD + (i & 3) * 4) = px[h][k];
+      }
+#pragma unroll
+      for (int k = 0; k < C::PW; ++k) {
+        int q = tid + 256 * k;
+        if (q < C::W4) {
+          asm volatile("" : "+v"(q));  // as in convbig_kernel: recompute the destinations, do not hoist them
+          int dst[4];
+          (void)cb_wsrc<BN>(a, n0, 0, q, dst);
+          float* w = Ws + h * C::WS;
+          w[dst[0]] = pw[h][k].x;
+          w[dst[1]] = pw[h][k].y;
+          w[dst[2]] = pw[h][k].z;
+          w[dst[3]] = pw[h][k].w;
+        }
+      }
+    }
+  };
+
+  f32x4 acc[4][WN];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  load(0);
+  for (int s = 0; s < nstage; ++s) {
+    __syncthreads();  // every wave is done reading the previous stage
+    store();
     __syncthreads();
-    float* Ys = Xs;  // [BM][BN / 2 + 1]
-    constexpr int LY = BN / 2 + 1;
-    if (wn == 0) {
+    if (s + 1 < nstage) load((s + 1) * CB_KC * SPS);  // in flight across this stage's MFMAs
+#pragma unroll
+    for (int h = 0; h < SPS; ++h) {
+      float4 av[4], bv[WN];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
+        av[i] = *reinterpret_cast<const float4*>(Xs + h * C::XS + (wm * 64 + i * 16 + l16) * CB_LD + 4 * lg);
 #pragma unroll
-        for (int v = 0; v < 4; ++v)
+      for (int j = 0; j < WN; ++j)
+        bv[j] = *reinterpret_cast<const float4*>(Ws + h * C::WS + (wn * (BN / 2) + j * 16 + l16) * CB_LD + 4 * lg);
 #pragma unroll
-          for (int j = 0; j < WN; ++j) Ys[(wm * 64 + i * 16 + 4 * lg + v) * LY + j * 16 + l16] = acc[i][j][v];
-    }
-    __syncthreads();
-    if (tid < CB_BM) {
-      const int64_t r = m0 + tid;
-      int64_t b;
-      int t;
-      const bool valid = row_bt(r, a.R, a.T, b, t);
-      const float* y = Ys + tid * LY;
-      float mx = -__builtin_inff();
-      for (int n = 0; n < a.N; ++n) mx = fmaxf(mx, y[n]);
-      float se = 0.f;
-      for (int n = 0; n < a.N; ++n) se += __expf(y[n] - mx);
-      if (r < a.R)
-        for (int n = 0; n < a.N; ++n) a.q_out[r * ldn + n] = valid ? __expf(y[n] - mx) / se : 0.f;
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < WN; ++j) {
+            const float ae = e == 0 ? av[i].x : e == 1 ? av[i].y : e == 2 ? av[i].z : av[i].w;
+            const float be = e == 0 ? bv[j].x : e == 1 ? bv[j].y : e == 2 ? bv[j].z : bv[j].w;
+            acc[i][j] = mfma16x16x4(ae, be, acc[i][j]);
+          }
     }
   }
+  cb_epilogue<BN, SOFTMAX>(a, acc, Xs, m0, n0);
 }
 
 // shapes the wide kernel takes: PCL in and out, Kc a multiple of 16 (whole slices), N a multiple of 4 (no pad
@@ -216,8 +334,14 @@ bool convbig_supported(const ConvArgs& a) {
 
 template <int BN, bool SM>
 static int launch_cb(const ConvArgs& a, hipStream_t s) {
-  const size_t lds = (size_t)ConvBigCfg<BN>::LDS_FLOATS * sizeof(float);
   const dim3 grid((unsigned)cdiv(a.R, CB_BM), (unsigned)cdiv(a.N, BN));
+  if (a.ks == 1 && a.Kc % (CB_KC * ConvBig1Cfg<BN>::SPS) == 0) {
+    const size_t lds1 = (size_t)ConvBig1Cfg<BN>::LDS_FLOATS * sizeof(float);
+    convbig1_kernel<BN, SM><<<grid, 256, lds1, s>>>(a);
+    VQHMM_LAUNCH_CHECK();
+    return VQHMM_OK;
+  }
+  const size_t lds = (size_t)ConvBigCfg<BN>::LDS_FLOATS * sizeof(float);
   convbig_kernel<BN, SM><<<grid, 256, lds, s>>>(a);
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;

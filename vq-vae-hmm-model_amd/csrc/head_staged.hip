@@ -125,20 +125,10 @@ __global__ __launch_bounds__(256) void head_l1_wide_kernel(StagedHeadArgs a) {
   const bool irow = i < K;
   const float cpri = -a.beta / loss_norm_batch(a.norm, a.B);
   const int64_t nw = (int64_t)gridDim.x * 4;
-  const bool small_r = a.R < (int64_t(1) << 32);
-  const uint32_t Tp32 = (uint32_t)a.T + 2u;
   for (int64_t r = (int64_t)blockIdx.x * 4 + wave; r < a.R; r += nw) {
     int64_t b;
     int t;
-    bool valid;
-    if (small_r) {  // 32-bit division for R < 2^32 (row_bt's 64-bit one otherwise)
-      const uint32_t bq = (uint32_t)r / Tp32;
-      b = bq;
-      t = (int)((uint32_t)r - bq * Tp32) - 1;
-      valid = t >= 0 && t < a.T;
-    } else {
-      valid = row_bt(r, a.R, a.T, b, t);
-    }
+    const bool valid = row_bt_fast(r, a.R, a.T, b, t);
     float* row = a.lgA + r * LDA;
     if (!valid) {  // pad rows: zero gradient rows (the wgrad / dgrad sums run over all rows)
       for (int e = lane; e < LDA; e += 64) row[e] = 0.f;
@@ -264,20 +254,10 @@ __global__ __launch_bounds__(256) void head_l1_pow2_kernel(StagedHeadArgs a) {
   const bool lead = lane % LPR == 0;
   const float cpri = -a.beta / loss_norm_batch(a.norm, a.B);
   const int64_t nw = (int64_t)gridDim.x * 4;
-  const bool small_r = a.R < (int64_t(1) << 32);
-  const uint32_t Tp32 = (uint32_t)a.T + 2u;
   for (int64_t r = (int64_t)blockIdx.x * 4 + wave; r < a.R; r += nw) {
     int64_t b;
     int t;
-    bool valid;
-    if (small_r) {  // 32-bit division for R < 2^32 (row_bt's 64-bit one otherwise)
-      const uint32_t bq = (uint32_t)r / Tp32;
-      b = bq;
-      t = (int)((uint32_t)r - bq * Tp32) - 1;
-      valid = t >= 0 && t < a.T;
-    } else {
-      valid = row_bt(r, a.R, a.T, b, t);
-    }
+    const bool valid = row_bt_fast(r, a.R, a.T, b, t);
     float* row = a.lgA + r * KK;
     if (!valid) {  // pad rows: zero gradient rows (the wgrad / dgrad sums run over all rows)
 #pragma unroll
@@ -385,8 +365,6 @@ __global__ __launch_bounds__(L2_NT) void head_l2_kernel(StagedHeadArgs a) {
   // per wave left ~200 dependent load -> reduce -> store rounds per wave at cfg3 (0.62 ms, latency-bound);
   // masked rows load but do not compute, as before
   const int64_t nw = (int64_t)gridDim.x * (L2_NT / 64);
-  const bool small_r = a.R < (int64_t(1) << 32);
-  const uint32_t Tp32 = (uint32_t)a.T + 2u;
   for (int64_t r0 = (int64_t)blockIdx.x * (L2_NT / 64) + wave; r0 < a.R; r0 += nw * RPW) {
     int64_t rr[RPW], L[RPW];
     int tt[RPW];
@@ -399,14 +377,7 @@ __global__ __launch_bounds__(L2_NT) void head_l2_kernel(StagedHeadArgs a) {
       int t = 0;
       rr[i] = r;
       ok[i] = r < a.R;
-      if (small_r) {  // 32-bit division for R < 2^32 (row_bt's 64-bit one otherwise)
-        const uint32_t bq = (uint32_t)r / Tp32;
-        b = bq;
-        t = (int)((uint32_t)r - bq * Tp32) - 1;
-        valid[i] = r < a.R && t >= 0 && t < a.T;
-      } else {
-        valid[i] = row_bt(r, a.R, a.T, b, t);
-      }
+      valid[i] = row_bt_fast(r, a.R, a.T, b, t);
       tt[i] = t;
       L[i] = valid[i] ? a.lengths[b] : 0;
       const bool vk = valid[i] && lane < K;
