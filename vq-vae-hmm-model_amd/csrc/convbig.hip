@@ -38,7 +38,7 @@ struct ConvBigCfg {
 // One float4 of the slice's weights: source address (or null: zeros) and the 4 LDS destinations (tap, n, c) it
 // scatters to.  Forward: per n the slice's (c, tap) pairs are 48 (k = 3) / 16 (k = 1) contiguous floats of W[n];
 // data gradient: per c the tile's (n, tap) pairs are 3 BN / BN contiguous floats of W[c].
-template <int BN>
+template <int BN, int LD = CB_LD>
 __device__ __forceinline__ const float* cb_wsrc(const ConvArgs& a, int n0, int c0, int q, int (&dst)[4]) {
   const int ks = a.ks;
   if (!a.w_dgrad) {
@@ -47,7 +47,7 @@ __device__ __forceinline__ const float* cb_wsrc(const ConvArgs& a, int n0, int c
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int idx = 4 * f + e, c = ks == 3 ? idx / 3 : idx, tap = ks == 3 ? idx - 3 * (idx / 3) : 0;
-      dst[e] = (tap * BN + n) * CB_LD + c;
+      dst[e] = (tap * BN + n) * LD + c;
     }
     if (n >= BN || n0 + n >= a.N) return nullptr;
     return a.W + ((int64_t)(n0 + n) * a.Kc + c0) * ks + 4 * f;
@@ -57,7 +57,7 @@ __device__ __forceinline__ const float* cb_wsrc(const ConvArgs& a, int n0, int c
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int idx = 4 * f + e, n = ks == 3 ? idx / 3 : idx, t = ks == 3 ? idx - 3 * (idx / 3) : 0;
-    dst[e] = ((ks - 1 - t) * BN + n) * CB_LD + c;
+    dst[e] = ((ks - 1 - t) * BN + n) * LD + c;
   }
   if (c >= CB_KC || n0 + (ks == 3 ? (4 * f) / 3 : 4 * f) >= a.N) return nullptr;  // N % 4 == 0: whole float4s
   return a.W + ((int64_t)(c0 + c) * a.N + n0) * ks + 4 * f;
@@ -225,7 +225,10 @@ struct ConvBig1Cfg {
   static constexpr int SPS = 2;                         // slices per stage
   static constexpr int X4 = CB_BM * 4, W4 = BN * 4;     // float4s of one slice's X rows / weight rows
   static constexpr int PX = X4 / 256, PW = (W4 + 255) / 256;
-  static constexpr int XS = CB_BM * CB_LD, WS = BN * CB_LD;
+  // LDS row stride 20 floats: the 16 rows a 16-lane group reads as float4s start at 16 distinct multiples of 4
+  // banks (20 r mod 64), all 64 banks once; 40 KB per workgroup at BN = 128, four workgroups per CU
+  static constexpr int LD = 20;
+  static constexpr int XS = CB_BM * LD, WS = BN * LD;
   static constexpr int LDS_FLOATS = SPS * (XS + WS);
 };
 
@@ -258,7 +261,7 @@ __global__ __launch_bounds__(256) void convbig1_kernel(ConvArgs a) {
       for (int k = 0; k < C::PW; ++k) {
         const int q = tid + 256 * k;
         int dst[4];
-        const float* src = q < C::W4 ? cb_wsrc<BN>(a, n0, c0 + CB_KC * h, q, dst) : nullptr;
+        const float* src = q < C::W4 ? cb_wsrc<BN, C::LD>(a, n0, c0 + CB_KC * h, q, dst) : nullptr;
         pw[h][k] = src ? *reinterpret_cast<const float4*>(src) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
     }
@@ -269,7 +272,7 @@ __global__ __launch_bounds__(256) void convbig1_kernel(ConvArgs a) {
 #pragma unroll
       for (int k = 0; k < C::PX; ++k) {
         const int i = tid + 256 * k;
-        *reinterpret_cast<float4*>(Xs + h * C::XS + (i >> 2) * CB_LD + (i & 3) * 4) = px[h][k];
+        *reinterpret_cast<float4*>(Xs + h * C::XS + (i >> 2) * C::LD + (i & 3) * 4) = px[h][k];
       }
 #pragma unroll
       for (int k = 0; k < C::PW; ++k) {
@@ -277,7 +280,7 @@ __global__ __launch_bounds__(256) void convbig1_kernel(ConvArgs a) {
         if (q < C::W4) {
           asm volatile("" : "+v"(q));  // as in convbig_kernel: recompute the destinations, do not hoist them
           int dst[4];
-          (void)cb_wsrc<BN>(a, n0, 0, q, dst);
+          (void)cb_wsrc<BN, C::LD>(a, n0, 0, q, dst);
           float* w = Ws + h * C::WS;
           w[dst[0]] = pw[h][k].x;
           w[dst[1]] = pw[h][k].y;
@@ -305,10 +308,10 @@ __global__ __launch_bounds__(256) void convbig1_kernel(ConvArgs a) {
       float4 av[4], bv[WN];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        av[i] = *reinterpret_cast<const float4*>(Xs + h * C::XS + (wm * 64 + i * 16 + l16) * CB_LD + 4 * lg);
+        av[i] = *reinterpret_cast<const float4*>(Xs + h * C::XS + (wm * 64 + i * 16 + l16) * C::LD + 4 * lg);
 #pragma unroll
       for (int j = 0; j < WN; ++j)
-        bv[j] = *reinterpret_cast<const float4*>(Ws + h * C::WS + (wn * (BN / 2) + j * 16 + l16) * CB_LD + 4 * lg);
+        bv[j] = *reinterpret_cast<const float4*>(Ws + h * C::WS + (wn * (BN / 2) + j * 16 + l16) * C::LD + 4 * lg);
 #pragma unroll
       for (int e = 0; e < 4; ++e)
 #pragma unroll
