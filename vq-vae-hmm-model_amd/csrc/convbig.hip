@@ -73,8 +73,29 @@ __device__ __forceinline__ void cb_epilogue(const ConvArgs& a, f32x4 (&acc)[4][B
   const int wm = wave & 1, wn = wave >> 1;
   const float sc = a.scale ? *a.scale : 1.f;
   const int ldn = a.N;  // N % 4 == 0: no pad channels
+  // bias and each 16-row block's ReLU-mask operands are loaded before any of its stores: loads after a store to
+  // `out` (which may alias them as far as the compiler knows) were each issued and waited for alone
+  // (vmcnt(0) 130 times per epilogue)
+  float bj[WN];
+#pragma unroll
+  for (int j = 0; j < WN; ++j) {
+    const int n = n0 + wn * (BN / 2) + j * 16 + l16;
+    bj[j] = a.bias && n < a.N ? a.bias[n] : 0.f;
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
+    float ax[4][WN];
+    if (a.act == 2) {
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int64_t r = m0 + wm * 64 + i * 16 + 4 * lg + v;
+#pragma unroll
+        for (int j = 0; j < WN; ++j) {
+          const int n = n0 + wn * (BN / 2) + j * 16 + l16;
+          ax[v][j] = r < a.R && n < a.N ? a.aux[r * ldn + n] : 0.f;
+        }
+      }
+    }
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       const int row = wm * 64 + i * 16 + 4 * lg + v;
@@ -86,9 +107,9 @@ __device__ __forceinline__ void cb_epilogue(const ConvArgs& a, f32x4 (&acc)[4][B
       for (int j = 0; j < WN; ++j) {
         const int n = n0 + wn * (BN / 2) + j * 16 + l16;
         float y = acc[i][j][v] * sc;
-        if (a.bias && n < a.N) y += a.bias[n];
+        if (a.bias && n < a.N) y += bj[j];
         if (a.act == 1) y = relu_f(y);
-        else if (a.act == 2 && r < a.R && n < a.N) y = a.aux[r * ldn + n] > 0.f ? y : 0.f;
+        else if (a.act == 2 && r < a.R && n < a.N) y = ax[v][j] > 0.f ? y : 0.f;
         y = valid ? y : 0.f;
         acc[i][j][v] = y;
         if (a.out && r < a.R && n < a.N) a.out[r * ldn + n] = y;
