@@ -137,21 +137,38 @@ __global__ __launch_bounds__(256) void conv_mm_kernel(ConvArgs a) {
       }
   __syncthreads();
   const float sc = a.scale ? *a.scale : 1.0f;
-  for (int i = tid; i < BM * BN; i += 256) {
-    const int row = i / BN, col = i - row * BN;
-    const int64_t r = m0 + row;
-    const int n = n0 + col;
-    float y = 0.f;
-    int64_t b;
-    int t;
-    if (n < a.N && row_bt(r, a.R, a.T, b, t)) {
-      y = Ys[row * LDY + col] * sc;
-      if (a.bias) y += a.bias[n];
-      if (a.act == 1) y = relu_f(y);
-      else if (a.act == 2) y = a.aux[r * ld4(a.N) + n] > 0.f ? y : 0.f;
+  // four elements per thread and pass, their bias / mask loads issued before any of their stores (a load after
+  // a store to `out`, which may alias it as far as the compiler knows, was issued and waited for alone)
+  constexpr int EP = 4;
+  for (int i0 = tid; i0 < BM * BN; i0 += 256 * EP) {
+    float bv[EP], mv[EP];
+#pragma unroll
+    for (int u = 0; u < EP; ++u) {
+      const int i = i0 + 256 * u, row = i / BN, n = n0 + (i - row * BN);
+      const int64_t r = m0 + row;
+      const bool in = i < BM * BN && n < a.N && r < a.R;
+      bv[u] = in && a.bias ? a.bias[n] : 0.f;
+      mv[u] = in && a.act == 2 ? a.aux[r * ld4(a.N) + n] : 0.f;
     }
-    Ys[row * LDY + col] = y;
-    if (a.out && n < ld4(a.N) && r < a.R) a.out[r * ld4(a.N) + n] = y;
+#pragma unroll
+    for (int u = 0; u < EP; ++u) {
+      const int i = i0 + 256 * u;
+      if (i >= BM * BN) break;
+      const int row = i / BN, col = i - row * BN;
+      const int64_t r = m0 + row;
+      const int n = n0 + col;
+      float y = 0.f;
+      int64_t b;
+      int t;
+      if (n < a.N && row_bt_fast(r, a.R, a.T, b, t)) {
+        y = Ys[row * LDY + col] * sc;
+        if (a.bias) y += bv[u];
+        if (a.act == 1) y = relu_f(y);
+        else if (a.act == 2) y = mv[u] > 0.f ? y : 0.f;
+      }
+      Ys[row * LDY + col] = y;
+      if (a.out && n < ld4(a.N) && r < a.R) a.out[r * ld4(a.N) + n] = y;
+    }
   }
   if (a.out_cf || a.tW) __syncthreads();
   if (a.out_cf) {
