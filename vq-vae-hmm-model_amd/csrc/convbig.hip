@@ -63,6 +63,16 @@ __device__ __forceinline__ const float* cb_wsrc(const ConvArgs& a, int n0, int c
   return a.W + ((int64_t)(c0 + c) * a.N + n0) * ks + 4 * f;
 }
 
+// 1-D grid -> (row block, column tile) with the column tiles of one row block back to back on one XCD
+// (workgroups are dealt to the 8 XCDs round robin): a row block's X rows then come from that XCD's L2 after the
+// first tile instead of from HBM once per column tile.  False for the padding workgroups.
+__device__ __forceinline__ bool cb_tile(int64_t nrb, int ny, int64_t& rb, int& ct) {
+  const int64_t w = blockIdx.x, xcd = w % 8, k = w / 8;
+  ct = (int)(k % ny);
+  rb = (k / ny) * 8 + xcd;
+  return rb < nrb;
+}
+
 // Epilogue shared by the k = 3 / k = 1 kernels: lane (lg, l16), register v -> row wm*64 + i*16 + 4 lg + v,
 // column wn*BN/2 + j*16 + l16; Xs is reused as the SOFTMAX staging buffer.
 template <int BN, bool SOFTMAX>
@@ -155,8 +165,11 @@ __global__ __launch_bounds__(256) void convbig_kernel(ConvArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lg = lane >> 4, l16 = lane & 15;
   const int wm = wave & 1, wn = wave >> 1;
-  const int64_t m0 = (int64_t)blockIdx.x * CB_BM;
-  const int n0 = blockIdx.y * BN;
+  int64_t rb;
+  int ct;
+  if (!cb_tile(cdiv(a.R, CB_BM), (int)cdiv(a.N, BN), rb, ct)) return;
+  const int64_t m0 = rb * CB_BM;
+  const int n0 = ct * BN;
   const int ldx = a.Kc, ks = a.ks, nslice = a.Kc / CB_KC;
   const int wrows = ks * BN * 4;  // valid weight float4s per slice
 
@@ -263,8 +276,11 @@ __global__ __launch_bounds__(256) void convbig1_kernel(ConvArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lg = lane >> 4, l16 = lane & 15;
   const int wm = wave & 1, wn = wave >> 1;
-  const int64_t m0 = (int64_t)blockIdx.x * CB_BM;
-  const int n0 = blockIdx.y * BN;
+  int64_t rb;
+  int ct;
+  if (!cb_tile(cdiv(a.R, CB_BM), (int)cdiv(a.N, BN), rb, ct)) return;
+  const int64_t m0 = rb * CB_BM;
+  const int n0 = ct * BN;
   const int ldx = a.Kc, nstage = a.Kc / (CB_KC * SPS);
 
   float4 px[SPS][C::PX], pw[SPS][C::PW];
@@ -358,7 +374,7 @@ bool convbig_supported(const ConvArgs& a) {
 
 template <int BN, bool SM>
 static int launch_cb(const ConvArgs& a, hipStream_t s) {
-  const dim3 grid((unsigned)cdiv(a.R, CB_BM), (unsigned)cdiv(a.N, BN));
+  const dim3 grid((unsigned)(cdiv(cdiv(a.R, CB_BM), 8) * 8 * cdiv(a.N, BN)));
   if (a.ks == 1 && a.Kc % (CB_KC * ConvBig1Cfg<BN>::SPS) == 0) {
     const size_t lds1 = (size_t)ConvBig1Cfg<BN>::LDS_FLOATS * sizeof(float);
     convbig1_kernel<BN, SM><<<grid, 256, lds1, s>>>(a);
