@@ -139,18 +139,25 @@ __device__ __forceinline__ void cb_epilogue(const ConvArgs& a, f32x4 (&acc)[4][B
           for (int j = 0; j < WN; ++j) Ys[(wm * 64 + i * 16 + 4 * lg + v) * LY + j * 16 + l16] = acc[i][j][v];
     }
     __syncthreads();
-    if (tid < CB_BM) {
+    if (tid < CB_BM) {  // thread per row, q written back over the row in LDS
       const int64_t r = m0 + tid;
       int64_t b;
       int t;
       const bool valid = row_bt_fast(r, a.R, a.T, b, t);
-      const float* y = Ys + tid * LY;
+      float* y = Ys + tid * LY;
       float mx = -__builtin_inff();
       for (int n = 0; n < a.N; ++n) mx = fmaxf(mx, y[n]);
       float se = 0.f;
       for (int n = 0; n < a.N; ++n) se += __expf(y[n] - mx);
-      if (r < a.R)
-        for (int n = 0; n < a.N; ++n) a.q_out[r * ldn + n] = valid ? __expf(y[n] - mx) / se : 0.f;
+      for (int n = 0; n < a.N; ++n) y[n] = valid ? __expf(y[n] - mx) / se : 0.f;
+    }
+    __syncthreads();
+    // the tile's q rows are one contiguous block of BM x N floats: stored by every thread, consecutive threads
+    // on consecutive floats (the thread-per-row stores were 128 B apart per lane)
+    const int64_t nq = std::min<int64_t>(CB_BM, a.R - m0) * a.N;
+    for (int e = tid; e < nq; e += 256) {
+      const int row = e / a.N, n = e - row * a.N;
+      a.q_out[m0 * ldn + e] = Ys[row * LY + n];
     }
   }
 }
