@@ -397,7 +397,7 @@ static int launch_cb(const ConvArgs& a, hipStream_t s) {
 int launch_convbig(const ConvArgs& a, hipStream_t s) {
   if (!convbig_supported(a)) return VQHMM_EUNSUPPORTED;
   if (a.R == 0) return VQHMM_OK;
-  if (a.q_out) return launch_cb<128, true>(a, s);
+  if (a.q_out) return a.N <= 32 ? launch_cb<64, true>(a, s) : launch_cb<128, true>(a, s);  // N <= BN / 2
   return a.N <= 64 ? launch_cb<64, false>(a, s) : launch_cb<128, false>(a, s);
 }
 
