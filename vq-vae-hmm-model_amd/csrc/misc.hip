@@ -269,9 +269,12 @@ __device__ void compose_adam_block(const ComposeAdamArgs& a, int64_t cb, int64_t
     }
     return;
   }
-  const int k = (int)(cb - nw);
+  // one block per (k, 64-wide h chunk): one block per k walked its H / 64 chunks one after another, each a
+  // chain of dependent load batches (cfg3: 32 blocks x 4 chunks, most of the 149 us launch)
+  const int nh = (int)cdiv(H, 64);
+  const int k = (int)((cb - nw) / nh), h0 = (int)((cb - nw) % nh) * 64;
   const int grp = threadIdx.x >> 6;
-  for (int h0 = 0; h0 < H; h0 += 64) {
+  {
     const int h = h0 + (threadIdx.x & 63);
     float sacc = 0.f;
     if (h < H)
@@ -386,7 +389,7 @@ int launch_tail(TailArgs& ta, const AdamArgs* adam, const float* g, hipStream_t 
 int launch_grad_tail(TailArgs& a, hipStream_t s) { return launch_tail(a, nullptr, nullptr, s); }
 
 int launch_compose_adam(const ComposeAdamArgs& a, hipStream_t s) {
-  const int64_t nb = cdiv(a.n, 256) + cdiv((int64_t)a.H * a.H * 3, 256) + a.K;
+  const int64_t nb = cdiv(a.n, 256) + cdiv((int64_t)a.H * a.H * 3, 256) + (int64_t)a.K * cdiv(a.H, 64);
   compose_adam_kernel<<<(unsigned)nb, 256, 0, s>>>(a);
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
