@@ -398,6 +398,7 @@ int launch_convbig(const ConvArgs& a, hipStream_t s) {
   if (!convbig_supported(a)) return VQHMM_EUNSUPPORTED;
   if (a.R == 0) return VQHMM_OK;
   if (a.q_out) return a.N <= 32 ? launch_cb<64, true>(a, s) : launch_cb<128, true>(a, s);  // N <= BN / 2
+  if (a.N <= 32) return launch_cb<32, false>(a, s);  // e.g. the dgrad of dec_conv1 into K = 32 states
   return a.N <= 64 ? launch_cb<64, false>(a, s) : launch_cb<128, false>(a, s);
 }
 
