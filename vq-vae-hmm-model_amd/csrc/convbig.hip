@@ -411,91 +411,92 @@ int launch_convbig(const ConvArgs& a, hipStream_t s) {
 // in flight in registers; operands are b32 reads with row strides = 16 (mod 64) floats (the four 16-lane groups
 // read rows 4 apart in disjoint banks).
 namespace {
-constexpr int WB_TN = 128, WB_TC = 64, WB_RT = 64;
-constexpr int WB_LDA = WB_TN + 16, WB_LDB = WB_TC + 16;
-constexpr int WB_DY4 = WB_RT * WB_TN / 4, WB_X4 = (WB_RT + 2) * WB_TC / 4;
-constexpr int WB_PD = WB_DY4 / 256, WB_PX = (WB_X4 + 255) / 256;
+constexpr int WB_TN = 128, WB_TC = 64, WB_RT = 64;  // the default tile (the kernel's MI = 4, NJ = 2)
 }  // namespace
 
-template <int KS>
+template <int KS, int MI, int NJ>
 __global__ __launch_bounds__(256) void wgradbig_kernel(WgradArgs a) {
-  __shared__ float dys[WB_RT * WB_LDA];
-  __shared__ float xs[(WB_RT + 2) * WB_LDB];
+  // TN = 32 MI outputs x TC = 32 NJ inputs per workgroup (128 x 64 by default; narrower for N or C <= 32, where
+  // the default tile was 1/2 to 3/4 empty): each wave 16 MI x 16 NJ of them
+  constexpr int TN = 32 * MI, TC = 32 * NJ, LDA = TN + 16, LDB = TC + 16;  // strides = 16 (mod 64)
+  constexpr int DY4 = WB_RT * TN / 4, X4 = (WB_RT + 2) * TC / 4, PD = DY4 / 256, PX = (X4 + 255) / 256;
+  __shared__ float dys[WB_RT * LDA];
+  __shared__ float xs[(WB_RT + 2) * LDB];
   __shared__ float bred[256];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lg = lane >> 4, l16 = lane & 15;
   const int wm = wave & 1, wn = wave >> 1;
-  const int ntc = (int)cdiv(a.C, WB_TC);
-  const int n0 = (blockIdx.x / ntc) * WB_TN, c0 = (blockIdx.x % ntc) * WB_TC;
+  const int ntc = (int)cdiv(a.C, TC);
+  const int n0 = (blockIdx.x / ntc) * TN, c0 = (blockIdx.x % ntc) * TC;
   const int64_t chunk = blockIdx.y;
   const int64_t rbeg = chunk * a.rows_per_chunk, rend = min(a.R, rbeg + a.rows_per_chunk);
   const int ldn = ld4(a.N), ldc = ld4(a.C);
   const bool do_bias = a.bias_slab && c0 == 0;
 
-  float4 pd[WB_PD], px[WB_PX];
+  float4 pd[PD], px[PX];
   auto load = [&](int64_t r0) {
 #pragma unroll
-    for (int k = 0; k < WB_PD; ++k) {
-      const int i = tid + 256 * k, row = i / (WB_TN / 4), n = n0 + (i - row * (WB_TN / 4)) * 4;
+    for (int k = 0; k < PD; ++k) {
+      const int i = tid + 256 * k, row = i / (TN / 4), n = n0 + (i - row * (TN / 4)) * 4;
       const int64_t r = r0 + row;
       pd[k] = (r < rend && n < ldn) ? *reinterpret_cast<const float4*>(a.dy + r * ldn + n) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
-    for (int k = 0; k < WB_PX; ++k) {
-      const int i = tid + 256 * k, row = i / (WB_TC / 4), c = c0 + (i - row * (WB_TC / 4)) * 4;
+    for (int k = 0; k < PX; ++k) {
+      const int i = tid + 256 * k, row = i / (TC / 4), c = c0 + (i - row * (TC / 4)) * 4;
       const int64_t r = r0 - 1 + row;
-      px[k] = (i < WB_X4 && r >= 0 && r < a.R && c < ldc) ? *reinterpret_cast<const float4*>(a.x + r * ldc + c)
+      px[k] = (i < X4 && r >= 0 && r < a.R && c < ldc) ? *reinterpret_cast<const float4*>(a.x + r * ldc + c)
                                                            : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
-  f32x4 acc[KS][4][2];
+  f32x4 acc[KS][MI][NJ];
 #pragma unroll
   for (int tp = 0; tp < KS; ++tp)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[tp][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < NJ; ++j) acc[tp][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float bacc = 0.f;
 
   load(rbeg);
   for (int64_t r0 = rbeg; r0 < rend; r0 += WB_RT) {
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < WB_PD; ++k) {
-      const int i = tid + 256 * k, row = i / (WB_TN / 4), n = (i - row * (WB_TN / 4)) * 4;
-      *reinterpret_cast<float4*>(dys + row * WB_LDA + n) = pd[k];
+    for (int k = 0; k < PD; ++k) {
+      const int i = tid + 256 * k, row = i / (TN / 4), n = (i - row * (TN / 4)) * 4;
+      *reinterpret_cast<float4*>(dys + row * LDA + n) = pd[k];
     }
 #pragma unroll
-    for (int k = 0; k < WB_PX; ++k) {
-      const int i = tid + 256 * k, row = i / (WB_TC / 4), c = (i - row * (WB_TC / 4)) * 4;
-      if (i < WB_X4) *reinterpret_cast<float4*>(xs + row * WB_LDB + c) = px[k];
+    for (int k = 0; k < PX; ++k) {
+      const int i = tid + 256 * k, row = i / (TC / 4), c = (i - row * (TC / 4)) * 4;
+      if (i < X4) *reinterpret_cast<float4*>(xs + row * LDB + c) = px[k];
     }
     __syncthreads();
     if (r0 + WB_RT < rend) load(r0 + WB_RT);
-    if (do_bias && tid < WB_TN) {
+    if (do_bias && tid < TN) {
       float bp[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) bp[k] = 0.f;
 #pragma unroll
-      for (int row = 0; row < WB_RT; ++row) bp[row & 7] += dys[row * WB_LDA + tid];
+      for (int row = 0; row < WB_RT; ++row) bp[row & 7] += dys[row * LDA + tid];
       bacc += ((bp[0] + bp[1]) + (bp[2] + bp[3])) + ((bp[4] + bp[5]) + (bp[6] + bp[7]));
     }
 #pragma unroll 4
     for (int st = 0; st < WB_RT / 4; ++st) {
       const int rr = 4 * st + lg;  // this lane group's row of the k-step
-      float av[4], bv[KS][2];
+      float av[MI], bv[KS][NJ];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) av[i] = dys[rr * WB_LDA + wm * 64 + i * 16 + l16];
-#pragma unroll
-      for (int tp = 0; tp < KS; ++tp)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) bv[tp][j] = xs[(rr + (KS == 3 ? tp : 1)) * WB_LDB + wn * 32 + j * 16 + l16];
+      for (int i = 0; i < MI; ++i) av[i] = dys[rr * LDA + wm * (TN / 2) + i * 16 + l16];
 #pragma unroll
       for (int tp = 0; tp < KS; ++tp)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < NJ; ++j) bv[tp][j] = xs[(rr + (KS == 3 ? tp : 1)) * LDB + wn * (TC / 2) + j * 16 + l16];
 #pragma unroll
-          for (int j = 0; j < 2; ++j) acc[tp][i][j] = mfma16x16x4(av[i], bv[tp][j], acc[tp][i][j]);
+      for (int tp = 0; tp < KS; ++tp)
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) acc[tp][i][j] = mfma16x16x4(av[i], bv[tp][j], acc[tp][i][j]);
     }
   }
   // ---- this chunk's partial: slab[chunk][n][c][tap]; lane (lg, l16), reg v -> n row 4 lg + v, c column l16
@@ -503,15 +504,15 @@ __global__ __launch_bounds__(256) void wgradbig_kernel(WgradArgs a) {
 #pragma unroll
   for (int tp = 0; tp < KS; ++tp)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < NJ; ++j)
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-          const int n = n0 + wm * 64 + i * 16 + 4 * lg + v, c = c0 + wn * 32 + j * 16 + l16;
+          const int n = n0 + wm * (TN / 2) + i * 16 + 4 * lg + v, c = c0 + wn * (TC / 2) + j * 16 + l16;
           if (n < a.N && c < a.C) out[((int64_t)n * a.C + c) * KS + tp] = acc[tp][i][j][v];
         }
-  if (do_bias && tid < WB_TN && n0 + tid < a.N) a.bias_slab[chunk * a.N + n0 + tid] = bacc;
+  if (do_bias && tid < TN && n0 + tid < a.N) a.bias_slab[chunk * a.N + n0 + tid] = bacc;
   (void)bred;
 }
 
@@ -532,8 +533,17 @@ int launch_wgradbig(const WgradArgs& a, hipStream_t s) {
   if (!wgradbig_supported(a)) return VQHMM_EUNSUPPORTED;
   if (a.R == 0) return VQHMM_OK;
   const dim3 grid((unsigned)(cdiv(a.N, WB_TN) * cdiv(a.C, WB_TC)), (unsigned)cdiv(a.R, a.rows_per_chunk));
-  if (a.ks == 3) wgradbig_kernel<3><<<grid, 256, 0, s>>>(a);
-  else wgradbig_kernel<1><<<grid, 256, 0, s>>>(a);
+  // narrower tiles only where they keep the default tile count (wgradbig_rows' chunking and the slabs)
+  const int mi = a.N <= 32 ? 1 : 4, nj = a.C <= 32 ? 1 : 2;
+  if (a.ks == 3) {
+    if (mi == 4 && nj == 1) wgradbig_kernel<3, 4, 1><<<grid, 256, 0, s>>>(a);
+    else if (mi == 1 && nj == 2) wgradbig_kernel<3, 1, 2><<<grid, 256, 0, s>>>(a);
+    else wgradbig_kernel<3, 4, 2><<<grid, 256, 0, s>>>(a);
+  } else {
+    if (mi == 4 && nj == 1) wgradbig_kernel<1, 4, 1><<<grid, 256, 0, s>>>(a);
+    else if (mi == 1 && nj == 2) wgradbig_kernel<1, 1, 2><<<grid, 256, 0, s>>>(a);
+    else wgradbig_kernel<1, 4, 2><<<grid, 256, 0, s>>>(a);
+  }
   VQHMM_LAUNCH_CHECK();
   return VQHMM_OK;
 }
