@@ -399,6 +399,9 @@ int launch_convbig(const ConvArgs& a, hipStream_t s) {
   if (a.R == 0) return VQHMM_OK;
   if (a.q_out) return a.N <= 32 ? launch_cb<64, true>(a, s) : launch_cb<128, true>(a, s);  // N <= BN / 2
   if (a.N <= 32) return launch_cb<32, false>(a, s);  // e.g. the dgrad of dec_conv1 into K = 32 states
+  // short 1x1 reductions (<= 4 stages): more, smaller workgroups per CU to overlap their load / epilogue latency
+  // (cfg3 to_params dgrad 459 -> 435 us, to_logits dgrad 151 -> 142)
+  if (a.ks == 1 && a.Kc <= 128 && a.N <= 256) return launch_cb<64, false>(a, s);
   return a.N <= 64 ? launch_cb<64, false>(a, s) : launch_cb<128, false>(a, s);
 }
 
