@@ -402,6 +402,9 @@ int launch_convbig(const ConvArgs& a, hipStream_t s) {
   // short 1x1 reductions (<= 4 stages): more, smaller workgroups per CU to overlap their load / epilogue latency
   // (cfg3 to_params dgrad 459 -> 435 us, to_logits dgrad 151 -> 142)
   if (a.ks == 1 && a.Kc <= 128 && a.N <= 256) return launch_cb<64, false>(a, s);
+  // k = 3 into <= 128 channels: two 64-column tiles (100 VGPRs, more waves per SIMD) beat one 128-column tile
+  // (145 VGPRs) despite reading X twice (cfg3 enc_conv2 + to_logits 1036 -> 996 us)
+  if (a.ks == 3 && a.N <= 128) return launch_cb<64, false>(a, s);
   return a.N <= 64 ? launch_cb<64, false>(a, s) : launch_cb<128, false>(a, s);
 }
 
