@@ -399,13 +399,10 @@ int launch_convbig(const ConvArgs& a, hipStream_t s) {
   if (a.R == 0) return VQHMM_OK;
   if (a.q_out) return a.N <= 32 ? launch_cb<64, true>(a, s) : launch_cb<128, true>(a, s);  // N <= BN / 2
   if (a.N <= 32) return launch_cb<32, false>(a, s);  // e.g. the dgrad of dec_conv1 into K = 32 states
-  // short 1x1 reductions (<= 4 stages): more, smaller workgroups per CU to overlap their load / epilogue latency
-  // (cfg3 to_params dgrad 459 -> 435 us, to_logits dgrad 151 -> 142)
-  if (a.ks == 1 && a.Kc <= 128 && a.N <= 256) return launch_cb<64, false>(a, s);
-  // k = 3 into <= 128 channels: two 64-column tiles (100 VGPRs, more waves per SIMD) beat one 128-column tile
-  // (145 VGPRs) despite reading X twice (cfg3 enc_conv2 + to_logits 1036 -> 996 us)
-  if (a.ks == 3 && a.N <= 128) return launch_cb<64, false>(a, s);
-  return a.N <= 64 ? launch_cb<64, false>(a, s) : launch_cb<128, false>(a, s);
+  // 64-column tiles for every wider layer: ~100 VGPRs against 145 for 128 columns, so more waves per SIMD; that
+  // outweighs X being read once per 64 output columns instead of once per 128 (cfg3, one box: k = 3 layers
+  // 16.19 -> 15.70 ms; k = 1 layers neutral, 15.70 -> 15.69)
+  return launch_cb<64, false>(a, s);
 }
 
 
